@@ -1,0 +1,29 @@
+"""MI355X-native (gfx950) batched bijector path of bat/EuclidianNormalizingFlows.jl.
+
+Python host mirror of the reference's transform API (the reference host language, Julia, is not
+installed in this image; the Julia ccall shim that binds the same C ABI is julia/ENFHip.jl).
+All compute goes through libenf.so (include/enf.h): hand-written HIP kernels for gfx950.
+"""
+from ._lib import EnfError, version  # noqa: F401
+from .trafos import (  # noqa: F401
+    CenterContract,
+    CenterStretch,
+    ComposedFunction,
+    DimensionMismatch,
+    HouseholderTrafo,
+    JohnsonTrafo,
+    JohnsonTrafoInv,
+    MethodError,
+    ScaleShiftTrafo,
+    Trafo,
+    compose,
+    inverse,
+    leaves,
+    with_logabsdet_jacobian,
+)
+
+__all__ = [
+    "ScaleShiftTrafo", "CenterStretch", "CenterContract", "JohnsonTrafo", "JohnsonTrafoInv",
+    "HouseholderTrafo", "ComposedFunction", "compose", "inverse", "with_logabsdet_jacobian",
+    "leaves", "Trafo", "MethodError", "DimensionMismatch", "EnfError", "version",
+]

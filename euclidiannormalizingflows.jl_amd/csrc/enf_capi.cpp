@@ -1,0 +1,393 @@
+// enf_capi.cpp -- the C ABI of libenf.so (include/enf.h): argument validation, flattening of a
+// composed flow into launch-sized step programs, device bookkeeping, error reporting, RCCL.
+// No C++ exception crosses the ABI: every entry point catches everything.
+#include "enf.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "enf_internal.h"
+#include "enf_train.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+enf_status fail(enf_status st, const std::string& msg) {
+  g_last_error = msg;
+  return st;
+}
+
+enf_status hip_fail(hipError_t e, const char* what) {
+  return fail(ENF_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define ENF_TRY try {
+#define ENF_CATCH                                                   \
+  }                                                                 \
+  catch (const std::exception& ex) {                                \
+    return fail(ENF_ERR_INVALID, std::string("exception: ") + ex.what()); \
+  }                                                                 \
+  catch (...) {                                                     \
+    return fail(ENF_ERR_INVALID, "unknown exception");              \
+  }
+
+std::mutex g_dev_mu;
+std::vector<enf::DeviceInfo> g_dev;
+
+enf_status device_info(enf::DeviceInfo* out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  if ((int)g_dev.size() <= dev) g_dev.resize(dev + 1);
+  if (g_dev[dev].num_cu == 0) {
+    int n = 0;
+    e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return hip_fail(e, "hipDeviceGetAttribute");
+    g_dev[dev].num_cu = n > 0 ? n : 1;
+  }
+  *out = g_dev[dev];
+  return ENF_OK;
+}
+
+int nparams_of(int op) {
+  switch (op) {
+    case ENF_OP_SCALESHIFT: return 2;
+    case ENF_OP_CENTER_STRETCH:
+    case ENF_OP_CENTER_CONTRACT: return 3;
+    case ENF_OP_JOHNSON:
+    case ENF_OP_JOHNSON_INV: return 4;
+    case ENF_OP_HOUSEHOLDER: return 1;
+    default: return -1;
+  }
+}
+
+enf_status validate_layers(int64_t D, const enf_layer* layers, int32_t nlayers) {
+  if (nlayers < 0) return fail(ENF_ERR_INVALID, "nlayers < 0");
+  if (nlayers > 0 && !layers) return fail(ENF_ERR_INVALID, "layers is NULL");
+  for (int32_t l = 0; l < nlayers; ++l) {
+    const int np = nparams_of(layers[l].op);
+    if (np < 0) return fail(ENF_ERR_INVALID, "layer " + std::to_string(l) + ": unknown op " + std::to_string(layers[l].op));
+    if (layers[l].op == ENF_OP_HOUSEHOLDER && layers[l].k < 1)
+      return fail(ENF_ERR_INVALID, "layer " + std::to_string(l) + ": HouseholderTrafo needs k >= 1 columns");
+    if (D > 0)
+      for (int q = 0; q < np; ++q)
+        if (!layers[l].p[q])
+          return fail(ENF_ERR_INVALID, "layer " + std::to_string(l) + ": parameter " + std::to_string(q) + " is NULL");
+  }
+  return ENF_OK;
+}
+
+}  // namespace
+
+namespace enf {
+// shared with enf_train.hip
+enf_status set_error(enf_status st, const char* msg) { return fail(st, msg); }
+enf_status current_device_info(DeviceInfo* out) { return device_info(out); }
+}  // namespace enf
+
+extern "C" {
+
+const char* enf_version(void) {
+  static char buf[64];
+  std::snprintf(buf, sizeof buf, "%d.%d.%d gfx950", ENF_VERSION_MAJOR, ENF_VERSION_MINOR, ENF_VERSION_PATCH);
+  return buf;
+}
+
+const char* enf_last_error(void) { return g_last_error.c_str(); }
+
+enf_status enf_device_count(int32_t* count) {
+  ENF_TRY
+  if (!count) return fail(ENF_ERR_INVALID, "count is NULL");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+  *count = n;
+  return ENF_OK;
+  ENF_CATCH
+}
+
+enf_status enf_set_device(int32_t device) {
+  ENF_TRY
+  hipError_t e = hipSetDevice(device);
+  return e == hipSuccess ? ENF_OK : hip_fail(e, "hipSetDevice");
+  ENF_CATCH
+}
+
+enf_status enf_get_device(int32_t* device) {
+  ENF_TRY
+  if (!device) return fail(ENF_ERR_INVALID, "device is NULL");
+  int d = 0;
+  hipError_t e = hipGetDevice(&d);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  *device = d;
+  return ENF_OK;
+  ENF_CATCH
+}
+
+enf_status enf_malloc(void** ptr, size_t bytes) {
+  ENF_TRY
+  if (!ptr) return fail(ENF_ERR_INVALID, "ptr is NULL");
+  hipError_t e = hipMalloc(ptr, bytes);
+  return e == hipSuccess ? ENF_OK : hip_fail(e, "hipMalloc");
+  ENF_CATCH
+}
+
+enf_status enf_free(void* ptr) {
+  ENF_TRY
+  hipError_t e = hipFree(ptr);
+  return e == hipSuccess ? ENF_OK : hip_fail(e, "hipFree");
+  ENF_CATCH
+}
+
+enf_status enf_memcpy(void* dst, const void* src, size_t bytes, int32_t kind, void* hip_stream) {
+  ENF_TRY
+  if (bytes == 0) return ENF_OK;
+  if (!dst || !src) return fail(ENF_ERR_INVALID, "memcpy: NULL pointer");
+  hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
+                  : kind == 1 ? hipMemcpyDeviceToHost
+                  : kind == 2 ? hipMemcpyDeviceToDevice : hipMemcpyDefault;
+  hipError_t e = hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)hip_stream);
+  return e == hipSuccess ? ENF_OK : hip_fail(e, "hipMemcpyAsync");
+  ENF_CATCH
+}
+
+enf_status enf_stream_synchronize(void* hip_stream) {
+  ENF_TRY
+  hipError_t e = hipStreamSynchronize((hipStream_t)hip_stream);
+  return e == hipSuccess ? ENF_OK : hip_fail(e, "hipStreamSynchronize");
+  ENF_CATCH
+}
+
+enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx, void* Y,
+                          int64_t ldy, void* ladj, int32_t accumulate_ladj, const enf_layer* layers,
+                          int32_t nlayers, void* hip_stream) {
+  ENF_TRY
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "dtype must be ENF_F32 or ENF_F64");
+  if (D < 0 || N < 0) return fail(ENF_ERR_INVALID, "D and N must be >= 0");
+  if (D > (int64_t)1 << 30) return fail(ENF_ERR_UNSUPPORTED, "D too large");
+  if (ldx < (D > 0 ? D : 1) || ldy < (D > 0 ? D : 1)) return fail(ENF_ERR_INVALID, "leading dimension < D");
+  enf_status vs = validate_layers(D, layers, nlayers);
+  if (vs != ENF_OK) return vs;
+  if (N == 0) return ENF_OK;
+  if (D > 0 && (!X || !Y)) return fail(ENF_ERR_INVALID, "X or Y is NULL");
+  const size_t elem = dtype == ENF_F64 ? 8 : 4;
+  hipStream_t st = (hipStream_t)hip_stream;
+  if (D > 0 && X != Y) {  // partial overlap of X and Y is not supported (exact aliasing is)
+    const char* xb = (const char*)X;
+    const char* yb = (const char*)Y;
+    const char* xe = xb + ((N - 1) * ldx + D) * elem;
+    const char* ye = yb + ((N - 1) * ldy + D) * elem;
+    if (xb < ye && yb < xe) return fail(ENF_ERR_INVALID, "X and Y overlap without being identical");
+  } else if (D > 0 && ldx != ldy) {
+    return fail(ENF_ERR_INVALID, "in-place call (X == Y) needs ldx == ldy");
+  }
+
+  // empty flow or empty samples: Y = X, ladj = 0 (ChangesOfVariables: identity has ladj 0)
+  if (D == 0 || nlayers == 0) {
+    if (D > 0 && X != Y) {
+      hipError_t e = hipMemcpy2DAsync(Y, ldy * elem, X, ldx * elem, D * elem, N, hipMemcpyDeviceToDevice, st);
+      if (e != hipSuccess) return hip_fail(e, "hipMemcpy2DAsync");
+    }
+    if (ladj && !accumulate_ladj) {
+      hipError_t e = hipMemsetAsync(ladj, 0, N * elem, st);
+      if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    }
+    return ENF_OK;
+  }
+
+  enf::DeviceInfo dev;
+  enf_status ds = device_info(&dev);
+  if (ds != ENF_OK) return ds;
+
+  // flatten into steps: one per transform, one per Householder reflection column
+  struct S { int32_t op, layer, col; };
+  std::vector<S> steps;
+  for (int32_t l = 0; l < nlayers; ++l) {
+    if (layers[l].op == ENF_OP_HOUSEHOLDER)
+      for (int32_t c = 0; c < layers[l].k; ++c) steps.push_back({layers[l].op, l, c});
+    else
+      steps.push_back({layers[l].op, l, 0});
+  }
+
+  // cut into launches bounded by the kernarg tables and the LDS parameter budget
+  size_t i = 0;
+  bool first = true;
+  while (i < steps.size()) {
+    enf::FlowArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.D = (int32_t)D;
+    a.N = N;
+    size_t recs = 0;
+    int last_layer = -1;
+    while (i < steps.size() && a.nsteps < enf::kMaxSteps) {
+      const S& s = steps[i];
+      const size_t w = (size_t)enf::record_width_host(s.op) * (size_t)D * elem;
+      const bool new_layer = s.layer != last_layer;
+      if (new_layer && a.nlayers >= enf::kMaxLayers) break;
+      if (recs + w > enf::kLdsParamBudget) {
+        if (a.nsteps == 0)
+          return fail(ENF_ERR_UNSUPPORTED, "D too large: one transform's parameter records exceed the LDS budget");
+        break;
+      }
+      if (new_layer) {
+        enf::LayerDesc& L = a.layers[a.nlayers++];
+        L.op = layers[s.layer].op;
+        L.k = layers[s.layer].k;
+        for (int q = 0; q < 4; ++q) L.p[q] = layers[s.layer].p[q];
+        last_layer = s.layer;
+      }
+      enf::Step& t = a.steps[a.nsteps++];
+      t.op = s.op;
+      t.layer = a.nlayers - 1;
+      t.col = s.col;
+      t.off = (int32_t)(recs / elem);
+      recs += w;
+      ++i;
+    }
+    a.X = first ? X : Y;
+    a.ldx = first ? ldx : ldy;
+    a.Y = Y;
+    a.ldy = ldy;
+    a.ladj = ladj;
+    a.accumulate = first ? accumulate_ladj : 1;
+    hipError_t e = enf::launch_flow(a, dtype == ENF_F64, st, dev);
+    if (e != hipSuccess) return hip_fail(e, "flow kernel launch");
+    first = false;
+  }
+  return ENF_OK;
+  ENF_CATCH
+}
+
+enf_status enf_flow_param_count(int64_t D, const enf_layer* layers, int32_t nlayers, int64_t* count) {
+  ENF_TRY
+  if (!count) return fail(ENF_ERR_INVALID, "count is NULL");
+  if (D < 0) return fail(ENF_ERR_INVALID, "D < 0");
+  enf_status vs = validate_layers(D, layers, nlayers);
+  if (vs != ENF_OK) return vs;
+  int64_t n = 0;
+  for (int32_t l = 0; l < nlayers; ++l)
+    n += D * (layers[l].op == ENF_OP_HOUSEHOLDER ? layers[l].k : nparams_of(layers[l].op));
+  *count = n;
+  return ENF_OK;
+  ENF_CATCH
+}
+
+enf_status enf_flow_negll_grad_workspace(enf_dtype dtype, int64_t D, int64_t N, const enf_layer* layers,
+                                         int32_t nlayers, size_t* bytes) {
+  ENF_TRY
+  if (!bytes) return fail(ENF_ERR_INVALID, "bytes is NULL");
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
+  if (D < 0 || N < 0) return fail(ENF_ERR_INVALID, "D and N must be >= 0");
+  enf_status vs = validate_layers(D, layers, nlayers);
+  if (vs != ENF_OK) return vs;
+  return enf::negll_grad_workspace(dtype == ENF_F64, D, N, layers, nlayers, bytes);
+  ENF_CATCH
+}
+
+enf_status enf_flow_negll_grad(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
+                               const enf_layer* layers, int32_t nlayers, void* out, void* workspace,
+                               size_t workspace_bytes, void* hip_stream) {
+  ENF_TRY
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
+  if (D < 0 || N < 0) return fail(ENF_ERR_INVALID, "D and N must be >= 0");
+  if (ldx < (D > 0 ? D : 1)) return fail(ENF_ERR_INVALID, "ldx < D");
+  enf_status vs = validate_layers(D, layers, nlayers);
+  if (vs != ENF_OK) return vs;
+  if (!out) return fail(ENF_ERR_INVALID, "out is NULL");
+  if (N == 0) return ENF_OK;
+  if (D > 0 && !X) return fail(ENF_ERR_INVALID, "X is NULL");
+  return enf::negll_grad(dtype == ENF_F64, D, N, X, ldx, layers, nlayers, out, workspace, workspace_bytes,
+                         (hipStream_t)hip_stream);
+  ENF_CATCH
+}
+
+enf_status enf_adagrad_step(enf_dtype dtype, int64_t count, void* params, void* acc, const void* grad,
+                            double grad_scale, double eta, double epsilon, void* hip_stream) {
+  ENF_TRY
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
+  if (count < 0) return fail(ENF_ERR_INVALID, "count < 0");
+  if (count == 0) return ENF_OK;
+  if (!params || !acc || !grad) return fail(ENF_ERR_INVALID, "NULL pointer");
+  return enf::adagrad_step(dtype == ENF_F64, count, params, acc, grad, grad_scale, eta, epsilon,
+                           (hipStream_t)hip_stream);
+  ENF_CATCH
+}
+
+enf_status enf_householder_normalize(enf_dtype dtype, int64_t D, int64_t k, void* V, void* hip_stream) {
+  ENF_TRY
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
+  if (D < 0 || k < 0) return fail(ENF_ERR_INVALID, "D and k must be >= 0");
+  if (D == 0 || k == 0) return ENF_OK;
+  if (!V) return fail(ENF_ERR_INVALID, "V is NULL");
+  return enf::householder_normalize(dtype == ENF_F64, D, k, V, (hipStream_t)hip_stream);
+  ENF_CATCH
+}
+
+// ---------------------------------------------------------------------------------- RCCL ----
+struct enf_comm_s {
+  ncclComm_t comm;
+};
+
+static_assert(sizeof(ncclUniqueId) == ENF_UNIQUE_ID_BYTES, "ncclUniqueId size");
+
+enf_status enf_comm_unique_id(uint8_t id[ENF_UNIQUE_ID_BYTES]) {
+  ENF_TRY
+  if (!id) return fail(ENF_ERR_INVALID, "id is NULL");
+  ncclUniqueId u;
+  ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) return fail(ENF_ERR_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  std::memcpy(id, &u, sizeof u);
+  return ENF_OK;
+  ENF_CATCH
+}
+
+enf_status enf_comm_init(enf_comm* comm, int32_t nranks, const uint8_t id[ENF_UNIQUE_ID_BYTES], int32_t rank) {
+  ENF_TRY
+  if (!comm || !id) return fail(ENF_ERR_INVALID, "NULL pointer");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(ENF_ERR_INVALID, "bad rank / nranks");
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof u);
+  auto* c = new enf_comm_s;
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return fail(ENF_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  *comm = c;
+  return ENF_OK;
+  ENF_CATCH
+}
+
+enf_status enf_comm_destroy(enf_comm comm) {
+  ENF_TRY
+  if (!comm) return ENF_OK;
+  ncclResult_t r = ncclCommDestroy(comm->comm);
+  delete comm;
+  if (r != ncclSuccess) return fail(ENF_ERR_RCCL, std::string("ncclCommDestroy: ") + ncclGetErrorString(r));
+  return ENF_OK;
+  ENF_CATCH
+}
+
+enf_status enf_allreduce_sum(enf_comm comm, void* buf, int64_t count, enf_dtype dtype, void* hip_stream) {
+  ENF_TRY
+  if (!comm) return fail(ENF_ERR_INVALID, "comm is NULL");
+  if (count < 0) return fail(ENF_ERR_INVALID, "count < 0");
+  if (count == 0) return ENF_OK;
+  if (!buf) return fail(ENF_ERR_INVALID, "buf is NULL");
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
+  ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, dtype == ENF_F64 ? ncclFloat64 : ncclFloat32, ncclSum,
+                                 comm->comm, (hipStream_t)hip_stream);
+  if (r != ncclSuccess) return fail(ENF_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  return ENF_OK;
+  ENF_CATCH
+}
+
+}  // extern "C"

@@ -1,0 +1,699 @@
+// enf_flow.hip -- gfx950 kernels for the batched forward / inverse + log|det J| path of
+// bat/EuclidianNormalizingFlows.jl (v0.1.0).
+//
+// One launch applies a whole composed flow (Julia `f_n o ... o f_1`) to a column-major D x N
+// batch: X is read from HBM once, every layer runs on registers, Y and the per-sample ladj are
+// written once ((2D+1)*sizeof(T) algorithmic bytes per sample).
+//
+// Data layout ("fragment" layout, fast path). A lane owns 16-byte fragments: V = 16/sizeof(T)
+// consecutive rows of one column (D >= V), or V/D whole columns (D < V). One wave-instruction
+// loads/stores 64 fragments = 1 KiB of contiguous HBM, fully coalesced; a wave tile is U such
+// instructions. The G = D/V lanes that share a column are adjacent, so the Householder dot
+// product v'x (src/householder_trafo.jl:4,9) is a per-lane partial sum plus log2(G) DPP
+// cross-lane adds (quad_perm / row_half_mirror / row_mirror), and the ladj column sum
+// (sum_ladjs, src/abstract_trafo.jl:9) is one such reduction per column at the end.
+//
+// Program. The host flattens the composition into "steps" (one per transform; one per
+// reflection of a chained HouseholderTrafo, src/householder_trafo.jl:71-78) and passes the
+// step table in the kernarg segment, so the per-step dispatch is a uniform scalar branch.
+// Each block's prologue derives per-row parameter records (1/lambda, delta*ln2, normalised
+// reflection vectors, exp(b*a) ...) from the raw device parameter vectors into LDS, plus the
+// constant part of the ladj (sum log|delta/lambda|, sum log|a|) in double precision.
+//
+// Arithmetic. fp64 follows the reference formulas with ocml's accurate double functions.
+// fp32 uses the hardware transcendental unit (v_log_f32 / v_exp_f32 / v_sqrt_f32 / v_rcp_f32,
+// each <= 1.4 ulp, measured on MI355X: profiles/r01_microbench.txt) with log2-domain
+// constants folded into the parameter records; errors are normwise few-ulp.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <type_traits>
+
+#include "enf_internal.h"
+
+namespace enf {
+
+// ------------------------------------------------------------------------------------------
+// device math
+// ------------------------------------------------------------------------------------------
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr double kLn2 = 0.69314718055994530942;
+constexpr double kLog2e = 1.44269504088896340736;
+
+__device__ __forceinline__ float hw_log2(float x) { return __builtin_amdgcn_logf(x); }
+__device__ __forceinline__ float hw_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float hw_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float hw_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// DPP cross-lane sum over aligned groups of G lanes (G <= 64, power of two). All 64 lanes must
+// be active. quad_perm(1,0,3,2) = 0xB1, quad_perm(2,3,0,1) = 0x4E, row_half_mirror = 0x141,
+// row_mirror = 0x140: after the quad steps every lane of a quad holds the quad sum, so a
+// mirror partner always lies in the other quad / half-row.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL,
+                                                               0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <int CTRL, typename T>
+__device__ __forceinline__ T dpp(T x) {
+  if constexpr (std::is_same_v<T, float>) return dpp_f<CTRL>(x);
+  else return dpp_d<CTRL>(x);
+}
+template <int G, typename T>
+__device__ __forceinline__ T group_sum(T x) {
+  if constexpr (G >= 2) x += dpp<0xB1>(x);
+  if constexpr (G >= 4) x += dpp<0x4E>(x);
+  if constexpr (G >= 8) x += dpp<0x141>(x);
+  if constexpr (G >= 16) x += dpp<0x140>(x);
+  if constexpr (G >= 32) x += __shfl_xor(x, 16);
+  if constexpr (G >= 64) x += __shfl_xor(x, 32);
+  return x;
+}
+
+// ------------------------------------------------------------------------------------------
+// parameter records in LDS: record width W(op) values of T per row, rows contiguous
+// ------------------------------------------------------------------------------------------
+//  fp32                                              fp64
+//  HOUSEHOLDER  W=1 {v_d * sqrt(2/v'v)}              same
+//  SCALESHIFT   W=2 {a, b}                           same
+//  JOHNSON      W=4 {gamma, delta*ln2, xi, 1/lambda} {gamma, delta, xi, lambda}
+//  JOHNSON_INV  W=4 {gamma, 1/delta, xi, lambda}     {gamma, delta, xi, lambda}
+//  CENTER_*     W=8 {b*log2e, c, ln2/b, exp(b*a),    {a, b, c, 0, ...}
+//                    exp(2*b*a), b*a*log2e, a, b}
+
+// Per-step constant ladj contribution (natural log units), over all D rows; computed in double.
+// Block prologue: one wave per step, rows over lanes, shuffle reduction.
+template <typename T, int DC>
+__device__ void build_program(const FlowArgs& a, T* __restrict__ rec, double* __restrict__ stepc,
+                              double* __restrict__ ctot) {
+  const int D = DC > 0 ? DC : a.D;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int s = wave; s < a.nsteps; s += nw) {
+    const Step st = a.steps[s];
+    const LayerDesc& L = a.layers[st.layer];
+    T* r = rec + st.off;
+    double part = 0.0;
+    for (int d = lane; d < D; d += 64) {
+      if (st.op == OP_HOUSEHOLDER) {
+        const double v = (double)((const T*)L.p[0])[(int64_t)st.col * D + d];
+        part += v * v;
+      } else if (st.op == OP_SCALESHIFT) {
+        const T av = ((const T*)L.p[0])[d], bv = ((const T*)L.p[1])[d];
+        r[2 * d] = av;
+        r[2 * d + 1] = bv;
+        part += log(fabs((double)av));
+      } else if (st.op == OP_JOHNSON || st.op == OP_JOHNSON_INV) {
+        const T g = ((const T*)L.p[0])[d], de = ((const T*)L.p[1])[d];
+        const T xi = ((const T*)L.p[2])[d], la = ((const T*)L.p[3])[d];
+        if constexpr (std::is_same_v<T, float>) {
+          if (st.op == OP_JOHNSON) {
+            r[4 * d + 0] = g;
+            r[4 * d + 1] = (float)((double)de * kLn2);
+            r[4 * d + 2] = xi;
+            r[4 * d + 3] = (float)(1.0 / (double)la);
+          } else {
+            r[4 * d + 0] = g;
+            r[4 * d + 1] = (float)(1.0 / (double)de);
+            r[4 * d + 2] = xi;
+            r[4 * d + 3] = la;
+          }
+        } else {
+          r[4 * d + 0] = g;
+          r[4 * d + 1] = de;
+          r[4 * d + 2] = xi;
+          r[4 * d + 3] = la;
+        }
+        // log|delta/lambda| (johnson_trafo.jl:41,51); the inverse negates (johnson_trafo.jl:104)
+        const double c = log(fabs((double)de)) - log(fabs((double)la));
+        part += st.op == OP_JOHNSON ? c : -c;
+      } else {  // CENTER_STRETCH / CENTER_CONTRACT
+        const T av = ((const T*)L.p[0])[d], bv = ((const T*)L.p[1])[d], cv = ((const T*)L.p[2])[d];
+        if constexpr (std::is_same_v<T, float>) {
+          const double b = bv, aa = av;
+          r[8 * d + 0] = (float)(b * kLog2e);
+          r[8 * d + 1] = cv;
+          r[8 * d + 2] = (float)(kLn2 / b);
+          r[8 * d + 3] = expf(bv * av);                  // exp(b*a) in T, as the reference
+          r[8 * d + 4] = expf(2.0f * bv * av);           // exp(2*b*a)
+          r[8 * d + 5] = (float)(b * aa * kLog2e);
+          r[8 * d + 6] = av;  // raw a, b for the generic kernel
+          r[8 * d + 7] = bv;
+        } else {
+          r[8 * d + 0] = av;
+          r[8 * d + 1] = bv;
+          r[8 * d + 2] = cv;
+          for (int q = 3; q < 8; ++q) r[8 * d + q] = 0.0;
+        }
+      }
+    }
+    // wave reduction of `part`
+    for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m);
+    if (st.op == OP_HOUSEHOLDER) {
+      // normalised reflection: H x = x - vh (vh'x), vh = v*sqrt(2/v'v) (householder_trafo.jl:9-10)
+      const double sc = sqrt(2.0 / part);
+      for (int d = lane; d < D; d += 64)
+        r[d] = (T)((double)((const T*)L.p[0])[(int64_t)st.col * D + d] * sc);
+      if (lane == 0) stepc[s] = 0.0;
+    } else {
+      if (lane == 0) stepc[s] = (st.op == OP_CENTER_STRETCH || st.op == OP_CENTER_CONTRACT) ? 0.0 : part;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double c = 0.0;
+    for (int s = 0; s < a.nsteps; ++s) c += stepc[s];
+    *ctot = c;
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------
+// per-element transforms. acc is the running per-lane ladj partial of one column, in units of
+// log2 (fp32) or natural log (fp64): ladj = C_total + UNIT * acc.
+// ------------------------------------------------------------------------------------------
+template <typename T>
+struct Unit;
+template <>
+struct Unit<float> { static constexpr float v = (float)kLn2; };
+template <>
+struct Unit<double> { static constexpr double v = 1.0; };
+
+// fp32 robust Johnson element (huge |z|, Inf, NaN): the rare path of the fragment kernel and the
+// generic kernel's form. asinh stays finite for |z| up to FLT_MAX; log(1+z^2) overflows to +Inf
+// exactly where the reference's fp32 `1 + ((x-xi)/lambda)^2` does (johnson_trafo.jl:41), so
+// the ladj is -Inf there, as in the reference.
+struct YL { float y, l; };
+__device__ __forceinline__ YL johnson_fwd_f32_slow(float x, float g, float d2, float xi, float il) {
+  const float z = (x - xi) * il;
+  const float t = fabsf(z);
+  const float q = fmaf(z, z, 1.0f);
+  const float L = t > 1e18f ? hw_log2(t) + 1.0f : hw_log2(t + hw_sqrt(q));  // log2(2|z|) when huge
+  return {fmaf(d2, copysignf(L, z), g), -0.5f * hw_log2(q)};             // ladj part in log2 units
+}
+
+// ------------------------------------------------------------------------------------------
+// the fragment kernel
+// ------------------------------------------------------------------------------------------
+template <typename T, int D>
+struct Frag {
+  static constexpr int V = 16 / (int)sizeof(T);        // elements per 16-B fragment
+  static constexpr int G = D >= V ? D / V : 1;         // lanes per column
+  static constexpr int CPF = D >= V ? 1 : V / D;       // columns per fragment
+  static constexpr int SEG = D >= V ? V : D;           // elements of one column in a fragment
+  static constexpr int COLS_PER_INSTR = 64 / G * CPF;  // columns per wave-instruction
+  static_assert(D >= V ? (D % V == 0 && G <= 64) : (V % D == 0), "unsupported D");
+};
+
+// fragment u of this lane holds rows r0 .. r0+SEG-1 of columns colf(u) .. colf(u)+CPF-1
+template <typename T, int D>
+__device__ __forceinline__ int64_t frag_col(int64_t col0, int u, int lane) {
+  using F = Frag<T, D>;
+  return col0 + (int64_t)u * F::COLS_PER_INSTR + (lane / F::G) * F::CPF;
+}
+
+// One wave tile = U fully coalesced 1-KiB wave-instructions (ldx == D, 16-B aligned).
+template <typename T, int D, int U, bool TAIL>
+__device__ __forceinline__ void load_tile(const FlowArgs& a, int64_t col0, T (&x)[U][Frag<T, D>::V]) {
+  using F = Frag<T, D>;
+  constexpr int V = F::V, G = F::G, SEG = F::SEG;
+  const int lane = threadIdx.x & 63;
+  const int r0 = D >= V ? V * (lane % G) : 0;
+  const T* __restrict__ X = (const T*)a.X;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t cf = frag_col<T, D>(col0, u, lane);
+    const int64_t eoff = cf * D + r0;
+    if (!TAIL) {
+      const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X + eoff));
+      __builtin_memcpy(&x[u][0], &v4, 16);
+    } else {
+#pragma unroll
+      for (int e = 0; e < V; ++e) x[u][e] = (cf + e / SEG) < a.N ? X[eoff + e] : (T)0;
+    }
+  }
+}
+
+template <typename T, int D, int U, bool LADJ, bool TAIL>
+__device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict__ rec, T ctot,
+                                          int64_t col0, T (&x)[U][Frag<T, D>::V]) {
+  using F = Frag<T, D>;
+  constexpr int V = F::V, G = F::G, CPF = F::CPF, SEG = F::SEG;
+  const int lane = threadIdx.x & 63;
+  T* __restrict__ Y = (T*)a.Y;
+  const int64_t N = a.N;
+  const int r0 = D >= V ? V * (lane % G) : 0;
+  int64_t colf[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) colf[u] = frag_col<T, D>(col0, u, lane);
+  T acc[U][CPF];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int c = 0; c < CPF; ++c) acc[u][c] = (T)0;
+
+  for (int s = 0; s < a.nsteps; ++s) {
+    const int op = a.steps[s].op;  // kernarg -> SGPR, uniform branch
+    const T* __restrict__ r = rec + a.steps[s].off;
+    if (op == OP_HOUSEHOLDER) {
+      T vh[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) vh[e] = r[r0 + e % SEG];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int c = 0; c < CPF; ++c) {
+          T dot = (T)0;
+#pragma unroll
+          for (int e = 0; e < SEG; ++e) dot = fma(vh[c * SEG + e], x[u][c * SEG + e], dot);
+          dot = group_sum<G>(dot);
+#pragma unroll
+          for (int e = 0; e < SEG; ++e) x[u][c * SEG + e] = fma(-dot, vh[c * SEG + e], x[u][c * SEG + e]);
+        }
+      }
+    } else if (op == OP_JOHNSON) {
+      T pg[V], pd[V], px[V], pl[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const int row = r0 + e % SEG;
+        pg[e] = r[4 * row + 0]; pd[e] = r[4 * row + 1]; px[e] = r[4 * row + 2]; pl[e] = r[4 * row + 3];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if constexpr (std::is_same_v<T, float>) {
+          // y = gamma + delta*asinh(z), asinh|z| = ln2*log2(|z| + sqrt(1+z^2))  (johnson_trafo.jl:31)
+          // ladj: log|delta/lambda| - log(1+z^2)/2                                (johnson_trafo.jl:41,51)
+          float xin[V];
+          float prod[CPF];
+#pragma unroll
+          for (int c = 0; c < CPF; ++c) prod[c] = 1.0f;
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            xin[e] = x[u][e];
+            const float z = (x[u][e] - px[e]) * pl[e];
+            const float q = fmaf(z, z, 1.0f);
+            const float L = hw_log2(fabsf(z) + hw_sqrt(q));
+            x[u][e] = fmaf(pd[e], copysignf(L, z), pg[e]);
+            prod[e / SEG] *= q;
+          }
+          // prod overflows (|z| >~ 1e9), or a non-finite input: exact elementwise rare path
+          bool bad = false;
+#pragma unroll
+          for (int c = 0; c < CPF; ++c) bad |= !(prod[c] <= FLT_MAX);
+          if (__builtin_expect(bad, 0)) {
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+              const YL r2 = johnson_fwd_f32_slow(xin[e], pg[e], pd[e], px[e], pl[e]);
+              x[u][e] = r2.y;
+              if (LADJ) acc[u][e / SEG] += r2.l;
+            }
+          } else if (LADJ) {
+#pragma unroll
+            for (int c = 0; c < CPF; ++c) acc[u][c] = fmaf(-0.5f, hw_log2(prod[c]), acc[u][c]);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            const double z = (x[u][e] - px[e]) / pl[e];
+            x[u][e] = pg[e] + pd[e] * asinh(z);
+            if (LADJ) acc[u][e / SEG] -= 0.5 * log1p(z * z);
+          }
+        }
+      }
+    } else if (op == OP_JOHNSON_INV) {
+      T pg[V], pd[V], px[V], pl[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const int row = r0 + e % SEG;
+        pg[e] = r[4 * row + 0]; pd[e] = r[4 * row + 1]; px[e] = r[4 * row + 2]; pl[e] = r[4 * row + 3];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          if constexpr (std::is_same_v<T, float>) {
+            // x = lambda*sinh((y-gamma)/delta) + xi (johnson_trafo.jl:36); ladj = -ladj_fwd(x_out)
+            // (johnson_trafo.jl:103-104) = -log|delta/lambda| + log(1 + sinh(w)^2)/2
+            const float w = (x[u][e] - pg[e]) * pd[e];
+            const float aw = fabsf(w);
+            // sinh: Taylor to w^7 below |w| = 0.5 (truncation < 1e-8 relative), else (E - 1/E)/2
+            const float E = hw_exp2(aw * (float)kLog2e);
+            const float big = 0.5f * (E - hw_rcp(E));
+            const float w2 = w * w;
+            const float sm = aw * fmaf(w2, fmaf(w2, fmaf(w2, 1.0f / 5040.0f, 1.0f / 120.0f), 1.0f / 6.0f), 1.0f);
+            const float sh = copysignf(aw < 0.5f ? sm : big, w);
+            x[u][e] = fmaf(pl[e], sh, px[e]);
+            if (LADJ) acc[u][e / SEG] = fmaf(0.5f, hw_log2(fmaf(sh, sh, 1.0f)), acc[u][e / SEG]);
+          } else {
+            const double w = (x[u][e] - pg[e]) / pd[e];
+            const double sh = sinh(w);
+            const double xo = pl[e] * sh + px[e];
+            x[u][e] = xo;
+            if (LADJ) {  // from the output, as the reference: log(1 + ((x_out - xi)/lambda)^2)/2
+              const double z = (xo - px[e]) / pl[e];
+              acc[u][e / SEG] += 0.5 * log1p(z * z);
+            }
+          }
+        }
+      }
+    } else if (op == OP_SCALESHIFT) {
+      // y = muladd(x, a, b) (scale_shift_trafo.jl:16); ladj = sum log|a| (constant, in ctot)
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const int row = r0 + e % SEG;
+        const T av = r[2 * row], bv = r[2 * row + 1];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u][e] = fma(x[u][e], av, bv);
+      }
+    } else if (op == OP_CENTER_STRETCH) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const int row = r0 + e % SEG;
+        const T* rr = r + 8 * row;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if constexpr (std::is_same_v<T, float>) {
+            // center_stretch.jl:4-8 with e = exp(|b x|); ladj = -contract_ladj(y) (:41-42)
+            const float bl = rr[0], c = rr[1], lnb = rr[2], E1 = rr[3], E2 = rr[4], bal = rr[5];
+            const float xv = x[u][e];
+            const float ex = hw_exp2(fabsf(xv * bl));
+            const float ome = 1.0f - ex;
+            const float A = fmaf(ome * ome, E2, 4.0f * ex);
+            const float inner = (hw_sqrt(A) - ome * E1) * 0.5f;
+            const float L = hw_log2(inner);
+            const float sg = xv > 0.f ? 1.f : (xv < 0.f ? -1.f : xv);  // Julia sign()
+            const float y = sg * L * lnb + c;
+            x[u][e] = y;
+            if (LADJ) {
+              const float yu = y - c;
+              const float e1 = hw_exp2(fmaf(-bl, yu, bal));
+              const float e2 = hw_exp2(fmaf(bl, yu, bal));
+              const float dy = hw_rcp(1.0f + e1) + hw_rcp(1.0f + e2);
+              acc[u][e / SEG] -= hw_log2(fabsf(dy));
+            }
+          } else {
+            const double av = rr[0], bv = rr[1], c = rr[2];
+            const double xv = x[u][e];
+            const double ex = exp(fabs(bv * xv));
+            const double ome = 1.0 - ex;
+            const double inner = (sqrt(ome * ome * exp(2.0 * bv * av) + 4.0 * ex) - ome * exp(bv * av)) / 2.0;
+            const double sg = xv > 0. ? 1. : (xv < 0. ? -1. : xv);
+            const double y = sg * log(inner) / bv + c;
+            x[u][e] = y;
+            if (LADJ) {
+              const double yu = y - c;
+              const double dy = 1.0 / (1.0 + exp(-bv * (yu - av))) + 1.0 / (1.0 + exp(bv * (yu + av)));
+              acc[u][e / SEG] -= log(fabs(dy));
+            }
+          }
+        }
+      }
+    } else {  // OP_CENTER_CONTRACT
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const int row = r0 + e % SEG;
+        const T* rr = r + 8 * row;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if constexpr (std::is_same_v<T, float>) {
+            // center_stretch.jl:11-15; ladj = contract_ladj(x) (:17-22, :65)
+            const float bl = rr[0], c = rr[1], lnb = rr[2], bal = rr[5];
+            const float xu = x[u][e] - c;
+            const float e1 = hw_exp2(fmaf(bl, xu, -bal));   // exp(b(xu - a))
+            const float e2 = hw_exp2(fmaf(-bl, xu, -bal));  // exp(-b(xu + a))
+            x[u][e] = (hw_log2(1.0f + e1) - hw_log2(1.0f + e2)) * lnb;
+            if (LADJ) {
+              const float e3 = hw_exp2(fmaf(-bl, xu, bal));  // exp(-b(xu - a))
+              const float e4 = hw_exp2(fmaf(bl, xu, bal));   // exp(b(xu + a))
+              const float dy = hw_rcp(1.0f + e3) + hw_rcp(1.0f + e4);
+              acc[u][e / SEG] += hw_log2(fabsf(dy));
+            }
+          } else {
+            const double av = rr[0], bv = rr[1], c = rr[2];
+            const double xu = x[u][e] - c;
+            x[u][e] = (log(1.0 + exp(bv * (xu - av))) - log(1.0 + exp(-bv * (xu + av)))) / bv;
+            if (LADJ) {
+              const double dy = 1.0 / (1.0 + exp(-bv * (xu - av))) + 1.0 / (1.0 + exp(bv * (xu + av)));
+              acc[u][e / SEG] += log(fabs(dy));
+            }
+          }
+        }
+      }
+    }
+  }
+
+  // ---- store Y and ladj
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t eoff = colf[u] * D + r0;
+    if (!TAIL) {
+      u32x4 v4;
+      __builtin_memcpy(&v4, &x[u][0], 16);
+      __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(Y + eoff));
+    } else {
+#pragma unroll
+      for (int e = 0; e < V; ++e)
+        if (colf[u] + e / SEG < N) Y[eoff + e] = x[u][e];
+    }
+  }
+  if (LADJ) {
+    T* __restrict__ ladj = (T*)a.ladj;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int c = 0; c < CPF; ++c) {
+        const T tot = group_sum<G>(acc[u][c]);
+        const int64_t col = colf[u] + c;
+        if ((lane % G) == 0 && (!TAIL || col < N)) {
+          const T v = fma(Unit<T>::v, tot, ctot);
+          ladj[col] = a.accumulate ? ladj[col] + v : v;
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int D, int U, bool LADJ>
+__global__ __launch_bounds__(256) void flow_frag_kernel(FlowArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* stepc = reinterpret_cast<double*>(smem);
+  double* ctotp = stepc + kMaxSteps;
+  T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
+  build_program<T, D>(a, rec, stepc, ctotp);
+  const T ctot = (T)*ctotp;
+
+  using F = Frag<T, D>;
+  constexpr int64_t COLS_PER_TILE = (int64_t)F::COLS_PER_INSTR * U;
+  const int64_t ntiles_full = a.N / COLS_PER_TILE;
+  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  // software pipeline: the next tile's loads are in flight while this tile computes
+  using XT = T[U][F::V];
+  XT xa, xb;
+  int64_t t = wave_id;
+  if (t < ntiles_full) load_tile<T, D, U, false>(a, t * COLS_PER_TILE, xa);
+  for (; t < ntiles_full; t += 2 * nwaves) {
+    const int64_t t1 = t + nwaves;
+    if (t1 < ntiles_full) load_tile<T, D, U, false>(a, t1 * COLS_PER_TILE, xb);
+    flow_tile<T, D, U, LADJ, false>(a, rec, ctot, t * COLS_PER_TILE, xa);
+    if (t1 >= ntiles_full) break;
+    const int64_t t2 = t1 + nwaves;
+    if (t2 < ntiles_full) load_tile<T, D, U, false>(a, t2 * COLS_PER_TILE, xa);
+    flow_tile<T, D, U, LADJ, false>(a, rec, ctot, t1 * COLS_PER_TILE, xb);
+  }
+  if (ntiles_full * COLS_PER_TILE < a.N && wave_id == ntiles_full % nwaves) {
+    load_tile<T, D, U, true>(a, ntiles_full * COLS_PER_TILE, xa);
+    flow_tile<T, D, U, LADJ, true>(a, rec, ctot, ntiles_full * COLS_PER_TILE, xa);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// generic kernel: any D, any leading dimensions, any alignment. One column per lane; the
+// column lives in Y (copied from X first), every step re-reads it from global memory.
+// ------------------------------------------------------------------------------------------
+template <typename T, bool LADJ>
+__global__ __launch_bounds__(256) void flow_generic_kernel(FlowArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* stepc = reinterpret_cast<double*>(smem);
+  double* ctotp = stepc + kMaxSteps;
+  T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
+  build_program<T, 0>(a, rec, stepc, ctotp);
+  const double ctot = *ctotp;
+  const int D = a.D;
+  const T* __restrict__ X = (const T*)a.X;
+  T* __restrict__ Y = (T*)a.Y;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a.N;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const T* x = X + j * a.ldx;
+    T* y = Y + j * a.ldy;
+    if (x != y)
+      for (int d = 0; d < D; ++d) y[d] = x[d];
+    double acc = 0.0;  // natural-log units
+    for (int s = 0; s < a.nsteps; ++s) {
+      const int op = a.steps[s].op;
+      const T* r = rec + a.steps[s].off;
+      if (op == OP_HOUSEHOLDER) {
+        T dot = 0;
+        for (int d = 0; d < D; ++d) dot = fma(r[d], y[d], dot);
+        for (int d = 0; d < D; ++d) y[d] = fma(-dot, r[d], y[d]);
+      } else if (op == OP_SCALESHIFT) {
+        for (int d = 0; d < D; ++d) y[d] = fma(y[d], r[2 * d], r[2 * d + 1]);
+      } else if (op == OP_JOHNSON) {
+        for (int d = 0; d < D; ++d) {
+          if constexpr (std::is_same_v<T, float>) {
+            const YL r2 = johnson_fwd_f32_slow(y[d], r[4 * d], r[4 * d + 1], r[4 * d + 2], r[4 * d + 3]);
+            y[d] = r2.y;
+            acc += (double)r2.l * kLn2;
+          } else {
+            const double z = (y[d] - r[4 * d + 2]) / r[4 * d + 3];
+            y[d] = r[4 * d] + r[4 * d + 1] * asinh(z);
+            acc -= 0.5 * log1p(z * z);
+          }
+        }
+      } else if (op == OP_JOHNSON_INV) {
+        for (int d = 0; d < D; ++d) {
+          if constexpr (std::is_same_v<T, float>) {
+            const float w = (y[d] - r[4 * d]) * r[4 * d + 1];
+            const float sh = sinhf(w);
+            y[d] = fmaf(r[4 * d + 3], sh, r[4 * d + 2]);
+            acc += 0.5 * log1p((double)sh * sh);
+          } else {
+            const double w = (y[d] - r[4 * d]) / r[4 * d + 1];
+            const double xo = r[4 * d + 3] * sinh(w) + r[4 * d + 2];
+            y[d] = xo;
+            const double z = (xo - r[4 * d + 2]) / r[4 * d + 3];
+            acc += 0.5 * log1p(z * z);
+          }
+        }
+      } else if (op == OP_CENTER_STRETCH || op == OP_CENTER_CONTRACT) {
+        for (int d = 0; d < D; ++d) {
+          const T* rr = r + 8 * d;
+          double av, bv, c;
+          if constexpr (std::is_same_v<T, float>) {
+            av = rr[6]; bv = rr[7]; c = rr[1];
+          } else {
+            av = rr[0]; bv = rr[1]; c = rr[2];
+          }
+          const T xv = y[d];
+          if (op == OP_CENTER_STRETCH) {
+            const T ex = (T)exp(fabs((T)bv * xv));
+            const T ome = (T)1 - ex;
+            const T inner = ((T)sqrt(ome * ome * (T)exp(2.0 * bv * av) + (T)4 * ex) - ome * (T)exp(bv * av)) / (T)2;
+            const T sg = xv > (T)0 ? (T)1 : (xv < (T)0 ? (T)-1 : xv);
+            const T yv = sg * (T)log(inner) / (T)bv + (T)c;
+            y[d] = yv;
+            const double yu = (double)yv - c;
+            acc -= log(fabs(1.0 / (1.0 + exp(-bv * (yu - av))) + 1.0 / (1.0 + exp(bv * (yu + av)))));
+          } else {
+            const double xu = (double)xv - c;
+            y[d] = (T)((log(1.0 + exp(bv * (xu - av))) - log(1.0 + exp(-bv * (xu + av)))) / bv);
+            acc += log(fabs(1.0 / (1.0 + exp(-bv * (xu - av))) + 1.0 / (1.0 + exp(bv * (xu + av)))));
+          }
+        }
+      }
+    }
+    if (LADJ) {
+      T* ladj = (T*)a.ladj;
+      const T v = (T)(ctot + acc);
+      ladj[j] = a.accumulate ? ladj[j] + v : v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host-side launch
+// ------------------------------------------------------------------------------------------
+size_t program_lds_bytes(const FlowArgs& a, size_t elem) {
+  size_t n = 0;
+  for (int s = 0; s < a.nsteps; ++s) n += (size_t)record_width(a.steps[s].op) * (size_t)a.D;
+  return kLdsHeader + n * elem;
+}
+
+// Tuning knobs (development only): ENF_BLOCKS_PER_CU caps resident blocks per CU in the grid size,
+// ENF_FRAG_U selects the tile depth U for D >= 16.
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+
+template <typename T, int D, int U, bool LADJ>
+static hipError_t launch_frag(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
+  using F = Frag<T, D>;
+  const int64_t cols_per_block = (int64_t)F::COLS_PER_INSTR * U * 4;
+  int per_cu = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flow_frag_kernel<T, D, U, LADJ>, 256, lds);
+  if (e != hipSuccess) return e;
+  static const int cap_env = env_int("ENF_BLOCKS_PER_CU", 0);
+  if (cap_env > 0 && per_cu > cap_env) per_cu = cap_env;
+  if (per_cu < 1) per_cu = 1;
+  int64_t blocks = (a.N + cols_per_block - 1) / cols_per_block;
+  const int64_t cap = (int64_t)dev.num_cu * per_cu;
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL((flow_frag_kernel<T, D, U, LADJ>), dim3((unsigned)blocks), dim3(256), lds, st, a);
+  return hipGetLastError();
+}
+
+template <typename T, bool LADJ>
+static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
+  constexpr bool f32 = std::is_same_v<T, float>;
+  switch (a.D) {
+    case 1: return launch_frag<T, 1, 4, LADJ>(a, lds, st, dev);
+    case 2: return launch_frag<T, 2, 4, LADJ>(a, lds, st, dev);
+    case 4: return launch_frag<T, 4, 4, LADJ>(a, lds, st, dev);
+    case 8: return launch_frag<T, 8, 4, LADJ>(a, lds, st, dev);
+    case 16: return launch_frag<T, 16, 4, LADJ>(a, lds, st, dev);
+    case 32: {
+      static const int u = env_int("ENF_FRAG_U", 4);
+      if (u == 2) return launch_frag<T, 32, 2, LADJ>(a, lds, st, dev);
+      if (u == 8) return launch_frag<T, 32, 8, LADJ>(a, lds, st, dev);
+      return launch_frag<T, 32, 4, LADJ>(a, lds, st, dev);
+    }
+    case 64: return f32 ? launch_frag<T, 64, 4, LADJ>(a, lds, st, dev) : launch_frag<T, 64, 2, LADJ>(a, lds, st, dev);
+    default: break;
+  }
+  return hipErrorInvalidValue;
+}
+
+bool frag_supported(const FlowArgs& a, size_t elem) {
+  const int D = a.D;
+  const bool pow2 = D >= 1 && D <= 64 && (D & (D - 1)) == 0;
+  if (!pow2) return false;
+  if (a.ldx != D || a.ldy != D) return false;
+  if (((uintptr_t)a.X | (uintptr_t)a.Y) & 15) return false;
+  (void)elem;
+  return true;
+}
+
+hipError_t launch_flow(const FlowArgs& a, bool f64, hipStream_t st, const DeviceInfo& dev) {
+  const size_t elem = f64 ? 8 : 4;
+  const size_t lds = program_lds_bytes(a, elem);
+  const bool ladj = a.ladj != nullptr;
+  if (frag_supported(a, elem)) {
+    if (f64) return ladj ? dispatch_D<double, true>(a, lds, st, dev) : dispatch_D<double, false>(a, lds, st, dev);
+    return ladj ? dispatch_D<float, true>(a, lds, st, dev) : dispatch_D<float, false>(a, lds, st, dev);
+  }
+  int64_t blocks = (a.N + 255) / 256;
+  const int64_t cap = (int64_t)dev.num_cu * 8;
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  if (f64) {
+    if (ladj) hipLaunchKernelGGL((flow_generic_kernel<double, true>), dim3((unsigned)blocks), dim3(256), lds, st, a);
+    else hipLaunchKernelGGL((flow_generic_kernel<double, false>), dim3((unsigned)blocks), dim3(256), lds, st, a);
+  } else {
+    if (ladj) hipLaunchKernelGGL((flow_generic_kernel<float, true>), dim3((unsigned)blocks), dim3(256), lds, st, a);
+    else hipLaunchKernelGGL((flow_generic_kernel<float, false>), dim3((unsigned)blocks), dim3(256), lds, st, a);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace enf

@@ -1,0 +1,144 @@
+/* enf.h -- C ABI of libenf.so, the MI355X-native (gfx950) bijector hot path of
+ * bat/EuclidianNormalizingFlows.jl.
+ *
+ * Every entry point is `extern "C"`, takes plain pointers and sizes, never throws, and returns
+ * an enf_status; the message of the last failure on the calling thread is enf_last_error().
+ * Compute calls are asynchronous on the given HIP stream (NULL = the default stream) and
+ * never keep a pointer past the completion of the work they enqueue. The caller owns every
+ * buffer. Data layout is Julia's: a batch is a column-major D x N matrix, sample j being the
+ * contiguous column X[j*ldx .. j*ldx+D-1]; ladj is a length-N vector (Julia's 1 x N row).
+ *
+ * Reference interface replaced (bat/EuclidianNormalizingFlows.jl v0.1.0):
+ *   ChangesOfVariables.with_logabsdet_jacobian(f, X) for
+ *     ScaleShiftTrafo   src/scale_shift_trafo.jl:15-24
+ *     CenterStretch     src/center_stretch.jl:37-43
+ *     CenterContract    src/center_stretch.jl:61-67
+ *     JohnsonTrafo      src/johnson_trafo.jl:74-80
+ *     JohnsonTrafoInv   src/johnson_trafo.jl:99-105
+ *     HouseholderTrafo  src/householder_trafo.jl:156-160 (vector and matrix V)
+ *   and their Base.ComposedFunction (ChangesOfVariables 0.1: inner first, ladj_inner+ladj_outer)
+ *   -> enf_flow_apply (one fused launch for the whole composition).
+ *   (f)(X)  (the same call sites without ladj)                    -> enf_flow_apply, ladj = NULL.
+ *   InverseFunctions.inverse(f)  is host-side parameter algebra (src/scale_shift_trafo.jl:26-30,
+ *   src/center_stretch.jl:45,69, src/johnson_trafo.jl:82,107, src/householder_trafo.jl:153-154)
+ *   and stays in the host mirror; inverse flows run through enf_flow_apply with swapped ops.
+ *   mvnormal_negll_trafo / mvnormal_negll_trafograd (src/optimize_whitening.jl:7-22)
+ *                                                                -> enf_flow_negll_grad
+ *   Optimisers.update(ADAGrad) + HouseholderTrafo functor re-normalisation
+ *     (src/optimize_whitening.jl:40, src/householder_trafo.jl:134-146) -> enf_adagrad_step
+ */
+#ifndef ENF_H
+#define ENF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ENF_VERSION_MAJOR 0
+#define ENF_VERSION_MINOR 1
+#define ENF_VERSION_PATCH 0
+
+typedef enum {
+  ENF_OK = 0,
+  ENF_ERR_INVALID = 1,     /* bad argument (shape, null pointer, unknown op ...) */
+  ENF_ERR_HIP = 2,         /* a HIP runtime call failed */
+  ENF_ERR_UNSUPPORTED = 3, /* valid request the library does not implement */
+  ENF_ERR_RCCL = 4         /* an RCCL call failed */
+} enf_status;
+
+typedef enum { ENF_F32 = 0, ENF_F64 = 1 } enf_dtype;
+
+/* Transform kinds; params p[0..3] are DEVICE pointers to length-D vectors of the flow's dtype
+ * (a Julia scalar parameter is broadcast to length D by the host). */
+typedef enum {
+  ENF_OP_SCALESHIFT = 0,      /* p = {a, b}:                 y = muladd(x, a, b)            */
+  ENF_OP_CENTER_STRETCH = 1,  /* p = {a, b, c}                                              */
+  ENF_OP_CENTER_CONTRACT = 2, /* p = {a, b, c}                                              */
+  ENF_OP_JOHNSON = 3,         /* p = {gamma, delta, xi, lambda}: y = g + d*asinh((x-xi)/l)  */
+  ENF_OP_JOHNSON_INV = 4,     /* p = {gamma, delta, xi, lambda}: y = l*sinh((x-g)/d) + xi   */
+  ENF_OP_HOUSEHOLDER = 5      /* p = {V}, V column-major D x k, reflections V[:,0]..V[:,k-1]
+                                 applied in column order (chained_householder_trafo!)        */
+} enf_op;
+
+typedef struct {
+  int32_t op;        /* enf_op */
+  int32_t k;         /* HOUSEHOLDER: number of reflection columns (>= 1); otherwise ignored */
+  const void* p[4];  /* device pointers */
+} enf_layer;
+
+/* ---------------------------------------------------------------- version / errors ---- */
+/* "MAJOR.MINOR.PATCH gfx950" */
+const char* enf_version(void);
+/* Message of the last failing call on this thread ("" if none). */
+const char* enf_last_error(void);
+
+/* ---------------------------------------------------------------- device helpers ------ */
+enf_status enf_device_count(int32_t* count);
+enf_status enf_set_device(int32_t device);
+enf_status enf_get_device(int32_t* device);
+enf_status enf_malloc(void** ptr, size_t bytes);
+enf_status enf_free(void* ptr);
+/* kind: 0 host->device, 1 device->host, 2 device->device, 3 default (inferred). Async on stream. */
+enf_status enf_memcpy(void* dst, const void* src, size_t bytes, int32_t kind, void* hip_stream);
+enf_status enf_stream_synchronize(void* hip_stream);
+
+/* ---------------------------------------------------------------- forward / inverse ---- */
+/* Apply the composed flow layers[0], then layers[1], ... (layers[0] innermost, i.e. the
+ * Julia value layers[n-1] o ... o layers[0]) to X (D x N, leading dim ldx >= D) and write
+ * Y (leading dim ldy >= D). Y may alias X exactly (ldx == ldy) for an in-place transform.
+ * ladj (length N) may be NULL (plain call f(X)); otherwise it receives sum over layers of the
+ * per-sample log|det J|, or has it ADDED when accumulate_ladj != 0.
+ * N == 0 is a no-op. Asynchronous on hip_stream. */
+enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
+                          void* Y, int64_t ldy, void* ladj, int32_t accumulate_ladj,
+                          const enf_layer* layers, int32_t nlayers, void* hip_stream);
+
+/* ---------------------------------------------------------------- training (config 5) -- */
+/* Number of gradient entries of the flow: sum over layers of D*nparams (Householder D*k).
+ * The gradient buffer layout is layer by layer, parameter by parameter, each a length-D vector
+ * (Householder: the D x k matrix, column-major), in the order of enf_layer.p. */
+enf_status enf_flow_param_count(int64_t D, const enf_layer* layers, int32_t nlayers,
+                                int64_t* count);
+/* Per-GPU UNNORMALISED sums for mvnormal_negll_trafo (src/optimize_whitening.jl:7-15) over the
+ * N local samples: out[0] += sum_j [ sum_d (y_dj^2 + log 2pi)/2 - ladj_j ]  (= N * negll),
+ * out[1 + i] += d(out[0]) / d(theta_i) for every flow parameter theta_i (layout above).
+ * out has 1 + param_count entries and is ACCUMULATED into (zero it first). Divide by the
+ * global batch size after the cross-GPU sum to obtain negll and its gradient.
+ * workspace: device scratch of enf_flow_negll_grad_workspace() bytes. */
+enf_status enf_flow_negll_grad_workspace(enf_dtype dtype, int64_t D, int64_t N,
+                                         const enf_layer* layers, int32_t nlayers,
+                                         size_t* bytes);
+enf_status enf_flow_negll_grad(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
+                               const enf_layer* layers, int32_t nlayers, void* out,
+                               void* workspace, size_t workspace_bytes, void* hip_stream);
+/* In-place ADAGrad step of Optimisers.jl 0.2 (eta, epsilon) over `count` parameters:
+ * acc += g.^2; theta -= eta * g ./ (sqrt.(acc) .+ epsilon), with g = grad * grad_scale.
+ * params/acc/grad are device arrays of the dtype. */
+enf_status enf_adagrad_step(enf_dtype dtype, int64_t count, void* params, void* acc,
+                            const void* grad, double grad_scale, double eta, double epsilon,
+                            void* hip_stream);
+/* HouseholderTrafo functor reconstruction (src/householder_trafo.jl:134-146): normalise each of
+ * the k columns of the D x k device matrix V to unit 2-norm, in place. */
+enf_status enf_householder_normalize(enf_dtype dtype, int64_t D, int64_t k, void* V,
+                                     void* hip_stream);
+
+/* ---------------------------------------------------------------- RCCL ---------------- */
+/* Opaque communicator for the gradient all-reduce (one rank per GPU, one process each). */
+typedef struct enf_comm_s* enf_comm;
+#define ENF_UNIQUE_ID_BYTES 128
+/* Rank 0 creates the id and ships it to the other ranks out of band. */
+enf_status enf_comm_unique_id(uint8_t id[ENF_UNIQUE_ID_BYTES]);
+enf_status enf_comm_init(enf_comm* comm, int32_t nranks, const uint8_t id[ENF_UNIQUE_ID_BYTES],
+                         int32_t rank);
+enf_status enf_comm_destroy(enf_comm comm);
+/* In-place sum all-reduce of `count` dtype elements over the communicator. */
+enf_status enf_allreduce_sum(enf_comm comm, void* buf, int64_t count, enf_dtype dtype,
+                             void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ENF_H */

@@ -1,0 +1,301 @@
+"""Generate the golden fixtures under tests/golden/ (TEST INFRASTRUCTURE ONLY).
+
+Julia is not installed here or on the GPU box, so the reference cannot be
+executed. The golden vectors are the reference FORMULAS evaluated exactly: mpmath at 50
+significant digits, with inputs that are exactly representable in the target precision, the
+result rounded to float64. They pin the oracle (oracle/enf_oracle.c) and the HIP kernels.
+
+Formulas (bat/EuclidianNormalizingFlows.jl v0.1.0):
+  center_stretch            src/center_stretch.jl:4-8
+  center_contract           src/center_stretch.jl:11-15
+  center_contract_ladj      src/center_stretch.jl:17-22
+  johnsontrafo[_inv]        src/johnson_trafo.jl:29-37
+  deriv_johnsontrafo[_inv]  src/johnson_trafo.jl:39-47
+  johnsontrafo[_inv]_ladj   src/johnson_trafo.jl:49-57
+  householder_trafo         src/householder_trafo.jl:8-11, chained :71-78
+  trafo ladj conventions    src/center_stretch.jl:39-43,63-67; src/johnson_trafo.jl:76-80,101-105;
+                            src/scale_shift_trafo.jl:18-24; src/householder_trafo.jl:159-160
+  composition               ChangesOfVariables 0.1: ladj(f o g) = ladj(g) + ladj(f)
+
+Usage: python oracle/gen_golden.py   (writes tests/golden/*.npz and kats.json; deterministic)
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import mpmath as mp
+import numpy as np
+
+mp.mp.dps = 50
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(os.path.dirname(HERE), "tests", "golden")
+
+OP_SCALESHIFT, OP_CENTER_STRETCH, OP_CENTER_CONTRACT, OP_JOHNSON, OP_JOHNSON_INV, OP_HOUSEHOLDER = range(6)
+
+
+def M(x):
+    return mp.mpf(float(x))
+
+
+def center_stretch(x, a, b, c):
+    x, a, b, c = M(x), M(a), M(b), M(c)
+    e = mp.exp(abs(b * x))
+    inner = (mp.sqrt((1 - e) ** 2 * mp.exp(2 * b * a) + 4 * e) - (1 - e) * mp.exp(b * a)) / 2
+    return mp.sign(x) * mp.log(inner) / b + c
+
+
+def center_contract(x, a, b, c):
+    x, a, b, c = M(x), M(a), M(b), M(c)
+    xu = x - c
+    return (mp.log(1 + mp.exp(b * (xu - a))) - mp.log(1 + mp.exp(-b * (xu + a)))) / b
+
+
+def center_contract_ladj(x, a, b, c):
+    x, a, b, c = M(x), M(a), M(b), M(c)
+    xu = x - c
+    return mp.log(abs(1 / (1 + mp.exp(-b * (xu - a))) + 1 / (1 + mp.exp(b * (xu + a)))))
+
+
+def johnsontrafo(x, g, d, xi, l):
+    x, g, d, xi, l = map(M, (x, g, d, xi, l))
+    return g + d * mp.asinh((x - xi) / l)
+
+
+def johnsontrafo_inv(x, g, d, xi, l):
+    x, g, d, xi, l = map(M, (x, g, d, xi, l))
+    return l * mp.sinh((x - g) / d) + xi
+
+
+def deriv_johnsontrafo(x, g, d, xi, l):
+    x, g, d, xi, l = map(M, (x, g, d, xi, l))
+    return (d / l) * (1 / mp.sqrt(1 + ((x - xi) / l) ** 2))
+
+
+def deriv_johnsontrafo_inv(x, g, d, xi, l):
+    x, g, d, xi, l = map(M, (x, g, d, xi, l))
+    return l * mp.cosh((x - g) / d) / d
+
+
+def johnsontrafo_ladj(x, g, d, xi, l):
+    return mp.log(abs(deriv_johnsontrafo(x, g, d, xi, l)))
+
+
+def johnsontrafo_inv_ladj(x, g, d, xi, l):
+    return mp.log(abs(deriv_johnsontrafo_inv(x, g, d, xi, l)))
+
+
+SCALAR = {
+    "center_stretch": center_stretch, "center_contract": center_contract,
+    "center_contract_ladj": center_contract_ladj, "johnsontrafo": johnsontrafo,
+    "johnsontrafo_inv": johnsontrafo_inv, "deriv_johnsontrafo": deriv_johnsontrafo,
+    "deriv_johnsontrafo_inv": deriv_johnsontrafo_inv, "johnsontrafo_ladj": johnsontrafo_ladj,
+    "johnsontrafo_inv_ladj": johnsontrafo_inv_ladj,
+}
+
+
+def trafo_exact(op, params, X):
+    """Exact (mpmath) with_logabsdet_jacobian of one transform over an mp matrix X (list of columns).
+
+    Returns (Y columns, ladj list)."""
+    D = len(X[0])
+    Y, L = [], []
+    for x in X:
+        if op == OP_SCALESHIFT:
+            a, b = params
+            y = [x[d] * M(a[d]) + M(b[d]) for d in range(D)]
+            l = mp.fsum(mp.log(abs(M(a[d]))) for d in range(D))
+        elif op == OP_CENTER_STRETCH:
+            a, b, c = params
+            y = [center_stretch_mp(x[d], a[d], b[d], c[d]) for d in range(D)]
+            l = -mp.fsum(ccl_mp(y[d], a[d], b[d], c[d]) for d in range(D))
+        elif op == OP_CENTER_CONTRACT:
+            a, b, c = params
+            y = [center_contract_mp(x[d], a[d], b[d], c[d]) for d in range(D)]
+            l = mp.fsum(ccl_mp(x[d], a[d], b[d], c[d]) for d in range(D))
+        elif op == OP_JOHNSON:
+            g, dl, xi, lm = params
+            z = [(x[d] - M(xi[d])) / M(lm[d]) for d in range(D)]
+            y = [M(g[d]) + M(dl[d]) * mp.asinh(z[d]) for d in range(D)]
+            l = mp.fsum(mp.log(abs(M(dl[d]) / M(lm[d]) / mp.sqrt(1 + z[d] ** 2))) for d in range(D))
+        elif op == OP_JOHNSON_INV:
+            g, dl, xi, lm = params
+            y = [M(lm[d]) * mp.sinh((x[d] - M(g[d])) / M(dl[d])) + M(xi[d]) for d in range(D)]
+            l = -mp.fsum(mp.log(abs(M(dl[d]) / M(lm[d]) / mp.sqrt(1 + ((y[d] - M(xi[d])) / M(lm[d])) ** 2)))
+                         for d in range(D))
+        elif op == OP_HOUSEHOLDER:
+            V = params[0]
+            y = list(x)
+            for i in range(V.shape[1]):
+                v = [M(V[d, i]) for d in range(D)]
+                k = mp.fsum(v[d] * y[d] for d in range(D)) / mp.fsum(vd * vd for vd in v)
+                y = [y[d] - 2 * k * v[d] for d in range(D)]
+            l = mp.mpf(0)
+        else:
+            raise ValueError(op)
+        Y.append(y)
+        L.append(l)
+    return Y, L
+
+
+def center_stretch_mp(x, a, b, c):
+    a, b, c = M(a), M(b), M(c)
+    e = mp.exp(abs(b * x))
+    inner = (mp.sqrt((1 - e) ** 2 * mp.exp(2 * b * a) + 4 * e) - (1 - e) * mp.exp(b * a)) / 2
+    return mp.sign(x) * mp.log(inner) / b + c
+
+
+def center_contract_mp(x, a, b, c):
+    a, b, c = M(a), M(b), M(c)
+    xu = x - c
+    return (mp.log(1 + mp.exp(b * (xu - a))) - mp.log(1 + mp.exp(-b * (xu + a)))) / b
+
+
+def ccl_mp(x, a, b, c):
+    a, b, c = M(a), M(b), M(c)
+    xu = x - c
+    return mp.log(abs(1 / (1 + mp.exp(-b * (xu - a))) + 1 / (1 + mp.exp(b * (xu + a)))))
+
+
+def flow_exact(layers, X):
+    """Exact composed flow over X (numpy D x N): returns float64 Y (D,N), ladj (N,)."""
+    D, N = X.shape
+    cols = [[M(X[d, j]) for d in range(D)] for j in range(N)]
+    tot = [mp.mpf(0)] * N
+    for op, params in layers:
+        cols, L = trafo_exact(op, params, cols)
+        tot = [t + l for t, l in zip(tot, L)]
+    Y = np.array([[float(cols[j][d]) for j in range(N)] for d in range(D)], dtype=np.float64)
+    return np.asfortranarray(Y), np.array([float(t) for t in tot], dtype=np.float64)
+
+
+def rand_params(rng, op, D, dtype, K=1):
+    """Synthetic parameter distributions of SURVEY.md §8(d)."""
+    u = lambda lo, hi: rng.uniform(lo, hi, D).astype(dtype)
+    if op == OP_SCALESHIFT:
+        return [(np.where(rng.random(D) < 0.5, -1, 1) * rng.uniform(0.5, 2, D)).astype(dtype),
+                rng.standard_normal(D).astype(dtype)]
+    if op in (OP_CENTER_STRETCH, OP_CENTER_CONTRACT):
+        return [u(0, 2), u(0.5, 2), u(-0.5, 0.5)]
+    if op in (OP_JOHNSON, OP_JOHNSON_INV):
+        return [u(-1, 1), u(0.5, 2), u(-0.5, 0.5), u(0.5, 2)]
+    if op == OP_HOUSEHOLDER:
+        return [np.asfortranarray(rng.standard_normal((D, K)).astype(dtype))]
+    raise ValueError(op)
+
+
+def save_flow(name, layers, X, dtype):
+    Y, L = flow_exact(layers, X)
+    d = {"X": X.astype(dtype), "Y_exact": Y, "ladj_exact": L, "ops": np.array([op for op, _ in layers], np.int32)}
+    for i, (op, params) in enumerate(layers):
+        for q, p in enumerate(params):
+            d[f"L{i}_p{q}"] = np.asarray(p, dtype=dtype)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **d)
+    print("wrote", name, X.shape)
+
+
+def gen_scalars(rng, dtype, n=160):
+    out = {}
+    for name, fn in SCALAR.items():
+        nargs = 4 if name.startswith("center") else 5
+        rows = []
+        for _ in range(n):
+            if name.startswith("center"):
+                a, b, c = rng.uniform(0, 2), rng.uniform(0.5, 2), rng.uniform(-0.5, 0.5)
+                x = rng.standard_normal() * 3 if name != "center_stretch" else rng.standard_normal() * 2
+                args = [x, a, b, c]
+            else:
+                args = [rng.standard_normal() * 3, rng.uniform(-1, 1), rng.uniform(0.5, 2),
+                        rng.uniform(-0.5, 0.5), rng.uniform(0.5, 2)]
+            args = [float(np.dtype(dtype).type(v)) for v in args]
+            rows.append(args + [float(fn(*args))])
+        out[name] = np.array(rows, dtype=np.float64).reshape(n, nargs + 1)
+    np.savez_compressed(os.path.join(OUT, f"scalars_{np.dtype(dtype).name}.npz"), **out)
+    print("wrote scalars", np.dtype(dtype).name)
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    # 1. the reference's own known-answer tests, with their exact values
+    kats = [
+        {"fn": "center_stretch", "args": [1.0, 7, 2, 4], "T": "float32", "expected": 11.927293,
+         "src": "test/test_center_stretch.jl:18"},
+        {"fn": "center_contract", "args": [12.0, 7, 2, 4], "T": "float32", "expected": 1.063464,
+         "src": "test/test_center_stretch.jl:19"},
+        {"fn": "johnsontrafo", "args": [0.3, 1, 3, -4, 0.5], "T": "float64", "expected": 9.544817734776984,
+         "src": "test/test_johnson_trafo.jl:21"},
+        {"fn": "johnsontrafo_inv", "args": [0.3, 1, 3, -4, 0.5], "T": "float64",
+         "expected": -4.1177281942392545, "src": "test/test_johnson_trafo.jl:22"},
+        {"fn": "center_contract_ladj", "args": [4.2, 4, 2, 3], "T": "float64", "expected": None,
+         "src": "test/test_center_stretch.jl:25 (pinned to log|d/dx center_contract| at rtol 0.01)"},
+        {"fn": "johnsontrafo_ladj", "args": [0.5, 4.2, 4, 2, 3], "T": "float64", "expected": None,
+         "src": "test/test_johnson_trafo.jl:28"},
+        {"fn": "johnsontrafo_inv_ladj", "args": [0.5, 4.2, 4, 2, 3], "T": "float64", "expected": None,
+         "src": "test/test_johnson_trafo.jl:29"},
+    ]
+    for k in kats:
+        args = [float(np.dtype(k["T"]).type(a)) for a in k["args"]]
+        k["exact"] = mp.nstr(SCALAR[k["fn"]](*args), 25)
+        # the ForwardDiff cross-checks: log|derivative| at the same point
+        if k["fn"] == "center_contract_ladj":
+            k["log_abs_derivative"] = mp.nstr(mp.log(abs(mp.diff(lambda t: center_contract(t, 4, 2, 3), mp.mpf(4.2)))), 25)
+        if k["fn"] == "johnsontrafo_ladj":
+            k["log_abs_derivative"] = mp.nstr(mp.log(abs(mp.diff(lambda t: johnsontrafo(t, 4.2, 4, 2, 3), mp.mpf(0.5)))), 25)
+        if k["fn"] == "johnsontrafo_inv_ladj":
+            k["log_abs_derivative"] = mp.nstr(mp.log(abs(mp.diff(lambda t: johnsontrafo_inv(t, 4.2, 4, 2, 3), mp.mpf(0.5)))), 25)
+    with open(os.path.join(OUT, "kats.json"), "w") as f:
+        json.dump(kats, f, indent=1)
+    print("wrote kats.json")
+
+    rng = np.random.default_rng(20261015)
+    gen_scalars(rng, np.float64)
+    gen_scalars(rng, np.float32)
+
+    # 2. the reference test matrices (test_center_stretch.jl:44-70, test_johnson_trafo.jl:51-77)
+    Xs = np.asfortranarray(rng.standard_normal((2, 3)))
+    save_flow("cs_ref_test", [(OP_CENTER_STRETCH, [np.array([4.0, 4.1]), np.array([2.0, 2.1]), np.array([3.0, 3.1])])],
+              Xs, np.float64)
+    save_flow("jt_ref_test", [(OP_JOHNSON, [np.array([10.0, 11.0]), np.array([3.5, 3.6]), np.array([10.0, 11.0]),
+                                            np.array([1.0, 1.1])])], Xs, np.float64)
+
+    # 3. every single transform, both precisions, D in {1, 2, 5, 32}
+    for dtype in (np.float64, np.float32):
+        tn = np.dtype(dtype).name
+        for D in (1, 2, 5, 32):
+            N = 48 if D == 32 else 64
+            for op in range(6):
+                K = 3 if op == OP_HOUSEHOLDER and D > 1 else 1
+                X = np.asfortranarray(rng.standard_normal((D, N)).astype(dtype))
+                if op == OP_JOHNSON_INV:
+                    X = np.asfortranarray((X * 1.5).astype(dtype))
+                if op == OP_CENTER_CONTRACT:
+                    X = np.asfortranarray((X * 3).astype(dtype))
+                save_flow(f"single_op{op}_D{D}_{tn}", [(op, rand_params(rng, op, D, dtype, K))], X, dtype)
+
+    # 4. config 2: JohnsonTrafo o HouseholderTrafo, D=2, fp64 (Householder applied first)
+    X = np.asfortranarray(rng.standard_normal((2, 256)))
+    save_flow("config2_JoH_D2_float64", [(OP_HOUSEHOLDER, rand_params(rng, OP_HOUSEHOLDER, 2, np.float64)),
+                                          (OP_JOHNSON, rand_params(rng, OP_JOHNSON, 2, np.float64))], X, np.float64)
+    # 5. config 3: J4 o H4 o ... o J1 o H1, D=32, fp32 (small N)
+    for dtype in (np.float32, np.float64):
+        layers = []
+        for _ in range(4):
+            layers.append((OP_HOUSEHOLDER, rand_params(rng, OP_HOUSEHOLDER, 32, dtype)))
+            layers.append((OP_JOHNSON, rand_params(rng, OP_JOHNSON, 32, dtype)))
+        X = np.asfortranarray(rng.standard_normal((32, 40)).astype(dtype))
+        save_flow(f"config3_flow8_D32_{np.dtype(dtype).name}", layers, X, dtype)
+    # 6. a mixed flow using every op (2-D example style, examples/nf_example_2d.jl:12-25)
+    for dtype in (np.float64, np.float32):
+        D = 4
+        layers = [(OP_SCALESHIFT, rand_params(rng, OP_SCALESHIFT, D, dtype)),
+                  (OP_HOUSEHOLDER, rand_params(rng, OP_HOUSEHOLDER, D, dtype, 2)),
+                  (OP_CENTER_CONTRACT, rand_params(rng, OP_CENTER_CONTRACT, D, dtype)),
+                  (OP_JOHNSON, rand_params(rng, OP_JOHNSON, D, dtype)),
+                  (OP_CENTER_STRETCH, rand_params(rng, OP_CENTER_STRETCH, D, dtype)),
+                  (OP_JOHNSON_INV, rand_params(rng, OP_JOHNSON_INV, D, dtype))]
+        X = np.asfortranarray(rng.standard_normal((D, 64)).astype(dtype))
+        save_flow(f"mixed_all_ops_D4_{np.dtype(dtype).name}", layers, X, dtype)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,173 @@
+"""ctypes front end of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may import this
+module, and only as the checker or as the timed CPU baseline. The product path
+(``libenf.so`` + the host package) never imports it.
+
+The oracle restates bat/EuclidianNormalizingFlows.jl v0.1.0 (see enf_oracle.c for the
+file:line of every function). Matrices are numpy arrays of shape (D, N) in Fortran
+(column-major) order, i.e. sample j is the contiguous column X[:, j], exactly as in Julia.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+
+OP_SCALESHIFT, OP_CENTER_STRETCH, OP_CENTER_CONTRACT, OP_JOHNSON, OP_JOHNSON_INV, OP_HOUSEHOLDER = range(6)
+NPARAMS = {OP_SCALESHIFT: 2, OP_CENTER_STRETCH: 3, OP_CENTER_CONTRACT: 3, OP_JOHNSON: 4,
+           OP_JOHNSON_INV: 4, OP_HOUSEHOLDER: 1}
+
+
+class _Layer(ctypes.Structure):
+    _fields_ = [("op", ctypes.c_int32), ("k", ctypes.c_int32), ("p", ctypes.c_void_p * 4)]
+
+
+def build() -> str:
+    """Compile liboracle.so with gcc (oracle/Makefile) if it is missing or stale."""
+    src = [os.path.join(_HERE, f) for f in ("enf_oracle.c", "enf_oracle.h", "Makefile")]
+    if not os.path.exists(_LIB) or os.path.getmtime(_LIB) < max(os.path.getmtime(s) for s in src):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        _lib = ctypes.CDLL(build())
+        for S, T in (("f64", ctypes.c_double), ("f32", ctypes.c_float), ("f80", ctypes.c_longdouble)):
+            for name in ("center_stretch", "center_contract", "center_contract_ladj"):
+                f = getattr(_lib, f"or_{name}_{S}")
+                f.restype, f.argtypes = T, [T] * 4
+            for name in ("johnsontrafo", "johnsontrafo_inv", "deriv_johnsontrafo",
+                         "deriv_johnsontrafo_inv", "johnsontrafo_ladj", "johnsontrafo_inv_ladj"):
+                f = getattr(_lib, f"or_{name}_{S}")
+                f.restype, f.argtypes = T, [T] * 5
+            f = getattr(_lib, f"or_flow_apply_{S}")
+            f.restype = ctypes.c_int
+            f.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                          ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                          ctypes.POINTER(_Layer), ctypes.c_int32]
+            f = getattr(_lib, f"or_flow_apply_mt_{S}")
+            f.restype = ctypes.c_int
+            f.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                          ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                          ctypes.POINTER(_Layer), ctypes.c_int32, ctypes.c_int]
+            f = getattr(_lib, f"or_mvnormal_negll_{S}")
+            f.restype = T
+            f.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
+    return _lib
+
+
+def _sfx(dtype) -> str:
+    dt = np.dtype(dtype)
+    if dt == np.float64:
+        return "f64"
+    if dt == np.float32:
+        return "f32"
+    if dt == np.longdouble and dt.itemsize > 8:
+        return "f80"
+    raise TypeError(f"oracle supports float32/float64, got {dt}")
+
+
+def scalar(name: str, dtype, *args) -> float:
+    """Evaluate one scalar reference function, e.g. scalar('johnsontrafo', np.float64, x, g, d, xi, l)."""
+    return getattr(lib(), f"or_{name}_{_sfx(dtype)}")(*[float(np.dtype(dtype).type(a)) for a in args])
+
+
+def _layers(layers, dtype, D):
+    """layers: list of (op, params) with params a list of arrays; Householder params[0] is D x K."""
+    keep = []
+    arr = (_Layer * max(1, len(layers)))()
+    for i, (op, params) in enumerate(layers):
+        arr[i].op = op
+        arr[i].k = 0
+        for q, p in enumerate(params):
+            a = np.asfortranarray(np.asarray(p, dtype=dtype))
+            if op == OP_HOUSEHOLDER:
+                a = a.reshape(D, -1, order="F")
+                arr[i].k = a.shape[1]
+            else:
+                a = np.broadcast_to(a, (D,)).copy()
+            keep.append(a)
+            arr[i].p[q] = a.ctypes.data
+    return arr, keep
+
+
+def flow_apply(layers, X: np.ndarray, nthreads: int = 0):
+    """Apply the composed flow (layers[0] innermost) to the column-major D x N matrix X.
+
+    Returns (Y, ladj) with Y (D, N) Fortran-ordered and ladj (N,). nthreads > 0 selects the
+    OpenMP column-block variant (same arithmetic per column)."""
+    X = np.asfortranarray(X)
+    D, N = X.shape
+    Y = np.empty((D, N), dtype=X.dtype, order="F")
+    ladj = np.empty(N, dtype=X.dtype)
+    arr, keep = _layers(layers, X.dtype, D)
+    S = _sfx(X.dtype)
+    if nthreads > 0:
+        rc = getattr(lib(), f"or_flow_apply_mt_{S}")(D, N, X.ctypes.data, D, Y.ctypes.data, D,
+                                                     ladj.ctypes.data, arr, len(layers), nthreads)
+    else:
+        rc = getattr(lib(), f"or_flow_apply_{S}")(D, N, X.ctypes.data, D, Y.ctypes.data, D,
+                                                  ladj.ctypes.data, arr, len(layers))
+    if rc != 0:
+        raise ValueError("oracle: unknown op in flow")
+    del keep
+    return Y, ladj
+
+
+def flow_apply_hi(layers, X: np.ndarray, nthreads: int = 8):
+    """The same flow evaluated in higher precision on the same (rounded) inputs and parameters:
+    fp32 data in float64, fp64 data in x87 extended precision. Returned as float64; the stand-in
+    for the exact values when measuring how accurate a T-precision evaluation is."""
+    X = np.asfortranarray(X)
+    hi = np.float64 if X.dtype == np.float32 else np.longdouble
+    lay = [(op, [np.asarray(p).astype(hi) for p in ps]) for op, ps in layers]
+    Y, L = flow_apply(lay, X.astype(hi), nthreads=nthreads)
+    return np.asfortranarray(Y.astype(np.float64)), L.astype(np.float64)
+
+
+def mvnormal_negll(Y: np.ndarray, ladj: np.ndarray) -> float:
+    Y = np.asfortranarray(Y)
+    D, N = Y.shape
+    ladj = np.ascontiguousarray(ladj, dtype=Y.dtype)
+    return getattr(lib(), f"or_mvnormal_negll_{_sfx(Y.dtype)}")(D, N, Y.ctypes.data, ladj.ctypes.data)
+
+
+def inverse_layers(layers, dtype=np.float64):
+    """InverseFunctions.inverse of a composition: reversed order, each layer inverted.
+
+    ScaleShift: (1/a, -(1/a)*b) (src/scale_shift_trafo.jl:26-30); CenterStretch <-> CenterContract
+    (src/center_stretch.jl:45,69); Johnson <-> JohnsonInv (src/johnson_trafo.jl:82,107);
+    Householder: reversed columns (src/householder_trafo.jl:153-154)."""
+    out = []
+    for op, params in reversed(layers):
+        if op == OP_SCALESHIFT:
+            a = np.asarray(params[0], dtype=dtype)
+            b = np.asarray(params[1], dtype=dtype)
+            ainv = (dtype(1) / a).astype(dtype)
+            out.append((op, [ainv, (-ainv * b).astype(dtype)]))
+        elif op == OP_CENTER_STRETCH:
+            out.append((OP_CENTER_CONTRACT, params))
+        elif op == OP_CENTER_CONTRACT:
+            out.append((OP_CENTER_STRETCH, params))
+        elif op == OP_JOHNSON:
+            out.append((OP_JOHNSON_INV, params))
+        elif op == OP_JOHNSON_INV:
+            out.append((OP_JOHNSON, params))
+        elif op == OP_HOUSEHOLDER:
+            V = np.asarray(params[0], dtype=dtype)
+            V = V.reshape(V.shape[0], -1, order="F")
+            out.append((op, [np.asfortranarray(V[:, ::-1])]))
+        else:
+            raise ValueError(op)
+    return out

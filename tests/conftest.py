@@ -1,0 +1,53 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libenf.so on the device)")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import oracle as o  # test infrastructure: the checker
+
+    o.build()
+    return o
+
+
+@pytest.fixture(scope="session")
+def enf():
+    from enf_pkg import load
+
+    return load()
+
+
+@pytest.fixture(scope="session")
+def gpu(enf):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test selected but torch.cuda.is_available() is False")
+    enf._lib.lib()
+    return torch.device("cuda:0")
+
+
+def load_golden_flow(name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    layers = []
+    for i, op in enumerate(z["ops"]):
+        ps, q = [], 0
+        while f"L{i}_p{q}" in z:
+            ps.append(z[f"L{i}_p{q}"])
+            q += 1
+        layers.append((int(op), ps))
+    return layers, z["X"], z["Y_exact"], z["ladj_exact"]

@@ -1,0 +1,272 @@
+"""GPU parity: libenf.so (through the host mirror and the raw C ABI) against the oracle and the
+exact golden vectors. Tolerances and the normwise criterion: tests/parity.py."""
+import ctypes
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_golden_flow
+from parity import (RTOL, assert_as_accurate, assert_flow_close, check_vs_oracle, col_err, colmajor_cuda,
+                    ladj_err, make_flow, make_trafo, rand_params, to_np)
+
+pytestmark = pytest.mark.gpu
+
+FLOW_FIXTURES = sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, "*.npz"))
+                       if "scalars" not in f)
+
+
+@pytest.mark.parametrize("name", FLOW_FIXTURES)
+def test_golden_flow(enf, gpu, oracle, name):
+    """Every committed fixture: GPU vs the exact (mpmath) reference formulas."""
+    layers, X, Yx, Lx = load_golden_flow(name)
+    f = make_flow(enf, layers)
+    Y, L = enf.with_logabsdet_jacobian(f, colmajor_cuda(X))
+    Yt, Lt = oracle.flow_apply(layers, X)
+    assert_as_accurate(to_np(Y), to_np(L), Yt, Lt, Yx, Lx, X.dtype, what=name)
+
+
+DS = [1, 2, 3, 4, 5, 8, 16, 32, 64, 100]
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("op", range(6))
+@pytest.mark.parametrize("D", DS)
+def test_single_op_vs_oracle(enf, gpu, oracle, dtype, op, D):
+    rng = np.random.default_rng(1000 * op + D)
+    N = 4099
+    K = 3 if op == 5 else 1
+    layers = [(op, rand_params(rng, op, D, dtype, K))]
+    X = rng.standard_normal((D, N)).astype(dtype)
+    if op == 2:
+        X *= 3
+    X = np.asfortranarray(X)
+    Y, L = enf.with_logabsdet_jacobian(make_flow(enf, layers), colmajor_cuda(X))
+    check_vs_oracle(oracle, layers, X, to_np(Y), to_np(L), dtype, what=f"op{op} D{D}")
+    # plain call f(X) gives the same Y
+    Y2 = make_flow(enf, layers)(colmajor_cuda(X))
+    assert np.array_equal(to_np(Y2), to_np(Y))
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("D", [2, 32, 64])
+def test_config3_pattern_vs_oracle(enf, gpu, oracle, dtype, D):
+    """J4∘H4∘…∘J1∘H1 (SURVEY.md §8(d) config 3 pattern) on 200k samples."""
+    rng = np.random.default_rng(7 + D)
+    layers = []
+    for _ in range(4):
+        layers += [(5, rand_params(rng, 5, D, dtype)), (3, rand_params(rng, 3, D, dtype))]
+    N = 200_003
+    X = np.asfortranarray(rng.standard_normal((D, N)).astype(dtype))
+    f = make_flow(enf, layers)
+    Y, L = enf.with_logabsdet_jacobian(f, colmajor_cuda(X))
+    check_vs_oracle(oracle, layers, X, to_np(Y), to_np(L), dtype, what=f"config3 D{D}")
+    # inverse flow round trip
+    X2, L2 = enf.with_logabsdet_jacobian(enf.inverse(f), Y)
+    assert col_err(to_np(X2), X) < (1e-4 if dtype == np.float32 else 1e-11)
+    assert ladj_err(-to_np(L2), to_np(L)) < 10 * RTOL[np.dtype(dtype)]
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_mixed_ops_long_flow(enf, gpu, oracle, dtype):
+    """Every op, Householder chains with several columns, > 16 layers / > 64 steps (several launches)."""
+    rng = np.random.default_rng(99)
+    D = 8
+    layers = []
+    for i in range(20):
+        op = [5, 3, 0, 5, 2, 1, 4][i % 7]
+        layers.append((op, rand_params(rng, op, D, dtype, K=5 if op == 5 else 1)))
+    X = np.asfortranarray((0.5 * rng.standard_normal((D, 3001))).astype(dtype))
+    Y, L = enf.with_logabsdet_jacobian(make_flow(enf, layers), colmajor_cuda(X))
+    check_vs_oracle(oracle, layers, X, to_np(Y), to_np(L), dtype, what="mixed long flow")
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 31, 32, 33, 127, 128, 129, 4097])
+def test_tails(enf, gpu, oracle, N):
+    """N not a multiple of the wave tile: the masked tail path."""
+    rng = np.random.default_rng(N)
+    for D in (1, 2, 32):
+        layers = [(5, rand_params(rng, 5, D, np.float32)), (3, rand_params(rng, 3, D, np.float32))]
+        X = np.asfortranarray(rng.standard_normal((D, N)).astype(np.float32))
+        Y, L = enf.with_logabsdet_jacobian(make_flow(enf, layers), colmajor_cuda(X))
+        check_vs_oracle(oracle, layers, X, to_np(Y), to_np(L), np.float32, what=f"tail D{D} N{N}")
+
+
+def test_batched_equals_per_column(enf, gpu):
+    """test/test_johnson_trafo.jl:71-74, test/test_center_stretch.jl:64-67 (exact ==)."""
+    rng = np.random.default_rng(5)
+    for f in (enf.JohnsonTrafo([10.0, 11.0], [3.5, 3.6], [10.0, 11.0], [1.0, 1.1]),
+              enf.CenterStretch([4.0, 4.1], [2.0, 2.1], [3.0, 3.1]),
+              enf.JohnsonTrafo(np.float32([0.1, 0.2]), np.float32([1, 2]), np.float32([0, 1]), np.float32([1, 3]))):
+        X = rng.standard_normal((2, 3))
+        if isinstance(f.gamma if hasattr(f, "gamma") else f.a, np.ndarray) and f.gamma.dtype == np.float32:
+            X = X.astype(np.float32)
+        Y, L = enf.with_logabsdet_jacobian(f, colmajor_cuda(X))
+        for j in range(3):
+            y, l = enf.with_logabsdet_jacobian(f, colmajor_cuda(X)[:, j].contiguous())
+            assert np.array_equal(to_np(y), to_np(Y)[:, j])
+            assert to_np(l) == to_np(L)[0, j]
+        X2, Li = enf.with_logabsdet_jacobian(enf.inverse(f), Y)
+        assert col_err(to_np(X2), X) < 1e-5
+        assert ladj_err(to_np(Li), -to_np(L)) < 1e-5
+
+
+def test_householder_matrix_oracle(enf, gpu):
+    """test/test_householder_trafo.jl:18-25,36-43: H(v) = I - 2vv'/(v'v); chain = H_K ... H_1."""
+    rng = np.random.default_rng(3)
+    v, X, V = rng.random(5), rng.random((5, 3)), rng.random((5, 3))
+    Hm = lambda v: np.eye(5) - 2 * np.outer(v, v) / (v @ v)
+    Y = to_np(enf.HouseholderTrafo(v)(colmajor_cuda(X)))
+    assert np.allclose(Y, Hm(v) @ X, rtol=1e-13, atol=1e-14)
+    YY = to_np(enf.HouseholderTrafo(v)(colmajor_cuda(Y)))
+    assert np.allclose(YY, X, rtol=1e-13, atol=1e-14)
+    chain = Hm(V[:, 2]) @ Hm(V[:, 1]) @ Hm(V[:, 0])
+    Yc, L = enf.with_logabsdet_jacobian(enf.HouseholderTrafo(V), colmajor_cuda(X))
+    assert np.allclose(to_np(Yc), chain @ X, rtol=1e-13, atol=1e-14)
+    assert np.array_equal(to_np(L), np.zeros((1, 3)))
+    Xr = to_np(enf.inverse(enf.HouseholderTrafo(V))(Yc))
+    assert np.allclose(Xr, X, rtol=1e-13, atol=1e-14)
+    # single sample: scalar 0 ladj (householder_trafo.jl:159)
+    y, l = enf.with_logabsdet_jacobian(enf.HouseholderTrafo(V), colmajor_cuda(X)[:, 0].contiguous())
+    assert float(l) == 0.0 and np.allclose(to_np(y), chain @ X[:, 0])
+
+
+def test_vector_input_scalar_ladj(enf, gpu, oracle):
+    """test/test_johnson_trafo.jl:40-48: vector x -> (y, sum of elementwise ladjs)."""
+    import torch
+
+    x = torch.tensor([0.5, 0.6], dtype=torch.float64, device="cuda")
+    f = enf.JohnsonTrafo([4.0, 4.1], [3.0, 3.1], [2.0, 2.1], [1.0, 1.1])
+    y, l = enf.with_logabsdet_jacobian(f, x)
+    assert y.shape == (2,) and l.shape == ()
+    ref_y = [oracle.scalar("johnsontrafo", np.float64, xv, g, d, xi, lm)
+             for xv, g, d, xi, lm in zip([0.5, 0.6], [4.0, 4.1], [3.0, 3.1], [2.0, 2.1], [1.0, 1.1])]
+    ref_l = sum(oracle.scalar("johnsontrafo_ladj", np.float64, xv, g, d, xi, lm)
+                for xv, g, d, xi, lm in zip([0.5, 0.6], [4.0, 4.1], [3.0, 3.1], [2.0, 2.1], [1.0, 1.1]))
+    assert np.allclose(to_np(y), ref_y, rtol=1e-14)
+    assert abs(float(l) - ref_l) <= 1e-13 * (abs(ref_l) + 1)
+
+
+def test_promotion_and_cpu_inputs(enf, gpu):
+    """Julia promotion: float64 params on float32 data compute in float64; numpy in -> numpy out."""
+    X = np.random.default_rng(0).standard_normal((2, 10)).astype(np.float32)
+    Y, L = enf.with_logabsdet_jacobian(enf.JohnsonTrafo([1.0, 2.0], [1.0, 1.0], [0.0, 0.0], [1.0, 1.0]), X)
+    assert isinstance(Y, np.ndarray) and Y.dtype == np.float64 and L.shape == (1, 10)
+    Y32 = enf.JohnsonTrafo(np.float32([1, 2]), np.float32([1, 1]), np.float32([0, 0]), np.float32([1, 1]))(X)
+    assert Y32.dtype == np.float32
+    Yi = enf.JohnsonTrafo(4, 2, 3, 1)(X)  # Int params do not promote (test_johnson_trafo.jl:18)
+    assert Yi.dtype == np.float32
+
+
+def _raw_apply(enf, dtype, D, N, Xptr, ldx, Yptr, ldy, Lptr, acc, layers_t):
+    lib = enf._lib
+    arr = (lib.Layer * len(layers_t))()
+    for i, (op, k, ptrs) in enumerate(layers_t):
+        arr[i].op, arr[i].k = op, k
+        for q, p in enumerate(ptrs):
+            arr[i].p[q] = p
+    return lib.lib().enf_flow_apply(dtype, D, N, Xptr, ldx, Yptr, ldy, Lptr, acc, arr, len(layers_t), None)
+
+
+def test_capi_inplace_accumulate_strided(enf, gpu, oracle):
+    """C ABI: Y == X in place, accumulate_ladj, leading dimensions > D, misaligned base."""
+    import torch
+
+    rng = np.random.default_rng(11)
+    D, N = 32, 5000
+    layers = [(5, rand_params(rng, 5, D, np.float32)), (3, rand_params(rng, 3, D, np.float32))]
+    X = np.asfortranarray(rng.standard_normal((D, N)).astype(np.float32))
+    Yr, Lr = oracle.flow_apply(layers, X)
+    dev = [[torch.from_numpy(np.ascontiguousarray(np.asarray(p).reshape(D, -1, order="F").T)).cuda()
+            for p in ps] for _, ps in layers]
+    lt = [(op, (np.asarray(ps[0]).reshape(D, -1, order="F").shape[1] if op == 5 else 0), [t.data_ptr() for t in dv])
+          for (op, ps), dv in zip(layers, dev)]
+    # in place + accumulate onto 1.5
+    buf = torch.from_numpy(np.ascontiguousarray(X.T)).cuda()
+    lad = torch.full((N,), 1.5, dtype=torch.float32, device="cuda")
+    assert _raw_apply(enf, 0, D, N, buf.data_ptr(), D, buf.data_ptr(), D, lad.data_ptr(), 1, lt) == 0
+    torch.cuda.synchronize()
+    assert_flow_close(buf.cpu().numpy().T, lad.cpu().numpy() - 1.5, Yr, Lr, np.float32, what="in-place")
+    # strided: ldx = D + 3, ldy = D + 5 (generic kernel)
+    Xs = torch.zeros((N, D + 3), dtype=torch.float32, device="cuda")
+    Xs[:, :D] = torch.from_numpy(np.ascontiguousarray(X.T)).cuda()
+    Ys = torch.zeros((N, D + 5), dtype=torch.float32, device="cuda")
+    assert _raw_apply(enf, 0, D, N, Xs.data_ptr(), D + 3, Ys.data_ptr(), D + 5, lad.data_ptr(), 0, lt) == 0
+    torch.cuda.synchronize()
+    assert_flow_close(Ys[:, :D].cpu().numpy().T, lad.cpu().numpy(), Yr, Lr, np.float32, what="strided")
+    # misaligned base pointer (4 bytes off a 16-B boundary): generic kernel
+    raw = torch.zeros(N * D + 1, dtype=torch.float32, device="cuda")
+    raw[1:] = torch.from_numpy(np.ascontiguousarray(X.T)).cuda().reshape(-1)
+    Ym = torch.zeros_like(raw)
+    assert _raw_apply(enf, 0, D, N, raw.data_ptr() + 4, D, Ym.data_ptr() + 4, D, None, 0, lt) == 0
+    torch.cuda.synchronize()
+    assert col_err(Ym[1:].reshape(N, D).cpu().numpy().T, Yr) < 1e-5
+    # errors: partial overlap, bad op, N == 0 no-op
+    assert _raw_apply(enf, 0, D, N, buf.data_ptr(), D, buf.data_ptr() + 4, D, None, 0, lt) == 1
+    assert _raw_apply(enf, 0, D, N, buf.data_ptr(), D, Ys.data_ptr(), D, None, 0, [(9, 0, [0])]) == 1
+    assert _raw_apply(enf, 0, D, 0, None, D, None, D, None, 0, lt) == 0
+
+
+def test_edge_values_fp32(enf, gpu, oracle):
+    """Huge, infinite and NaN inputs follow the reference's fp32 semantics (prod-overflow rare path)."""
+    D = 4
+    vals = np.float32([0.0, -0.0, 1e-30, 1e10, -1e10, 3e19, -3e38, np.inf, -np.inf, np.nan, 5.0, -7.0])
+    N = 64
+    X = np.zeros((D, N), np.float32)
+    X.flat[: vals.size] = vals
+    X.flat[vals.size: 2 * vals.size] = vals[::-1]
+    X = np.asfortranarray(X)
+    params = [np.float32([0.1, -0.2, 0.3, 0.0]), np.float32([1, 2, 0.5, 1]), np.float32([0, 0.1, -0.1, 0]),
+              np.float32([1, 0.5, 2, 1])]
+    Yr, Lr = oracle.flow_apply([(3, params)], X)
+    Y, L = enf.with_logabsdet_jacobian(enf.JohnsonTrafo(*params), colmajor_cuda(X))
+    Y, L = to_np(Y), to_np(L).reshape(-1)
+    assert np.array_equal(np.isnan(Y), np.isnan(Yr)) and np.array_equal(np.isnan(L), np.isnan(Lr))
+    fin = np.isfinite(Yr)
+    assert np.array_equal(np.isinf(Y), np.isinf(Yr)) and np.all(np.sign(Y[~fin & ~np.isnan(Yr)]) ==
+                                                                 np.sign(Yr[~fin & ~np.isnan(Yr)]))
+    assert col_err(np.where(fin, Y, 0), np.where(fin, Yr, 0)) < 1e-5
+    finl = np.isfinite(Lr)
+    assert np.array_equal(np.isinf(L), np.isinf(Lr))
+    assert ladj_err(L[finl], Lr[finl]) < 1e-5
+
+
+def test_zero_samples_and_empty_flow(enf, gpu):
+    import torch
+
+    X = torch.zeros((3, 0), dtype=torch.float32, device="cuda")
+    Y, L = enf.with_logabsdet_jacobian(enf.JohnsonTrafo(np.float32([1, 1, 1]), 1, 0, 1), X)
+    assert Y.shape == (3, 0) and L.shape == (1, 0)
+
+
+def test_full_size_round_trip_config3(enf, gpu):
+    """Config 3 at full size (D=32, N=1e7, fp32): size-independent properties -- inverse(f)(f(X)) == X
+    and ladj(inverse) == -ladj -- plus oracle parity on a strided sample of columns."""
+    import torch
+
+    import oracle as orc
+
+    rng = np.random.default_rng(2026)
+    D, N = 32, 10_000_000
+    layers = []
+    for _ in range(4):
+        layers += [(5, rand_params(rng, 5, D, np.float32)), (3, rand_params(rng, 3, D, np.float32))]
+    f = make_flow(enf, layers)
+    g = torch.Generator(device="cuda").manual_seed(0x5EED)
+    X = torch.randn((N, D), generator=g, device="cuda", dtype=torch.float32).t()
+    Y, L = enf.with_logabsdet_jacobian(f, X)
+    X2, L2 = enf.with_logabsdet_jacobian(enf.inverse(f), Y)
+    # round trip, checked on the GPU in chunks to bound host memory
+    worst = 0.0
+    for c0 in range(0, N, 1_000_000):
+        a, b = X[:, c0:c0 + 1_000_000], X2[:, c0:c0 + 1_000_000]
+        scale = a.abs() + a.abs().amax(dim=0, keepdim=True)
+        worst = max(worst, float(((b - a).abs() / scale).max()))
+    assert worst < 1e-4, worst
+    el = float(((L2 + L).abs() / (L.abs() + 1)).max())
+    assert el < 1e-5, el
+    idx = np.arange(0, N, 997)
+    Xs = np.asfortranarray(X[:, idx].cpu().numpy())
+    check_vs_oracle(orc, layers, Xs, Y[:, idx].cpu().numpy(), L[0, idx].cpu().numpy(), np.float32,
+                    what="config3 sample")
