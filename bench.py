@@ -28,14 +28,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICRO
 MFMA_NOTE = "elementwise/rank-1 maps: HBM roofline (SURVEY.md §8(d))"
 
 
-def build_flow(D, pairs, np_dtype, seed=42):
-    """Parameters from a host RNG with seed 42 in per-layer order."""
+def build_flow(D, pairs, np_dtype, seed=42, pattern=None):
+    """Parameters from a host RNG with seed 42 in per-layer order.
+    pattern: layer letters applied in order (H = Householder, J = Johnson); default "HJ" * pairs."""
     rng = np.random.default_rng(seed)
     layers = []
-    for _ in range(pairs):
-        layers.append((5, [rng.standard_normal(D).astype(np_dtype)]))
-        layers.append((3, [rng.uniform(-1, 1, D).astype(np_dtype), rng.uniform(0.5, 2, D).astype(np_dtype),
-                           rng.uniform(-0.5, 0.5, D).astype(np_dtype), rng.uniform(0.5, 2, D).astype(np_dtype)]))
+    for ch in (pattern or "HJ" * pairs):
+        if ch == "H":
+            layers.append((5, [rng.standard_normal(D).astype(np_dtype)]))
+        elif ch == "J":
+            layers.append((3, [rng.uniform(-1, 1, D).astype(np_dtype), rng.uniform(0.5, 2, D).astype(np_dtype),
+                               rng.uniform(-0.5, 0.5, D).astype(np_dtype), rng.uniform(0.5, 2, D).astype(np_dtype)]))
+        else:
+            raise ValueError(f"unknown layer letter {ch!r}")
     return layers
 
 
@@ -50,6 +55,7 @@ def main():
     ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-samples", type=int, default=3_000_000)
+    ap.add_argument("--pattern", default=None, help="diagnostic layer pattern, e.g. HHHHHHHH (overrides --pairs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -72,7 +78,7 @@ def main():
     t_dtype = torch.float32 if args.dtype == "f32" else torch.float64
     esz = 4 if args.dtype == "f32" else 8
     D, N = args.D, args.N
-    layers = build_flow(D, args.pairs, np_dtype)
+    layers = build_flow(D, args.pairs, np_dtype, pattern=args.pattern)
 
     # synthetic X: N(0,1) columns from torch's counter-based (Philox) CUDA generator; each rank
     # draws its own shard (global column offset = rank * N)
@@ -155,9 +161,9 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic: X ~ N(0,1) (torch Philox, seed 0x5EED+rank); params seed 42",
-            "config": {"workload": f"{'∘'.join(['J','H'] * args.pairs)} composed flow fwd+ladj, "
-                                   f"D={D}, N={N} per GPU ({args.pairs} Householder + {args.pairs} Johnson)",
-                       "D": D, "N_per_gpu": N, "layers": 2 * args.pairs, "parallelism": f"sample-shard x{world}"},
+            "config": {"workload": f"{'∘'.join(reversed(args.pattern or 'HJ' * args.pairs))} composed flow "
+                                   f"fwd+ladj, D={D}, N={N} per GPU",
+                       "D": D, "N_per_gpu": N, "layers": len(layers), "parallelism": f"sample-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": kern_ms, "kernel_ms_max_rank": kern_ms_max,

@@ -218,6 +218,7 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
   }
 
   // cut into launches bounded by the kernarg tables and the LDS parameter budget
+  const bool frag = enf::frag_path(D, ldx, ldy, X, Y) && enf::frag_path(D, ldy, ldy, Y, Y);
   size_t i = 0;
   bool first = true;
   while (i < steps.size()) {
@@ -225,11 +226,12 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
     std::memset(&a, 0, sizeof a);
     a.D = (int32_t)D;
     a.N = N;
+    a.frag = frag ? 1 : 0;
     size_t recs = 0;
     int last_layer = -1;
     while (i < steps.size() && a.nsteps < enf::kMaxSteps) {
       const S& s = steps[i];
-      const size_t w = (size_t)enf::record_width_host(s.op) * (size_t)D * elem;
+      const size_t w = enf::record_elems(s.op, D, elem, frag) * elem;
       const bool new_layer = s.layer != last_layer;
       if (new_layer && a.nlayers >= enf::kMaxLayers) break;
       if (recs + w > enf::kLdsParamBudget) {
@@ -249,6 +251,7 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
       t.layer = a.nlayers - 1;
       t.col = s.col;
       t.off = (int32_t)(recs / elem);
+      a.desc[a.nsteps - 1] = t.op | (t.off << 4);
       recs += w;
       ++i;
     }

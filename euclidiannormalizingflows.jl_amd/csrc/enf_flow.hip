@@ -81,8 +81,9 @@ __device__ __forceinline__ T group_sum(T x) {
 }
 
 // ------------------------------------------------------------------------------------------
-// parameter records in LDS: record width W(op) values of T per row, rows contiguous
+// parameter records in LDS
 // ------------------------------------------------------------------------------------------
+// A step's record holds W(op) parameter values per row (enf_internal.h record_width):
 //  fp32                                              fp64
 //  HOUSEHOLDER  W=1 {v_d * sqrt(2/v'v)}              same
 //  SCALESHIFT   W=2 {a, b}                           same
@@ -90,17 +91,69 @@ __device__ __forceinline__ T group_sum(T x) {
 //  JOHNSON_INV  W=4 {gamma, 1/delta, xi, lambda}     {gamma, delta, xi, lambda}
 //  CENTER_*     W=8 {b*log2e, c, ln2/b, exp(b*a),    {a, b, c, 0, ...}
 //                    exp(2*b*a), b*a*log2e, a, b}
+// Layout: [group g][param q][element e] with RV elements per group; element (g, e) is row
+// g*RV + e (D >= RV) or e % D (D < RV). The fragment kernel uses RV = V = 16/sizeof(T), so a
+// lane reads each parameter of its V rows with ONE 16-byte LDS read; the generic kernel uses
+// RV = 1 (row-major records). Size: W * max(D, RV) values (enf_internal.h record_elems).
+template <typename T>
+__device__ __forceinline__ void param_values(int op, const LayerDesc& L, int col, int D, int row, double hscale,
+                                             T (&out)[8]) {
+  if (op == OP_HOUSEHOLDER) {
+    out[0] = (T)((double)((const T*)L.p[0])[(int64_t)col * D + row] * hscale);
+  } else if (op == OP_SCALESHIFT) {
+    out[0] = ((const T*)L.p[0])[row];
+    out[1] = ((const T*)L.p[1])[row];
+  } else if (op == OP_JOHNSON || op == OP_JOHNSON_INV) {
+    const T g = ((const T*)L.p[0])[row], de = ((const T*)L.p[1])[row];
+    const T xi = ((const T*)L.p[2])[row], la = ((const T*)L.p[3])[row];
+    out[0] = g;
+    out[2] = xi;
+    if constexpr (std::is_same_v<T, float>) {
+      if (op == OP_JOHNSON) {
+        out[1] = (float)((double)de * kLn2);
+        out[3] = (float)(1.0 / (double)la);
+      } else {
+        out[1] = (float)(1.0 / (double)de);
+        out[3] = la;
+      }
+    } else {
+      out[1] = de;
+      out[3] = la;
+    }
+  } else {  // CENTER_STRETCH / CENTER_CONTRACT
+    const T av = ((const T*)L.p[0])[row], bv = ((const T*)L.p[1])[row], cv = ((const T*)L.p[2])[row];
+    if constexpr (std::is_same_v<T, float>) {
+      const double b = bv, aa = av;
+      out[0] = (float)(b * kLog2e);
+      out[1] = cv;
+      out[2] = (float)(kLn2 / b);
+      out[3] = expf(bv * av);         // exp(b*a) in T, as the reference (center_stretch.jl:7)
+      out[4] = expf(2.0f * bv * av);  // exp(2*b*a)
+      out[5] = (float)(b * aa * kLog2e);
+      out[6] = av;  // raw a, b for the generic kernel
+      out[7] = bv;
+    } else {
+      out[0] = av;
+      out[1] = bv;
+      out[2] = cv;
+      for (int q = 3; q < 8; ++q) out[q] = 0.0;
+    }
+  }
+}
 
-// Per-step constant ladj contribution (natural log units), over all D rows; computed in double.
-// Block prologue: one wave per step, rows over lanes, shuffle reduction.
-template <typename T, int DC>
+// Block prologue: one wave per step. Pass 1 reduces over the D distinct rows (v'v for a
+// reflection; the constant ladj part sum log|delta/lambda|, sum log|a| in double); pass 2 writes
+// the records in the layout above. ctot = sum of the per-step constants (natural log).
+template <typename T, int DC, int RV>
 __device__ void build_program(const FlowArgs& a, T* __restrict__ rec, double* __restrict__ stepc,
                               double* __restrict__ ctot) {
   const int D = DC > 0 ? DC : a.D;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int nent = D > RV ? D : RV;  // record entries per parameter
   for (int s = wave; s < a.nsteps; s += nw) {
     const Step st = a.steps[s];
     const LayerDesc& L = a.layers[st.layer];
+    const int W = record_width(st.op);
     T* r = rec + st.off;
     double part = 0.0;
     for (int d = lane; d < D; d += 64) {
@@ -108,65 +161,25 @@ __device__ void build_program(const FlowArgs& a, T* __restrict__ rec, double* __
         const double v = (double)((const T*)L.p[0])[(int64_t)st.col * D + d];
         part += v * v;
       } else if (st.op == OP_SCALESHIFT) {
-        const T av = ((const T*)L.p[0])[d], bv = ((const T*)L.p[1])[d];
-        r[2 * d] = av;
-        r[2 * d + 1] = bv;
-        part += log(fabs((double)av));
+        part += log(fabs((double)((const T*)L.p[0])[d]));  // scale_shift_trafo.jl:22
       } else if (st.op == OP_JOHNSON || st.op == OP_JOHNSON_INV) {
-        const T g = ((const T*)L.p[0])[d], de = ((const T*)L.p[1])[d];
-        const T xi = ((const T*)L.p[2])[d], la = ((const T*)L.p[3])[d];
-        if constexpr (std::is_same_v<T, float>) {
-          if (st.op == OP_JOHNSON) {
-            r[4 * d + 0] = g;
-            r[4 * d + 1] = (float)((double)de * kLn2);
-            r[4 * d + 2] = xi;
-            r[4 * d + 3] = (float)(1.0 / (double)la);
-          } else {
-            r[4 * d + 0] = g;
-            r[4 * d + 1] = (float)(1.0 / (double)de);
-            r[4 * d + 2] = xi;
-            r[4 * d + 3] = la;
-          }
-        } else {
-          r[4 * d + 0] = g;
-          r[4 * d + 1] = de;
-          r[4 * d + 2] = xi;
-          r[4 * d + 3] = la;
-        }
         // log|delta/lambda| (johnson_trafo.jl:41,51); the inverse negates (johnson_trafo.jl:104)
-        const double c = log(fabs((double)de)) - log(fabs((double)la));
+        const double c = log(fabs((double)((const T*)L.p[1])[d])) - log(fabs((double)((const T*)L.p[3])[d]));
         part += st.op == OP_JOHNSON ? c : -c;
-      } else {  // CENTER_STRETCH / CENTER_CONTRACT
-        const T av = ((const T*)L.p[0])[d], bv = ((const T*)L.p[1])[d], cv = ((const T*)L.p[2])[d];
-        if constexpr (std::is_same_v<T, float>) {
-          const double b = bv, aa = av;
-          r[8 * d + 0] = (float)(b * kLog2e);
-          r[8 * d + 1] = cv;
-          r[8 * d + 2] = (float)(kLn2 / b);
-          r[8 * d + 3] = expf(bv * av);                  // exp(b*a) in T, as the reference
-          r[8 * d + 4] = expf(2.0f * bv * av);           // exp(2*b*a)
-          r[8 * d + 5] = (float)(b * aa * kLog2e);
-          r[8 * d + 6] = av;  // raw a, b for the generic kernel
-          r[8 * d + 7] = bv;
-        } else {
-          r[8 * d + 0] = av;
-          r[8 * d + 1] = bv;
-          r[8 * d + 2] = cv;
-          for (int q = 3; q < 8; ++q) r[8 * d + q] = 0.0;
-        }
       }
     }
-    // wave reduction of `part`
     for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m);
-    if (st.op == OP_HOUSEHOLDER) {
-      // normalised reflection: H x = x - vh (vh'x), vh = v*sqrt(2/v'v) (householder_trafo.jl:9-10)
-      const double sc = sqrt(2.0 / part);
-      for (int d = lane; d < D; d += 64)
-        r[d] = (T)((double)((const T*)L.p[0])[(int64_t)st.col * D + d] * sc);
-      if (lane == 0) stepc[s] = 0.0;
-    } else {
-      if (lane == 0) stepc[s] = (st.op == OP_CENTER_STRETCH || st.op == OP_CENTER_CONTRACT) ? 0.0 : part;
+    // normalised reflection: H x = x - vh (vh'x), vh = v*sqrt(2/v'v) (householder_trafo.jl:9-10)
+    const double hscale = st.op == OP_HOUSEHOLDER ? sqrt(2.0 / part) : 0.0;
+    for (int i = lane; i < nent; i += 64) {
+      const int g = D >= RV ? i / RV : 0, e = i % RV;
+      const int row = D >= RV ? i : e % D;
+      T vals[8];
+      param_values<T>(st.op, L, st.col, D, row, hscale, vals);
+      for (int q = 0; q < W; ++q) r[(g * W + q) * RV + e] = vals[q];
     }
+    if (lane == 0)
+      stepc[s] = (st.op == OP_HOUSEHOLDER || st.op == OP_CENTER_STRETCH || st.op == OP_CENTER_CONTRACT) ? 0.0 : part;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -193,8 +206,7 @@ struct Unit<double> { static constexpr double v = 1.0; };
 // exactly where the reference's fp32 `1 + ((x-xi)/lambda)^2` does (johnson_trafo.jl:41), so
 // the ladj is -Inf there, as in the reference.
 struct YL { float y, l; };
-__device__ __forceinline__ YL johnson_fwd_f32_slow(float x, float g, float d2, float xi, float il) {
-  const float z = (x - xi) * il;
+__device__ __forceinline__ YL johnson_fwd_f32_slow(float z, float g, float d2) {
   const float t = fabsf(z);
   const float q = fmaf(z, z, 1.0f);
   const float L = t > 1e18f ? hw_log2(t) + 1.0f : hw_log2(t + hw_sqrt(q));  // log2(2|z|) when huge
@@ -243,15 +255,57 @@ __device__ __forceinline__ void load_tile(const FlowArgs& a, int64_t col0, T (&x
   }
 }
 
-template <typename T, int D, int U, bool LADJ, bool TAIL>
+// 16-byte LDS read of V parameter values
+template <typename T, int V>
+__device__ __forceinline__ void lds_vec(const T* __restrict__ p, T (&v)[V]) {
+  static_assert(V * sizeof(T) == 16, "16-byte vectors");
+  const u32x4 w = *reinterpret_cast<const u32x4*>(p);
+  __builtin_memcpy(&v[0], &w, 16);
+}
+
+// Run the step program on one wave tile held in registers (x), then store Y and ladj.
+// ladj output of a wave tile. G == 1: a lane owns whole columns (CPF per fragment) and stores
+// them as one CPF-vector per fragment. G > 1: column totals are staged through the wave's LDS
+// slots and written by NLS = ceil(TC/64) full-wave stores (TC = columns per tile; when TC < 64
+// the upper lanes store duplicates of the same values to the same addresses, so no lane mask
+// and no branch is needed: the vmcnt accounting of the tile loop stays static).
+template <typename T, int D, int U>
+struct LadjOut {
+  using F = Frag<T, D>;
+  static constexpr int TC = F::COLS_PER_INSTR * U;
+  static constexpr int NLS = F::G == 1 ? U : (TC + 63) / 64;
+  static constexpr int W = F::G == 1 ? F::CPF : 1;  // values per lane per store
+  __device__ static __forceinline__ int64_t col(int64_t col0, int k, int lane) {
+    if constexpr (F::G == 1) return frag_col<T, D>(col0, k, lane);
+    else return col0 + (int64_t)k * 64 + (TC >= 64 ? lane : lane % TC);
+  }
+};
+
+// LM: 0 no ladj, 1 write ladj, 2 add to ladj (accumulate_ladj)
+template <typename T, int D, int U, int LM>
+__device__ __forceinline__ void load_ladj_old(const FlowArgs& a, int64_t col0, T (&old)[LadjOut<T, D, U>::NLS][LadjOut<T, D, U>::W]) {
+  using LO = LadjOut<T, D, U>;
+  const int lane = threadIdx.x & 63;
+  const T* __restrict__ ladj = (const T*)a.ladj;
+#pragma unroll
+  for (int k = 0; k < LO::NLS; ++k)
+#pragma unroll
+    for (int w = 0; w < LO::W; ++w) old[k][w] = LM == 2 ? ladj[LO::col(col0, k, lane) + w] : (T)0;
+}
+
+template <typename T, int D, int U, int LM, bool TAIL>
 __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict__ rec, T ctot,
-                                          int64_t col0, T (&x)[U][Frag<T, D>::V]) {
+                                          int64_t col0, T (&x)[U][Frag<T, D>::V],
+                                          const T (&old)[LadjOut<T, D, U>::NLS][LadjOut<T, D, U>::W],
+                                          T* __restrict__ stage) {
+  constexpr bool LADJ = LM > 0;
   using F = Frag<T, D>;
   constexpr int V = F::V, G = F::G, CPF = F::CPF, SEG = F::SEG;
   const int lane = threadIdx.x & 63;
   T* __restrict__ Y = (T*)a.Y;
   const int64_t N = a.N;
   const int r0 = D >= V ? V * (lane % G) : 0;
+  const int grp = D >= V ? lane % G : 0;  // parameter-record group of this lane
   int64_t colf[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) colf[u] = frag_col<T, D>(col0, u, lane);
@@ -260,14 +314,22 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int c = 0; c < CPF; ++c) acc[u][c] = (T)0;
+  // make the vmcnt wait for THIS tile's loads happen here, with the next tile's loads still in
+  // flight (inside the runtime step loop the compiler would otherwise drain vmcnt to 0)
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < V; ++e) asm volatile("" : "+v"(x[u][e]));
 
+  int desc = a.desc[0];  // op | record offset << 4; a.desc[nsteps] is a sentinel
   for (int s = 0; s < a.nsteps; ++s) {
-    const int op = a.steps[s].op;  // kernarg -> SGPR, uniform branch
-    const T* __restrict__ r = rec + a.steps[s].off;
+    const int next = a.desc[s + 1];  // scalar load issued a step ahead
+    const int op = desc & 15;
+    const T* __restrict__ r = rec + (desc >> 4) + grp * record_width(op) * V;
+    desc = next;
     if (op == OP_HOUSEHOLDER) {
       T vh[V];
-#pragma unroll
-      for (int e = 0; e < V; ++e) vh[e] = r[r0 + e % SEG];
+      lds_vec<T, V>(r, vh);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -282,60 +344,70 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
       }
     } else if (op == OP_JOHNSON) {
       T pg[V], pd[V], px[V], pl[V];
+      lds_vec<T, V>(r, pg);
+      lds_vec<T, V>(r + V, pd);
+      lds_vec<T, V>(r + 2 * V, px);
+      lds_vec<T, V>(r + 3 * V, pl);
+      if constexpr (std::is_same_v<T, float>) {
+        // y = gamma + delta*asinh(z), asinh|z| = ln2*log2(|z| + sqrt(1+z^2))  (johnson_trafo.jl:31)
+        // ladj: log|delta/lambda| - log(1+z^2)/2, one log2 of the product of the q = 1+z^2 of a
+        // fragment's rows                                                    (johnson_trafo.jl:41,51)
+        // Pass 1: z for the whole tile (in place) and its largest |z|; the product of <= 4 q stays
+        // finite for |z| <= 2^15, larger or infinite |z| take the exact elementwise path (one
+        // uniform branch per tile, so the fast path interleaves all U*V elements). NaN needs no
+        // special path: it propagates through the fast formulas as through the reference's.
+        float zmax = 0.f;
 #pragma unroll
-      for (int e = 0; e < V; ++e) {
-        const int row = r0 + e % SEG;
-        pg[e] = r[4 * row + 0]; pd[e] = r[4 * row + 1]; px[e] = r[4 * row + 2]; pl[e] = r[4 * row + 3];
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if constexpr (std::is_same_v<T, float>) {
-          // y = gamma + delta*asinh(z), asinh|z| = ln2*log2(|z| + sqrt(1+z^2))  (johnson_trafo.jl:31)
-          // ladj: log|delta/lambda| - log(1+z^2)/2                                (johnson_trafo.jl:41,51)
-          float xin[V];
-          float prod[CPF];
-#pragma unroll
-          for (int c = 0; c < CPF; ++c) prod[c] = 1.0f;
+        for (int u = 0; u < U; ++u)
 #pragma unroll
           for (int e = 0; e < V; ++e) {
-            xin[e] = x[u][e];
-            const float z = (x[u][e] - px[e]) * pl[e];
-            const float q = fmaf(z, z, 1.0f);
-            const float L = hw_log2(fabsf(z) + hw_sqrt(q));
-            x[u][e] = fmaf(pd[e], copysignf(L, z), pg[e]);
-            prod[e / SEG] *= q;
+            x[u][e] = (x[u][e] - px[e]) * pl[e];
+            zmax = fmaxf(zmax, fabsf(x[u][e]));
           }
-          // prod overflows (|z| >~ 1e9), or a non-finite input: exact elementwise rare path
-          bool bad = false;
+        if (__builtin_expect(!(zmax <= 32768.f), 0)) {
 #pragma unroll
-          for (int c = 0; c < CPF; ++c) bad |= !(prod[c] <= FLT_MAX);
-          if (__builtin_expect(bad, 0)) {
+          for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int e = 0; e < V; ++e) {
-              const YL r2 = johnson_fwd_f32_slow(xin[e], pg[e], pd[e], px[e], pl[e]);
+              const YL r2 = johnson_fwd_f32_slow(x[u][e], pg[e], pd[e]);
               x[u][e] = r2.y;
               if (LADJ) acc[u][e / SEG] += r2.l;
             }
-          } else if (LADJ) {
-#pragma unroll
-            for (int c = 0; c < CPF; ++c) acc[u][c] = fmaf(-0.5f, hw_log2(prod[c]), acc[u][c]);
-          }
         } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            float prod[CPF];
+#pragma unroll
+            for (int c = 0; c < CPF; ++c) prod[c] = 1.0f;
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+              const float z = x[u][e];
+              const float q = fmaf(z, z, 1.0f);
+              const float L = hw_log2(fabsf(z) + hw_sqrt(q));
+              x[u][e] = fmaf(pd[e], copysignf(L, z), pg[e]);
+              prod[e / SEG] *= q;
+            }
+            if (LADJ)
+#pragma unroll
+              for (int c = 0; c < CPF; ++c) acc[u][c] = fmaf(-0.5f, hw_log2(prod[c]), acc[u][c]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
 #pragma unroll
           for (int e = 0; e < V; ++e) {
             const double z = (x[u][e] - px[e]) / pl[e];
             x[u][e] = pg[e] + pd[e] * asinh(z);
             if (LADJ) acc[u][e / SEG] -= 0.5 * log1p(z * z);
           }
-        }
       }
     } else if (op == OP_JOHNSON_INV) {
       T pg[V], pd[V], px[V], pl[V];
-#pragma unroll
-      for (int e = 0; e < V; ++e) {
-        const int row = r0 + e % SEG;
-        pg[e] = r[4 * row + 0]; pd[e] = r[4 * row + 1]; px[e] = r[4 * row + 2]; pl[e] = r[4 * row + 3];
-      }
+      lds_vec<T, V>(r, pg);
+      lds_vec<T, V>(r + V, pd);
+      lds_vec<T, V>(r + 2 * V, px);
+      lds_vec<T, V>(r + 3 * V, pl);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -355,8 +427,7 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
             if (LADJ) acc[u][e / SEG] = fmaf(0.5f, hw_log2(fmaf(sh, sh, 1.0f)), acc[u][e / SEG]);
           } else {
             const double w = (x[u][e] - pg[e]) / pd[e];
-            const double sh = sinh(w);
-            const double xo = pl[e] * sh + px[e];
+            const double xo = pl[e] * sinh(w) + px[e];
             x[u][e] = xo;
             if (LADJ) {  // from the output, as the reference: log(1 + ((x_out - xi)/lambda)^2)/2
               const double z = (xo - px[e]) / pl[e];
@@ -367,23 +438,24 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
       }
     } else if (op == OP_SCALESHIFT) {
       // y = muladd(x, a, b) (scale_shift_trafo.jl:16); ladj = sum log|a| (constant, in ctot)
+      T pa[V], pb[V];
+      lds_vec<T, V>(r, pa);
+      lds_vec<T, V>(r + V, pb);
 #pragma unroll
-      for (int e = 0; e < V; ++e) {
-        const int row = r0 + e % SEG;
-        const T av = r[2 * row], bv = r[2 * row + 1];
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int u = 0; u < U; ++u) x[u][e] = fma(x[u][e], av, bv);
-      }
+        for (int e = 0; e < V; ++e) x[u][e] = fma(x[u][e], pa[e], pb[e]);
     } else if (op == OP_CENTER_STRETCH) {
+      T rr[8][V];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) lds_vec<T, V>(r + q * V, rr[q]);
 #pragma unroll
       for (int e = 0; e < V; ++e) {
-        const int row = r0 + e % SEG;
-        const T* rr = r + 8 * row;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           if constexpr (std::is_same_v<T, float>) {
             // center_stretch.jl:4-8 with e = exp(|b x|); ladj = -contract_ladj(y) (:41-42)
-            const float bl = rr[0], c = rr[1], lnb = rr[2], E1 = rr[3], E2 = rr[4], bal = rr[5];
+            const float bl = rr[0][e], c = rr[1][e], lnb = rr[2][e], E1 = rr[3][e], E2 = rr[4][e], bal = rr[5][e];
             const float xv = x[u][e];
             const float ex = hw_exp2(fabsf(xv * bl));
             const float ome = 1.0f - ex;
@@ -401,7 +473,7 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
               acc[u][e / SEG] -= hw_log2(fabsf(dy));
             }
           } else {
-            const double av = rr[0], bv = rr[1], c = rr[2];
+            const double av = rr[0][e], bv = rr[1][e], c = rr[2][e];
             const double xv = x[u][e];
             const double ex = exp(fabs(bv * xv));
             const double ome = 1.0 - ex;
@@ -418,15 +490,16 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
         }
       }
     } else {  // OP_CENTER_CONTRACT
+      T rr[8][V];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) lds_vec<T, V>(r + q * V, rr[q]);
 #pragma unroll
       for (int e = 0; e < V; ++e) {
-        const int row = r0 + e % SEG;
-        const T* rr = r + 8 * row;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           if constexpr (std::is_same_v<T, float>) {
             // center_stretch.jl:11-15; ladj = contract_ladj(x) (:17-22, :65)
-            const float bl = rr[0], c = rr[1], lnb = rr[2], bal = rr[5];
+            const float bl = rr[0][e], c = rr[1][e], lnb = rr[2][e], bal = rr[5][e];
             const float xu = x[u][e] - c;
             const float e1 = hw_exp2(fmaf(bl, xu, -bal));   // exp(b(xu - a))
             const float e2 = hw_exp2(fmaf(-bl, xu, -bal));  // exp(-b(xu + a))
@@ -438,7 +511,7 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
               acc[u][e / SEG] += hw_log2(fabsf(dy));
             }
           } else {
-            const double av = rr[0], bv = rr[1], c = rr[2];
+            const double av = rr[0][e], bv = rr[1][e], c = rr[2][e];
             const double xu = x[u][e] - c;
             x[u][e] = (log(1.0 + exp(bv * (xu - av))) - log(1.0 + exp(-bv * (xu + av)))) / bv;
             if (LADJ) {
@@ -465,54 +538,103 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
         if (colf[u] + e / SEG < N) Y[eoff + e] = x[u][e];
     }
   }
-  if (LADJ) {
+  if constexpr (LADJ) {
+    using LO = LadjOut<T, D, U>;
     T* __restrict__ ladj = (T*)a.ladj;
+    if constexpr (G == 1) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+      for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int c = 0; c < CPF; ++c) {
-        const T tot = group_sum<G>(acc[u][c]);
-        const int64_t col = colf[u] + c;
-        if ((lane % G) == 0 && (!TAIL || col < N)) {
-          const T v = fma(Unit<T>::v, tot, ctot);
-          ladj[col] = a.accumulate ? ladj[col] + v : v;
+        for (int c = 0; c < CPF; ++c) {
+          const int64_t col = colf[u] + c;
+          const T v = fma(Unit<T>::v, acc[u][c], ctot) + old[u][c];
+          if (!TAIL) ladj[col] = v;
+          else if (col < N) ladj[col] = v;
         }
+      }
+    } else {
+      // group totals -> the wave's LDS slots (leaders only) -> full-wave coalesced stores
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const T tot = group_sum<G>(acc[u][0]);
+        if ((lane % G) == 0) stage[u * F::COLS_PER_INSTR + lane / G] = tot;
+      }
+#pragma unroll
+      for (int k = 0; k < LO::NLS; ++k) {
+        const int c = k * 64 + (LO::TC >= 64 ? lane : lane % LO::TC);
+        const T v = fma(Unit<T>::v, stage[c], ctot) + old[k][0];
+        const int64_t col = col0 + c;
+        if (!TAIL) ladj[col] = v;
+        else if (col < N) ladj[col] = v;
       }
     }
   }
 }
 
-template <typename T, int D, int U, bool LADJ>
-__global__ __launch_bounds__(256) void flow_frag_kernel(FlowArgs a) {
+// OCC: minimum waves per SIMD the register allocation must allow (launch-bounds occupancy hint)
+template <typename T, int D, int U, int LM, int OCC>
+__global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* stepc = reinterpret_cast<double*>(smem);
   double* ctotp = stepc + kMaxSteps;
+  T* stage = reinterpret_cast<T*>(smem + kLdsScalars) + (threadIdx.x >> 6) * kStagePerWave;
   T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
-  build_program<T, D>(a, rec, stepc, ctotp);
+  build_program<T, D, Frag<T, D>::V>(a, rec, stepc, ctotp);
   const T ctot = (T)*ctotp;
 
   using F = Frag<T, D>;
+  using LO = LadjOut<T, D, U>;
+  static_assert(F::G == 1 || LO::TC <= kStagePerWave, "ladj staging area too small");
   constexpr int64_t COLS_PER_TILE = (int64_t)F::COLS_PER_INSTR * U;
   const int64_t ntiles_full = a.N / COLS_PER_TILE;
-  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  // wave-uniform tile indices (readfirstlane: scalar registers, uniform branches)
+  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) +
+                          __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  // software pipeline: the next tile's loads are in flight while this tile computes
+  // software pipeline: the next tile's loads are in flight while this tile computes. Memory
+  // operations per iteration are branch-free and in a fixed order (old ladj, prefetch, stores):
+  // past the last tile the prefetch re-reads the current tile instead of being skipped, so the
+  // compiler's vmcnt waits only ever cover the current tile.
+  // The first half-iteration is peeled so that the loop header is reached from the entry and from
+  // the back edge with the same outstanding memory operations (the previous tile's stores behind
+  // the current tile's loads): the compiler's static vmcnt waits then leave the stores in flight.
   using XT = T[U][F::V];
+  using OT = T[LO::NLS][LO::W];
   XT xa, xb;
-  int64_t t = wave_id;
-  if (t < ntiles_full) load_tile<T, D, U, false>(a, t * COLS_PER_TILE, xa);
-  for (; t < ntiles_full; t += 2 * nwaves) {
-    const int64_t t1 = t + nwaves;
-    if (t1 < ntiles_full) load_tile<T, D, U, false>(a, t1 * COLS_PER_TILE, xb);
-    flow_tile<T, D, U, LADJ, false>(a, rec, ctot, t * COLS_PER_TILE, xa);
-    if (t1 >= ntiles_full) break;
-    const int64_t t2 = t1 + nwaves;
-    if (t2 < ntiles_full) load_tile<T, D, U, false>(a, t2 * COLS_PER_TILE, xa);
-    flow_tile<T, D, U, LADJ, false>(a, rec, ctot, t1 * COLS_PER_TILE, xb);
+  OT old;
+  const int64_t t = wave_id;
+  if (t < ntiles_full) {
+    load_tile<T, D, U, false>(a, t * COLS_PER_TILE, xa);
+    int64_t t1 = t + nwaves;
+    load_ladj_old<T, D, U, LM>(a, t * COLS_PER_TILE, old);
+    load_tile<T, D, U, false>(a, (t1 < ntiles_full ? t1 : t) * COLS_PER_TILE, xb);
+    flow_tile<T, D, U, LM, false>(a, rec, ctot, t * COLS_PER_TILE, xa, old, stage);
+    while (t1 < ntiles_full) {
+      const int64_t t2 = t1 + nwaves;
+      load_ladj_old<T, D, U, LM>(a, t1 * COLS_PER_TILE, old);
+      load_tile<T, D, U, false>(a, (t2 < ntiles_full ? t2 : t1) * COLS_PER_TILE, xa);
+      flow_tile<T, D, U, LM, false>(a, rec, ctot, t1 * COLS_PER_TILE, xb, old, stage);
+      if (t2 >= ntiles_full) break;
+      const int64_t t3 = t2 + nwaves;
+      load_ladj_old<T, D, U, LM>(a, t2 * COLS_PER_TILE, old);
+      load_tile<T, D, U, false>(a, (t3 < ntiles_full ? t3 : t2) * COLS_PER_TILE, xb);
+      flow_tile<T, D, U, LM, false>(a, rec, ctot, t2 * COLS_PER_TILE, xa, old, stage);
+      t1 = t3;
+    }
   }
   if (ntiles_full * COLS_PER_TILE < a.N && wave_id == ntiles_full % nwaves) {
-    load_tile<T, D, U, true>(a, ntiles_full * COLS_PER_TILE, xa);
-    flow_tile<T, D, U, LADJ, true>(a, rec, ctot, ntiles_full * COLS_PER_TILE, xa);
+    const int64_t c0 = ntiles_full * COLS_PER_TILE;
+    load_tile<T, D, U, true>(a, c0, xa);
+    // tail: old ladj only for existing columns
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < LO::NLS; ++k)
+#pragma unroll
+      for (int w = 0; w < LO::W; ++w) {
+        const int64_t c = LO::col(c0, k, lane) + w;
+        old[k][w] = (LM == 2 && c < a.N) ? ((const T*)a.ladj)[c] : (T)0;
+      }
+    flow_tile<T, D, U, LM, true>(a, rec, ctot, c0, xa, old, stage);
   }
 }
 
@@ -526,7 +648,7 @@ __global__ __launch_bounds__(256) void flow_generic_kernel(FlowArgs a) {
   double* stepc = reinterpret_cast<double*>(smem);
   double* ctotp = stepc + kMaxSteps;
   T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
-  build_program<T, 0>(a, rec, stepc, ctotp);
+  build_program<T, 0, 1>(a, rec, stepc, ctotp);
   const double ctot = *ctotp;
   const int D = a.D;
   const T* __restrict__ X = (const T*)a.X;
@@ -550,7 +672,7 @@ __global__ __launch_bounds__(256) void flow_generic_kernel(FlowArgs a) {
       } else if (op == OP_JOHNSON) {
         for (int d = 0; d < D; ++d) {
           if constexpr (std::is_same_v<T, float>) {
-            const YL r2 = johnson_fwd_f32_slow(y[d], r[4 * d], r[4 * d + 1], r[4 * d + 2], r[4 * d + 3]);
+            const YL r2 = johnson_fwd_f32_slow((y[d] - r[4 * d + 2]) * r[4 * d + 3], r[4 * d], r[4 * d + 1]);
             y[d] = r2.y;
             acc += (double)r2.l * kLn2;
           } else {
@@ -613,8 +735,9 @@ __global__ __launch_bounds__(256) void flow_generic_kernel(FlowArgs a) {
 // host-side launch
 // ------------------------------------------------------------------------------------------
 size_t program_lds_bytes(const FlowArgs& a, size_t elem) {
+  const bool frag = frag_supported(a, elem);
   size_t n = 0;
-  for (int s = 0; s < a.nsteps; ++s) n += (size_t)record_width(a.steps[s].op) * (size_t)a.D;
+  for (int s = 0; s < a.nsteps; ++s) n += record_elems(a.steps[s].op, a.D, elem, frag);
   return kLdsHeader + n * elem;
 }
 
@@ -625,12 +748,12 @@ static int env_int(const char* name, int dflt) {
   return v && *v ? atoi(v) : dflt;
 }
 
-template <typename T, int D, int U, bool LADJ>
+template <typename T, int D, int U, int LM, int OCC = 1>
 static hipError_t launch_frag(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
   using F = Frag<T, D>;
   const int64_t cols_per_block = (int64_t)F::COLS_PER_INSTR * U * 4;
   int per_cu = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flow_frag_kernel<T, D, U, LADJ>, 256, lds);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flow_frag_kernel<T, D, U, LM, OCC>, 256, lds);
   if (e != hipSuccess) return e;
   static const int cap_env = env_int("ENF_BLOCKS_PER_CU", 0);
   if (cap_env > 0 && per_cu > cap_env) per_cu = cap_env;
@@ -639,11 +762,11 @@ static hipError_t launch_frag(const FlowArgs& a, size_t lds, hipStream_t st, con
   const int64_t cap = (int64_t)dev.num_cu * per_cu;
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL((flow_frag_kernel<T, D, U, LADJ>), dim3((unsigned)blocks), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((flow_frag_kernel<T, D, U, LM, OCC>), dim3((unsigned)blocks), dim3(256), lds, st, a);
   return hipGetLastError();
 }
 
-template <typename T, bool LADJ>
+template <typename T, int LADJ>
 static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
   constexpr bool f32 = std::is_same_v<T, float>;
   switch (a.D) {
@@ -653,9 +776,13 @@ static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, cons
     case 8: return launch_frag<T, 8, 4, LADJ>(a, lds, st, dev);
     case 16: return launch_frag<T, 16, 4, LADJ>(a, lds, st, dev);
     case 32: {
+      // tuning variants (ENF_FRAG_U / ENF_FRAG_OCC), default U=4 without an occupancy bound
       static const int u = env_int("ENF_FRAG_U", 4);
+      static const int occ = env_int("ENF_FRAG_OCC", 1);
+      if (u == 2 && occ == 6) return launch_frag<T, 32, 2, LADJ, 6>(a, lds, st, dev);
+      if (u == 2 && occ == 8) return launch_frag<T, 32, 2, LADJ, 8>(a, lds, st, dev);
       if (u == 2) return launch_frag<T, 32, 2, LADJ>(a, lds, st, dev);
-      if (u == 8) return launch_frag<T, 32, 8, LADJ>(a, lds, st, dev);
+      if (u == 4 && occ == 5) return launch_frag<T, 32, 4, LADJ, 5>(a, lds, st, dev);
       return launch_frag<T, 32, 4, LADJ>(a, lds, st, dev);
     }
     case 64: return f32 ? launch_frag<T, 64, 4, LADJ>(a, lds, st, dev) : launch_frag<T, 64, 2, LADJ>(a, lds, st, dev);
@@ -665,13 +792,8 @@ static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, cons
 }
 
 bool frag_supported(const FlowArgs& a, size_t elem) {
-  const int D = a.D;
-  const bool pow2 = D >= 1 && D <= 64 && (D & (D - 1)) == 0;
-  if (!pow2) return false;
-  if (a.ldx != D || a.ldy != D) return false;
-  if (((uintptr_t)a.X | (uintptr_t)a.Y) & 15) return false;
   (void)elem;
-  return true;
+  return a.frag != 0;  // decided once per call by the host (records are laid out for it)
 }
 
 hipError_t launch_flow(const FlowArgs& a, bool f64, hipStream_t st, const DeviceInfo& dev) {
@@ -679,8 +801,11 @@ hipError_t launch_flow(const FlowArgs& a, bool f64, hipStream_t st, const Device
   const size_t lds = program_lds_bytes(a, elem);
   const bool ladj = a.ladj != nullptr;
   if (frag_supported(a, elem)) {
-    if (f64) return ladj ? dispatch_D<double, true>(a, lds, st, dev) : dispatch_D<double, false>(a, lds, st, dev);
-    return ladj ? dispatch_D<float, true>(a, lds, st, dev) : dispatch_D<float, false>(a, lds, st, dev);
+    const int lm = !ladj ? 0 : (a.accumulate ? 2 : 1);
+    if (f64) return lm == 0 ? dispatch_D<double, 0>(a, lds, st, dev)
+                  : lm == 1 ? dispatch_D<double, 1>(a, lds, st, dev) : dispatch_D<double, 2>(a, lds, st, dev);
+    return lm == 0 ? dispatch_D<float, 0>(a, lds, st, dev)
+         : lm == 1 ? dispatch_D<float, 1>(a, lds, st, dev) : dispatch_D<float, 2>(a, lds, st, dev);
   }
   int64_t blocks = (a.N + 255) / 256;
   const int64_t cap = (int64_t)dev.num_cu * 8;

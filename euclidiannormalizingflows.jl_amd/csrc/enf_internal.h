@@ -18,8 +18,11 @@ enum : int32_t {
 
 constexpr int kMaxLayers = 16;  // layers per launch (kernarg table)
 constexpr int kMaxSteps = 64;   // steps per launch (one per transform / per reflection)
-// LDS header: per-step double scratch + the double ladj constant, padded to 16 B
-constexpr size_t kLdsHeader = ((kMaxSteps + 1) * sizeof(double) + 15) / 16 * 16;
+// LDS header: per-step double scratch + the double ladj constant (padded to 16 B), then the
+// per-wave ladj staging slots of the fragment kernel (4 waves x kStagePerWave values of T <= 8 B)
+constexpr size_t kLdsScalars = ((kMaxSteps + 1) * sizeof(double) + 15) / 16 * 16;
+constexpr int kStagePerWave = 256;
+constexpr size_t kLdsHeader = kLdsScalars + 4 * kStagePerWave * sizeof(double);
 constexpr size_t kLdsParamBudget = 32 * 1024;  // parameter records per launch
 
 struct LayerDesc {
@@ -46,8 +49,11 @@ struct FlowArgs {
   int32_t nsteps;
   int32_t nlayers;
   int32_t accumulate;
+  int32_t frag;  // 1: fragment kernel (records laid out with RV = 16/elem), 0: generic kernel
+  int32_t pad_;
   LayerDesc layers[kMaxLayers];
   Step steps[kMaxSteps];
+  int32_t desc[kMaxSteps + 1];  // per step: op | (record offset << 4); desc[nsteps] = sentinel 0
 };
 
 struct DeviceInfo {
@@ -59,6 +65,22 @@ __host__ __device__ constexpr int record_width(int op) {
   return op == OP_HOUSEHOLDER ? 1 : op == OP_SCALESHIFT ? 2 : (op == OP_JOHNSON || op == OP_JOHNSON_INV) ? 4 : 8;
 }
 inline int record_width_host(int op) { return record_width(op); }
+
+// The fragment (fast) kernel handles D in {1,2,4,...,64}, contiguous columns (ld == D) and
+// 16-byte aligned X / Y; everything else runs on the generic kernel.
+inline bool frag_path(int64_t D, int64_t ldx, int64_t ldy, const void* X, const void* Y) {
+  const bool pow2 = D >= 1 && D <= 64 && (D & (D - 1)) == 0;
+  return pow2 && ldx == D && ldy == D && ((((uintptr_t)X) | ((uintptr_t)Y)) & 15) == 0;
+}
+
+// Values of T in one step's LDS record: W * max(D, RV) (RV = 16/elem on the fragment path, else 1),
+// rounded up to 16 bytes.
+inline size_t record_elems(int op, int64_t D, size_t elem, bool frag) {
+  const int64_t rv = frag ? (int64_t)(16 / elem) : 1;
+  size_t n = (size_t)record_width(op) * (size_t)(D > rv ? D : rv);
+  const size_t q = 16 / elem;
+  return (n + q - 1) / q * q;
+}
 
 size_t program_lds_bytes(const FlowArgs& a, size_t elem);
 bool frag_supported(const FlowArgs& a, size_t elem);
