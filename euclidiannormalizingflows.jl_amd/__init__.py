@@ -22,7 +22,18 @@ from .trafos import (  # noqa: F401
     with_logabsdet_jacobian,
 )
 
+from .train import (  # noqa: F401
+    ADAGrad,
+    FlowState,
+    WhiteningResult,
+    mvnormal_negll_trafo,
+    mvnormal_negll_trafograd,
+    optimize_whitening,
+)
+
 __all__ = [
+    "ADAGrad", "FlowState", "WhiteningResult", "mvnormal_negll_trafo", "mvnormal_negll_trafograd",
+    "optimize_whitening",
     "ScaleShiftTrafo", "CenterStretch", "CenterContract", "JohnsonTrafo", "JohnsonTrafoInv",
     "HouseholderTrafo", "ComposedFunction", "compose", "inverse", "with_logabsdet_jacobian",
     "leaves", "Trafo", "MethodError", "DimensionMismatch", "EnfError", "version",

@@ -1,23 +1,523 @@
-// enf_grad.hip -- fused forward + backward of the whitening loss (config 5), see include/enf.h
-// enf_flow_negll_grad. (Implementation follows.)
+// enf_grad.hip -- fused forward + backward of the whitening loss (config 5, optimize_whitening).
+//
+// For the N local samples (columns) of X and the composed flow y = f_L o ... o f_1 (x):
+//   S      = sum_j [ sum_d (y_dj^2 + log 2pi)/2 - ladj_j ]            (= B * mvnormal_negll_trafo,
+//                                                                    src/optimize_whitening.jl:7-15)
+//   dS/dth for every flow parameter                                   (mvnormal_negll_trafograd, :18-22)
+// out[0] += S, out[1 + i] += dS/dth_i (layout: include/enf.h enf_flow_param_count).
+//
+// Kernel structure: fragment layout as the forward kernel (enf_flow.hip), one fragment (16 B) per
+// lane per tile. The forward pass stores every step's input in LDS (the reference's chained
+// Householder pullback instead recomputes inputs by re-reflection, householder_trafo.jl:88-103;
+// storing is exact and costs 1 KiB of LDS per step per wave). The backward pass walks the steps
+// in reverse with the cotangent g = dS/du (starting at g = y), accumulating per-row parameter
+// gradients into LDS (fp32 LDS atomics, summed per block), and writes one partial gradient
+// vector per block; a second kernel sums the block partials in double, in block order, applies
+// the Householder direction projection (householder_trafo.jl:22-40) and adds into out.
+//
+// The arithmetic here is the accurate library form (ocml asinh/log/exp/... in T); it is not the
+// headline path.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+#include <cstring>
+#include <type_traits>
+#include <vector>
+
+#include "enf_internal.h"
 #include "enf_train.h"
 
 namespace enf {
 
+constexpr int kMaxGradSteps = 32;
+constexpr int kMaxGradLayers = 16;
+
+struct GradArgs {
+  const void* X;
+  int64_t N;
+  int64_t ldx;
+  int32_t D;
+  int32_t nsteps;
+  int32_t nlayers;
+  int32_t nparams;  // gradient entries of this flow
+  void* partial;    // [gridDim.x][1 + nparams] of double (loss first)
+  LayerDesc layers[kMaxGradLayers];
+  int32_t op[kMaxGradSteps];
+  int32_t layer[kMaxGradSteps];
+  int32_t col[kMaxGradSteps];     // Householder column
+  int32_t roff[kMaxGradSteps];    // record offset (elements of T) in LDS
+  int32_t goff[kMaxGradSteps];    // gradient offset of the step's first parameter vector
+};
+
+__host__ __device__ constexpr int grad_nparams(int op) {
+  return op == OP_HOUSEHOLDER ? 1 : op == OP_SCALESHIFT ? 2 : (op == OP_JOHNSON || op == OP_JOHNSON_INV) ? 4 : 3;
+}
+
+typedef unsigned int u32x4g __attribute__((ext_vector_type(4)));
+
+template <int CTRL, typename T>
+__device__ __forceinline__ T gdpp(T x) {
+  if constexpr (std::is_same_v<T, float>) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+  }
+}
+template <int G, typename T>
+__device__ __forceinline__ T gsum(T x) {
+  if constexpr (G >= 2) x += gdpp<0xB1>(x);
+  if constexpr (G >= 4) x += gdpp<0x4E>(x);
+  if constexpr (G >= 8) x += gdpp<0x141>(x);
+  if constexpr (G >= 16) x += gdpp<0x140>(x);
+  if constexpr (G >= 32) x += __shfl_xor(x, 16);
+  if constexpr (G >= 64) x += __shfl_xor(x, 32);
+  return x;
+}
+
+template <typename T>
+__device__ __forceinline__ T sigm(T t) { return (T)1 / ((T)1 + exp(-t)); }
+
+// Per-element forward of one step (accurate form). Returns the output; adds the element's ladj
+// term (natural log) to lad.
+template <typename T>
+__device__ __forceinline__ T fwd_elem(int op, T x, const T* p, T& lad) {
+  switch (op) {
+    case OP_SCALESHIFT: lad += log(fabs(p[0])); return fma(x, p[0], p[1]);
+    case OP_JOHNSON: {
+      const T z = (x - p[2]) / p[3];
+      lad += log(fabs(p[1] / p[3])) - (T)0.5 * log1p(z * z);
+      return p[0] + p[1] * asinh(z);
+    }
+    case OP_JOHNSON_INV: {
+      const T w = (x - p[0]) / p[1];
+      const T y = p[3] * sinh(w) + p[2];
+      const T z = (y - p[2]) / p[3];
+      lad -= log(fabs(p[1] / p[3])) - (T)0.5 * log1p(z * z);
+      return y;
+    }
+    case OP_CENTER_CONTRACT: {
+      const T a = p[0], b = p[1], xu = x - p[2];
+      lad += log(fabs(sigm(b * (xu - a)) + sigm(-b * (xu + a))));
+      return (log1p(exp(b * (xu - a))) - log1p(exp(-b * (xu + a)))) / b;
+    }
+    case OP_CENTER_STRETCH: {
+      const T a = p[0], b = p[1], c = p[2];
+      const T e = exp(fabs(b * x));
+      const T ome = (T)1 - e;
+      const T inner = (sqrt(ome * ome * exp((T)2 * b * a) + (T)4 * e) - ome * exp(b * a)) / (T)2;
+      const T sg = x > (T)0 ? (T)1 : (x < (T)0 ? (T)-1 : x);
+      const T y = sg * log(inner) / b + c;
+      const T yu = y - c;
+      lad -= log(fabs(sigm(b * (yu - a)) + sigm(-b * (yu + a))));
+      return y;
+    }
+    default: return x;
+  }
+}
+
+// Backward of one elementwise step for one element: input x, output cotangent g (dS/dy).
+// Adds dS/dparam into dp[0..np) and returns dS/dx. S contains -ladj, hence the "- dl" terms.
+template <typename T>
+__device__ __forceinline__ T bwd_elem(int op, T x, T g, const T* p, T* dp) {
+  switch (op) {
+    case OP_SCALESHIFT: {  // y = x a + b ; l = log|a|
+      dp[0] += g * x - (T)1 / p[0];
+      dp[1] += g;
+      return g * p[0];
+    }
+    case OP_JOHNSON: {  // y = gm + dl*asinh(z), z = (x - xi)/lm ; l = log|dl/lm| - log(1+z^2)/2
+      const T dl = p[1], lm = p[3];
+      const T z = (x - p[2]) / lm;
+      const T s2 = (T)1 + z * z, s = sqrt(s2);
+      dp[0] += g;
+      dp[1] += g * asinh(z) - (T)1 / dl;
+      dp[2] += -g * dl / (lm * s) - z / (lm * s2);
+      dp[3] += -g * dl * z / (lm * s) + (T)1 / lm - z * z / (lm * s2);
+      return g * dl / (lm * s) + z / (lm * s2);
+    }
+    case OP_JOHNSON_INV: {  // y = lm*sinh(w) + xi, w = (x - gm)/dl ; l = log|lm/dl| + log cosh w
+      const T dl = p[1], lm = p[3];
+      const T w = (x - p[0]) / dl;
+      const T ch = cosh(w), th = tanh(w);
+      dp[0] += -g * lm * ch / dl + th / dl;
+      dp[1] += -g * lm * ch * w / dl + (T)1 / dl + th * w / dl;
+      dp[2] += g;
+      dp[3] += g * sinh(w) - (T)1 / lm;
+      return g * lm * ch / dl - th / dl;
+    }
+    case OP_CENTER_CONTRACT: {
+      // y = (softplus(t1) - softplus(t2))/b, t1 = b(xu - a), t2 = -b(xu + a), xu = x - c
+      // l = log(s1 + s2), s_i = sigmoid(t_i); dy/dx = s1 + s2
+      const T a = p[0], b = p[1], xu = x - p[2];
+      const T t1 = b * (xu - a), t2 = -b * (xu + a);
+      const T s1 = sigm(t1), s2 = sigm(t2), ss = s1 + s2;
+      const T y = (log1p(exp(t1)) - log1p(exp(t2))) / b;
+      const T q1 = s1 * ((T)1 - s1), q2 = s2 * ((T)1 - s2);
+      const T dydx = ss, dyda = s2 - s1, dydb = (s1 * (xu - a) - s2 * (xu + a)) / b - y / b;
+      const T dldx = (q1 * b - q2 * b) / ss, dlda = -(q1 + q2) * b / ss, dldb = (q1 * (xu - a) - q2 * (xu + a)) / ss;
+      dp[0] += g * dyda - dlda;
+      dp[1] += g * dydb - dldb;
+      dp[2] += -(g * dydx - dldx);  // d/dc = -d/dx
+      return g * dydx - dldx;
+    }
+    case OP_CENTER_STRETCH: {
+      // y = cs(x) with cc(y) = x: dy/dx = 1/cc'(y), dy/dth = -dcc/dth(y)/cc'(y);
+      // l = -lcc(y): dl/dth = -(dlcc/dy dy/dth + dlcc/dth), dl/dx = -dlcc/dy dy/dx
+      const T a = p[0], b = p[1], c = p[2];
+      T lad = 0;
+      const T y = fwd_elem<T>(OP_CENTER_STRETCH, x, p, lad);
+      const T yu = y - c;
+      const T t1 = b * (yu - a), t2 = -b * (yu + a);
+      const T s1 = sigm(t1), s2 = sigm(t2), ss = s1 + s2;
+      const T ccv = (log1p(exp(t1)) - log1p(exp(t2))) / b;  // = x (up to rounding)
+      const T q1 = s1 * ((T)1 - s1), q2 = s2 * ((T)1 - s2);
+      const T cc_a = s2 - s1, cc_b = (s1 * (yu - a) - s2 * (yu + a)) / b - ccv / b, cc_c = -ss;
+      const T lcc_y = (q1 * b - q2 * b) / ss, lcc_a = -(q1 + q2) * b / ss, lcc_b = (q1 * (yu - a) - q2 * (yu + a)) / ss,
+              lcc_c = -lcc_y;
+      const T dydx = (T)1 / ss;
+      const T dyda = -cc_a / ss, dydb = -cc_b / ss, dydc = -cc_c / ss;
+      const T dlda = -(lcc_y * dyda + lcc_a), dldb = -(lcc_y * dydb + lcc_b), dldc = -(lcc_y * dydc + lcc_c);
+      const T dldx = -lcc_y * dydx;
+      dp[0] += g * dyda - dlda;
+      dp[1] += g * dydb - dldb;
+      dp[2] += g * dydc - dldc;
+      return g * dydx - dldx;
+    }
+    default: return g;
+  }
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
+  constexpr int V = 16 / (int)sizeof(T);
+  constexpr int G = D >= V ? D / V : 1;
+  constexpr int CPF = D >= V ? 1 : V / D;
+  constexpr int SEG = D >= V ? V : D;
+  constexpr int COLS = 64 / G * CPF;  // columns per wave tile (one fragment per lane)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // LDS: [grad accumulators: nparams floats][loss: 4 waves x double][records][activations]
+  float* gacc = reinterpret_cast<float*>(smem);
+  const int gbytes = ((a.nparams * 4 + 15) / 16) * 16;
+  double* lossw = reinterpret_cast<double*>(smem + gbytes);
+  T* rec = reinterpret_cast<T*>(smem + gbytes + 64);
+  int nrec = 0;
+  for (int s = 0; s < a.nsteps; ++s) nrec += grad_nparams(a.op[s]) * (D > V ? D : V);
+  T* act = rec + ((nrec + 3) / 4) * 4 + (threadIdx.x >> 6) * (a.nsteps * 64 * V);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < a.nparams; i += blockDim.x) gacc[i] = 0.f;
+  // raw parameter records, layout [group][param][element] as the forward kernel (RV = V)
+  for (int s = 0; s < a.nsteps; ++s) {
+    const LayerDesc& L = a.layers[a.layer[s]];
+    const int np = grad_nparams(a.op[s]);
+    const int nent = D > V ? D : V;
+    for (int i = tid; i < nent; i += blockDim.x) {
+      const int g = D >= V ? i / V : 0, e = i % V;
+      const int row = D >= V ? i : e % D;
+      for (int q = 0; q < np; ++q) {
+        T v;
+        if (a.op[s] == OP_HOUSEHOLDER) {
+          // normalised reflection vector vh = v*sqrt(2/v'v) (computed per block, sum in double)
+          const T* vc = (const T*)L.p[0] + (int64_t)a.col[s] * D;
+          double vv = 0.0;
+          for (int d = 0; d < D; ++d) vv += (double)vc[d] * (double)vc[d];
+          v = (T)((double)vc[row] * sqrt(2.0 / vv));
+        } else {
+          v = ((const T*)L.p[q])[row];
+        }
+        rec[a.roff[s] + (g * np + q) * V + e] = v;
+      }
+    }
+  }
+  __syncthreads();
+
+  const int r0 = D >= V ? V * (lane % G) : 0;
+  const int grp = D >= V ? lane % G : 0;
+  const int64_t ntiles = (a.N + COLS - 1) / COLS;
+  double lossp = 0.0;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < ntiles; t += (int64_t)gridDim.x * 4) {
+    const int64_t c0 = t * COLS + (lane / G) * CPF;
+    T x[V];
+    bool valid[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int64_t c = c0 + e / SEG;
+      valid[e] = c < a.N;
+      x[e] = valid[e] ? ((const T*)a.X)[c * a.ldx + r0 + e % SEG] : (T)0;
+    }
+    // ---- forward, storing each step's input
+    T lad[CPF];
+#pragma unroll
+    for (int c = 0; c < CPF; ++c) lad[c] = (T)0;
+    for (int s = 0; s < a.nsteps; ++s) {
+      T* as = act + s * 64 * V + lane * V;
+#pragma unroll
+      for (int e = 0; e < V; ++e) as[e] = x[e];
+      const int op = a.op[s];
+      const T* r = rec + a.roff[s] + grp * grad_nparams(op) * V;
+      if (op == OP_HOUSEHOLDER) {
+#pragma unroll
+        for (int c = 0; c < CPF; ++c) {
+          T dot = 0;
+#pragma unroll
+          for (int e = 0; e < SEG; ++e) dot = fma(r[c * SEG + e], x[c * SEG + e], dot);
+          dot = gsum<G>(dot);
+#pragma unroll
+          for (int e = 0; e < SEG; ++e) x[c * SEG + e] = fma(-dot, r[c * SEG + e], x[c * SEG + e]);
+        }
+      } else {
+        const int np = grad_nparams(op);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          T p[4];
+          for (int q = 0; q < np; ++q) p[q] = r[q * V + e];
+          T l = 0;
+          x[e] = fwd_elem<T>(op, x[e], p, l);
+          lad[e / SEG] += l;
+        }
+      }
+    }
+    // ---- loss: sum_d (y^2 + log 2pi)/2 - ladj (only valid columns)
+    {
+      T part = 0;
+#pragma unroll
+      for (int e = 0; e < V; ++e)
+        if (valid[e]) part += (x[e] * x[e] + (T)1.8378770664093454836) / (T)2;
+#pragma unroll
+      for (int c = 0; c < CPF; ++c) {
+        const T tot = gsum<G>(lad[c]);  // all lanes active (DPP)
+        if (valid[c * SEG] && (lane % G) == 0) part -= tot;
+      }
+      lossp += (double)part;
+    }
+    // ---- backward: g = dS/dy = y (invalid columns carry g = 0 and contribute nothing)
+    T g[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) g[e] = valid[e] ? x[e] : (T)0;
+    for (int s = a.nsteps - 1; s >= 0; --s) {
+      const T* as = act + s * 64 * V + lane * V;
+      T xin[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) xin[e] = as[e];
+      const int op = a.op[s];
+      const int np = grad_nparams(op);
+      const T* r = rec + a.roff[s] + grp * np * V;
+      if (op == OP_HOUSEHOLDER) {
+        // y = x - vh (vh'x): dS/dx = g - vh (vh'g); with w = vh/sqrt2 (unit), the direction
+        // gradient dS/dw_d = -2 (g_d (w'x) + x_d (w'g)) = -sqrt2 (g_d (vh'x) + x_d (vh'g)); the
+        // projection onto v (householder_trafo.jl:32,39) is applied after the sample sum.
+#pragma unroll
+        for (int c = 0; c < CPF; ++c) {
+          T vx = 0, vg = 0;
+#pragma unroll
+          for (int e = 0; e < SEG; ++e) {
+            vx = fma(r[c * SEG + e], xin[c * SEG + e], vx);
+            vg = fma(r[c * SEG + e], g[c * SEG + e], vg);
+          }
+          vx = gsum<G>(vx);
+          vg = gsum<G>(vg);
+#pragma unroll
+          for (int e = 0; e < SEG; ++e) {
+            const int row = r0 + e;
+            const T contrib = g[c * SEG + e] * vx + xin[c * SEG + e] * vg;
+            if (valid[c * SEG + e]) atomicAdd(&gacc[a.goff[s] + row], (float)contrib);
+            g[c * SEG + e] = fma(-vg, r[c * SEG + e], g[c * SEG + e]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          T p[4], dp[4] = {0, 0, 0, 0};
+          for (int q = 0; q < np; ++q) p[q] = r[q * V + e];
+          const T gx = bwd_elem<T>(op, xin[e], g[e], p, dp);
+          if (valid[e]) {
+            const int row = r0 + e % SEG;
+            for (int q = 0; q < np; ++q) atomicAdd(&gacc[a.goff[s] + q * D + row], (float)dp[q]);
+          }
+          g[e] = valid[e] ? gx : (T)0;
+        }
+      }
+    }
+  }
+  // ---- block partials
+  for (int m = 32; m >= 1; m >>= 1) lossp += __shfl_xor(lossp, m);
+  if (lane == 0) lossw[wave] = lossp;
+  __syncthreads();
+  double* out = (double*)a.partial + (int64_t)blockIdx.x * (1 + a.nparams);
+  if (tid == 0) out[0] = lossw[0] + lossw[1] + lossw[2] + lossw[3];
+  for (int i = tid; i < a.nparams; i += blockDim.x) out[1 + i] = (double)gacc[i];
+}
+
+// Sum the block partials (double, block order), project Householder direction gradients, add to out.
+struct ReduceArgs {
+  const double* partial;
+  int32_t nblocks;
+  int32_t nparams;
+  int32_t D;
+  int32_t nh;  // Householder columns
+  void* out;
+  // per Householder column: offset of its gradient vector and its device column pointer
+  int32_t hoff[kMaxGradSteps];
+  const void* hcol[kMaxGradSteps];
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void grad_reduce_kernel(ReduceArgs r) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* tot = reinterpret_cast<double*>(smem);  // 1 + nparams
+  for (int i = threadIdx.x; i < 1 + r.nparams; i += blockDim.x) {
+    double s = 0.0;
+    for (int b = 0; b < r.nblocks; ++b) s += r.partial[(int64_t)b * (1 + r.nparams) + i];
+    tot[i] = s;
+  }
+  __syncthreads();
+  // Householder: dS/dw = -sqrt2 * G;  dS/dv = (dS/dw - w (dS/dw . w)) / |v|  (householder_trafo.jl:32)
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    for (int h = 0; h < r.nh; ++h) {
+      const T* v = (const T*)r.hcol[h];
+      double* gw = tot + 1 + r.hoff[h];
+      double vv = 0.0, wd = 0.0;
+      for (int d = lane; d < r.D; d += 64) vv += (double)v[d] * (double)v[d];
+      for (int m = 32; m >= 1; m >>= 1) vv += __shfl_xor(vv, m);
+      const double nrm = sqrt(vv);
+      for (int d = lane; d < r.D; d += 64) wd += -1.4142135623730951 * gw[d] * ((double)v[d] / nrm);
+      for (int m = 32; m >= 1; m >>= 1) wd += __shfl_xor(wd, m);
+      for (int d = lane; d < r.D; d += 64) {
+        const double dw = -1.4142135623730951 * gw[d];
+        gw[d] = (dw - ((double)v[d] / nrm) * wd) / nrm;
+      }
+    }
+  }
+  __syncthreads();
+  T* out = (T*)r.out;
+  for (int i = threadIdx.x; i < 1 + r.nparams; i += blockDim.x) out[i] += (T)tot[i];
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+struct Plan {
+  GradArgs ga;
+  ReduceArgs ra;
+  size_t lds = 0;
+  int blocks = 0;
+};
+
+bool grad_D_supported(int64_t D) { return D >= 1 && D <= 64 && (D & (D - 1)) == 0; }
+
+enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, int32_t nlayers, Plan& P) {
+  std::memset(&P.ga, 0, sizeof P.ga);
+  std::memset(&P.ra, 0, sizeof P.ra);
+  if (!grad_D_supported(D)) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: D must be a power of two <= 64");
+  if (nlayers > kMaxGradLayers) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: more than 16 layers");
+  const int V = f64 ? 2 : 4;
+  const int nent = (int)(D > V ? D : V);
+  int s = 0, goff = 0, roff = 0;
+  for (int l = 0; l < nlayers; ++l) {
+    P.ga.layers[l].op = layers[l].op;
+    P.ga.layers[l].k = layers[l].k;
+    for (int q = 0; q < 4; ++q) P.ga.layers[l].p[q] = layers[l].p[q];
+    const int ncol = layers[l].op == OP_HOUSEHOLDER ? layers[l].k : 1;
+    for (int c = 0; c < ncol; ++c) {
+      if (s >= kMaxGradSteps) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: more than 32 steps");
+      P.ga.op[s] = layers[l].op;
+      P.ga.layer[s] = l;
+      P.ga.col[s] = c;
+      P.ga.roff[s] = roff;
+      P.ga.goff[s] = goff + (layers[l].op == OP_HOUSEHOLDER ? c * (int)D : 0);
+      if (layers[l].op == OP_HOUSEHOLDER) {
+        P.ra.hoff[P.ra.nh] = P.ga.goff[s];
+        P.ra.hcol[P.ra.nh] = (const char*)layers[l].p[0] + (size_t)c * D * (f64 ? 8 : 4);
+        ++P.ra.nh;
+      }
+      roff += grad_nparams(layers[l].op) * nent;
+      ++s;
+    }
+    goff += (int)D * (layers[l].op == OP_HOUSEHOLDER ? layers[l].k : grad_nparams(layers[l].op));
+  }
+  P.ga.D = (int32_t)D;
+  P.ga.N = N;
+  P.ga.nsteps = s;
+  P.ga.nlayers = nlayers;
+  P.ga.nparams = goff;
+  const size_t esz = f64 ? 8 : 4;
+  const size_t gbytes = ((size_t)goff * 4 + 15) / 16 * 16;
+  const size_t rbytes = ((size_t)(roff + 3) / 4) * 4 * esz;
+  const size_t abytes = (size_t)4 * s * 64 * V * esz;
+  P.lds = gbytes + 64 + rbytes + abytes;
+  if (P.lds > 160 * 1024) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: flow too large for LDS");
+  const int cols = (int)(64 / (D >= V ? D / V : 1) * (D >= V ? 1 : V / D));
+  const int64_t tiles = (N + cols - 1) / cols;
+  int64_t blocks = (tiles + 3) / 4;
+  DeviceInfo dev;
+  if (current_device_info(&dev) != ENF_OK) return ENF_ERR_HIP;
+  const int64_t cap = (int64_t)dev.num_cu * 2;
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  P.blocks = (int)blocks;
+  P.ra.nblocks = P.blocks;
+  P.ra.nparams = goff;
+  P.ra.D = (int32_t)D;
+  return ENF_OK;
+}
+
+template <typename T, int DD>
+hipError_t launch_grad_D(const Plan& P, hipStream_t st) {
+  if (P.lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)negll_grad_kernel<T, DD>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)P.lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((negll_grad_kernel<T, DD>), dim3(P.blocks), dim3(256), P.lds, st, P.ga);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_grad(const Plan& P, hipStream_t st) {
+  hipError_t e0 = hipSuccess;
+  switch (P.ga.D) {
+#define ENF_G(DD) case DD: e0 = launch_grad_D<T, DD>(P, st); break;
+    ENF_G(1) ENF_G(2) ENF_G(4) ENF_G(8) ENF_G(16) ENF_G(32) ENF_G(64)
+#undef ENF_G
+    default: return hipErrorInvalidValue;
+  }
+  if (e0 != hipSuccess) return e0;
+  hipLaunchKernelGGL((grad_reduce_kernel<T>), dim3(1), dim3(256), (size_t)(1 + P.ra.nparams) * 8, st, P.ra);
+  return hipGetLastError();
+}
+
+}  // namespace
+
 enf_status negll_grad_workspace(bool f64, int64_t D, int64_t N, const enf_layer* layers, int32_t nlayers,
                                 size_t* bytes) {
-  (void)f64; (void)D; (void)N; (void)layers; (void)nlayers;
-  *bytes = 0;
+  Plan P;
+  enf_status s = make_plan(f64, D, N > 0 ? N : 1, layers, nlayers, P);
+  if (s != ENF_OK) return s;
+  *bytes = (size_t)P.blocks * (1 + (size_t)P.ga.nparams) * sizeof(double);
   return ENF_OK;
 }
 
 enf_status negll_grad(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
                       int32_t nlayers, void* out, void* workspace, size_t workspace_bytes, hipStream_t st) {
-  (void)f64; (void)D; (void)N; (void)X; (void)ldx; (void)layers; (void)nlayers; (void)out;
-  (void)workspace; (void)workspace_bytes; (void)st;
-  return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: not implemented yet");
+  Plan P;
+  enf_status s = make_plan(f64, D, N, layers, nlayers, P);
+  if (s != ENF_OK) return s;
+  const size_t need = (size_t)P.blocks * (1 + (size_t)P.ga.nparams) * sizeof(double);
+  if (!workspace || workspace_bytes < need) return set_error(ENF_ERR_INVALID, "enf_flow_negll_grad: workspace too small");
+  P.ga.X = X;
+  P.ga.ldx = ldx;
+  P.ga.partial = workspace;
+  P.ra.partial = (const double*)workspace;
+  P.ra.out = out;
+  hipError_t e = f64 ? launch_grad<double>(P, st) : launch_grad<float>(P, st);
+  if (e != hipSuccess) return set_error(ENF_ERR_HIP, hipGetErrorString(e));
+  return ENF_OK;
 }
 
 }  // namespace enf

@@ -1,0 +1,144 @@
+# ENFHip.jl -- Julia ccall binding of libenf.so (include/enf.h) for bat/EuclidianNormalizingFlows.jl.
+#
+# NOT EXECUTED IN THIS PIPELINE: Julia is not installed in the build image nor on the GPU boxes
+# (SURVEY.md §0). This file is the reference-side binding a maintainer adds; it mirrors
+# include/enf.h one to one and is reviewed against the Python host mirror
+# (euclidiannormalizingflows.jl_amd/trafos.py), which exercises the same C ABI in tests/.
+#
+# It adds methods (no type piracy: they dispatch on the package-owned HipMatrix) to the generic
+# functions the reference extends (src/EuclidianNormalizingFlows.jl:38-40):
+#     (f)(X::HipMatrix), ChangesOfVariables.with_logabsdet_jacobian(f, X::HipMatrix)
+# for f any of ScaleShiftTrafo, CenterStretch, CenterContract, JohnsonTrafo, JohnsonTrafoInv,
+# HouseholderTrafo, or a ComposedFunction of them -- a composition is flattened into ONE
+# enf_flow_apply call (one fused kernel launch). InverseFunctions.inverse stays the reference's.
+module ENFHip
+
+using ChangesOfVariables, InverseFunctions
+import ChangesOfVariables: with_logabsdet_jacobian
+using EuclidianNormalizingFlows: ScaleShiftTrafo, CenterStretch, CenterContract, JohnsonTrafo,
+                                 JohnsonTrafoInv, HouseholderTrafo
+
+const libenf = get(ENV, "ENF_LIBRARY", "libenf.so")
+
+const ENF_F32, ENF_F64 = Cint(0), Cint(1)
+const OP_SCALESHIFT, OP_CENTER_STRETCH, OP_CENTER_CONTRACT = Int32(0), Int32(1), Int32(2)
+const OP_JOHNSON, OP_JOHNSON_INV, OP_HOUSEHOLDER = Int32(3), Int32(4), Int32(5)
+
+# enf_layer (include/enf.h)
+struct EnfLayer
+    op::Int32
+    k::Int32
+    p::NTuple{4,Ptr{Cvoid}}
+end
+
+# --- device memory owned by this module -------------------------------------------------------
+mutable struct HipBuffer
+    ptr::Ptr{Cvoid}
+    bytes::Int
+    function HipBuffer(bytes::Integer)
+        r = Ref{Ptr{Cvoid}}(C_NULL)
+        check(ccall((:enf_malloc, libenf), Cint, (Ref{Ptr{Cvoid}}, Csize_t), r, bytes))
+        b = new(r[], bytes)
+        finalizer(b -> ccall((:enf_free, libenf), Cint, (Ptr{Cvoid},), b.ptr), b)
+        b
+    end
+end
+
+"""Column-major D x N matrix resident on the GPU (Julia's sample-per-column convention)."""
+struct HipMatrix{T<:Union{Float32,Float64}}
+    buf::HipBuffer
+    D::Int
+    N::Int
+end
+HipMatrix{T}(D::Integer, N::Integer) where {T} = HipMatrix{T}(HipBuffer(max(D * N, 1) * sizeof(T)), D, N)
+Base.size(X::HipMatrix) = (X.D, X.N)
+Base.eltype(::HipMatrix{T}) where {T} = T
+
+function HipMatrix(A::AbstractMatrix{T}) where {T<:Union{Float32,Float64}}
+    X = HipMatrix{T}(size(A)...)
+    Ac = Matrix{T}(A)
+    check(ccall((:enf_memcpy, libenf), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Csize_t, Int32, Ptr{Cvoid}),
+                X.buf.ptr, Ac, sizeof(Ac), 0, C_NULL))
+    check(ccall((:enf_stream_synchronize, libenf), Cint, (Ptr{Cvoid},), C_NULL))
+    X
+end
+
+function Base.Array(X::HipMatrix{T}) where {T}
+    A = Matrix{T}(undef, X.D, X.N)
+    check(ccall((:enf_memcpy, libenf), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Csize_t, Int32, Ptr{Cvoid}),
+                A, X.buf.ptr, sizeof(A), 1, C_NULL))
+    check(ccall((:enf_stream_synchronize, libenf), Cint, (Ptr{Cvoid},), C_NULL))
+    A
+end
+
+function check(status::Cint)
+    status == 0 && return nothing
+    msg = unsafe_string(ccall((:enf_last_error, libenf), Cstring, ()))
+    error("libenf error $status: $msg")
+end
+
+# --- flattening: layer list, innermost first; params uploaded as length-D device vectors -------
+_vec(p::Real, D, ::Type{T}) where {T} = fill(T(p), D)
+_vec(p::AbstractVector, D, ::Type{T}) where {T} = (length(p) == D || throw(DimensionMismatch()); Vector{T}(p))
+
+_leaves(f::ComposedFunction) = vcat(_leaves(f.inner), _leaves(f.outer))
+_leaves(f) = Any[f]
+
+_op(::ScaleShiftTrafo) = (OP_SCALESHIFT, (:a, :b))
+_op(::CenterStretch) = (OP_CENTER_STRETCH, (:a, :b, :c))
+_op(::CenterContract) = (OP_CENTER_CONTRACT, (:a, :b, :c))
+_op(::JohnsonTrafo) = (OP_JOHNSON, (:gamma, :delta, :xi, :lambda))
+_op(::JohnsonTrafoInv) = (OP_JOHNSON_INV, (:gamma, :delta, :xi, :lambda))
+_op(::HouseholderTrafo) = (OP_HOUSEHOLDER, (:V,))
+
+function _layers(fs, D, ::Type{T}) where {T}
+    keep = HipMatrix[]
+    layers = EnfLayer[]
+    for f in fs
+        op, names = _op(f)
+        ptrs = Ptr{Cvoid}[C_NULL, C_NULL, C_NULL, C_NULL]
+        k = 0
+        for (q, nm) in enumerate(names)
+            p = getfield(f, nm)
+            A = op == OP_HOUSEHOLDER ? Matrix{T}(reshape(p, D, :)) : reshape(_vec(p, D, T), D, 1)
+            op == OP_HOUSEHOLDER && (k = size(A, 2))
+            M = HipMatrix(A)
+            push!(keep, M)
+            ptrs[q] = M.buf.ptr
+        end
+        push!(layers, EnfLayer(op, Int32(k), Tuple(ptrs)))
+    end
+    layers, keep
+end
+
+const _Supported = Union{ScaleShiftTrafo,CenterStretch,CenterContract,JohnsonTrafo,JohnsonTrafoInv,
+                         HouseholderTrafo,ComposedFunction}
+
+function _apply(f, X::HipMatrix{T}, want_ladj::Bool) where {T}
+    fs = _leaves(f)
+    layers, keep = _layers(fs, X.D, T)
+    Y = HipMatrix{T}(X.D, X.N)
+    ladj = want_ladj ? HipMatrix{T}(1, X.N) : nothing
+    check(ccall((:enf_flow_apply, libenf), Cint,
+                (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int32,
+                 Ptr{EnfLayer}, Int32, Ptr{Cvoid}),
+                T === Float64 ? ENF_F64 : ENF_F32, X.D, X.N, X.buf.ptr, X.D, Y.buf.ptr, X.D,
+                want_ladj ? ladj.buf.ptr : C_NULL, 0, layers, length(layers), C_NULL))
+    GC.@preserve keep nothing
+    Y, ladj
+end
+
+# (f)(X) and with_logabsdet_jacobian(f, X): one fused launch; ladj is a 1 x N HipMatrix (Julia's
+# Adjoint row, src/abstract_trafo.jl:9)
+(f::ScaleShiftTrafo)(X::HipMatrix) = _apply(f, X, false)[1]
+(f::CenterStretch)(X::HipMatrix) = _apply(f, X, false)[1]
+(f::CenterContract)(X::HipMatrix) = _apply(f, X, false)[1]
+(f::JohnsonTrafo)(X::HipMatrix) = _apply(f, X, false)[1]
+(f::JohnsonTrafoInv)(X::HipMatrix) = _apply(f, X, false)[1]
+(f::HouseholderTrafo)(X::HipMatrix) = _apply(f, X, false)[1]
+
+with_logabsdet_jacobian(f::_Supported, X::HipMatrix) = _apply(f, X, true)
+
+export HipMatrix
+
+end # module

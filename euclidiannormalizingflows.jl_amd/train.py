@@ -1,0 +1,261 @@
+"""Device-resident whitening training (optimize_whitening), backed by libenf.so.
+
+Julia (src/optimize_whitening.jl)                        here
+-------------------------------------------------------  -----------------------------------------------
+mvnormal_negll_trafo(trafo, X)          :7-15             mvnormal_negll_trafo(trafo, X)
+mvnormal_negll_trafograd(trafo, X)      :18-22            mvnormal_negll_trafograd(trafo, X) -> (negll, grads)
+optimize_whitening(smpls, trafo, opt; nbatches,          optimize_whitening(smpls, trafo, opt, nbatches=100,
+                   nepochs, optstate, negll_history)        nepochs=100, optstate=None, negll_history=None)
+  :25-45                                                   -> WhiteningResult(result, optimizer_state,
+                                                                              negll_history)
+Optimisers.ADAGrad(eta=0.1f0, epsilon=eps(Float32))       ADAGrad(eta=0.1, epsilon=eps(float32))
+
+Per training step (one minibatch): one fused forward+backward launch (enf_flow_negll_grad) over the
+local samples, an optional cross-GPU sum of the (1 + P) loss/gradient values (torch.distributed,
+which is RCCL on ROCm; no collective at world size 1), the ADAGrad update (enf_adagrad_step) on
+the flat device parameter vector and the HouseholderTrafo column re-normalisation
+(enf_householder_normalize, src/householder_trafo.jl:134-146), all on the device; the per-step
+negll is written to a device history buffer and copied to the host once at the end.
+
+Samples ``smpls`` are the reference's VectorOfSimilarVectors flattened: a (D, N) column-major
+matrix (``flatview``). Minibatches are consecutive column ranges of
+``round(N / nbatches)`` samples (Iterators.partition, the last one possibly shorter). With a
+process group, each rank takes an equal contiguous share of every minibatch and the gradient is
+normalised by the GLOBAL minibatch size, so every rank applies the identical update.
+
+Trainable parameters are the array-valued fields (Optimisers/Functors treat scalar fields as
+constants). Known reference quirk: under Zygote the primal ladj of a
+ScaleShiftTrafo is 0 (rrule(similar_fill), src/abstract_trafo.jl:30-33), so the reference's
+recorded negll misses +sum(log|a|); ``mvnormal_negll_trafograd(..., similar_fill_quirk=True)``
+reproduces that value (the gradient is unaffected either way); optimize_whitening records the
+true negll.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from .trafos import (HouseholderTrafo, ScaleShiftTrafo, Trafo, _as_cpu_array, _colmajor, _is_vector, _kind,
+                     _ld, _promote, _to_device_matrix, compose, leaves)
+
+LOG2PI = float(np.log(2 * np.pi))
+
+
+@dataclass
+class ADAGrad:
+    """Optimisers.jl 0.2 ADAGrad: acc starts at epsilon; acc += g^2; x -= eta*g/(sqrt(acc) + epsilon)."""
+    eta: float = float(np.float32(0.1))
+    epsilon: float = float(np.finfo(np.float32).eps)
+
+
+@dataclass
+class WhiteningResult:
+    result: object
+    optimizer_state: "FlowState"
+    negll_history: List[float]
+
+
+class FlowState:
+    """Flat device parameter vector of a flow (layout of enf_flow_param_count) + ADAGrad state."""
+
+    def __init__(self, trafo, D: int, dtype, device, optimizer: Optional[ADAGrad] = None):
+        self.trafos: List[Trafo] = leaves(trafo)
+        self.D, self.dtype, self.device = D, dtype, device
+        segs, self.trainable, self.shapes = [], [], []
+        for t in self.trafos:
+            for name, p in zip(t.FIELDS, t.params()):
+                if isinstance(t, HouseholderTrafo):
+                    A = _as_cpu_array(p).astype(np.float64)
+                    A = A.reshape(D, -1) if A.ndim == 2 else A.reshape(D, 1)
+                    segs.append(np.asfortranarray(A).reshape(-1, order="F"))
+                    self.shapes.append(("V", _as_cpu_array(p).shape))
+                else:
+                    segs.append(np.broadcast_to(_as_cpu_array(p).astype(np.float64), (D,)).copy())
+                    self.shapes.append((name, _as_cpu_array(p).shape))
+                self.trainable.append(_is_vector(p))
+        sizes = [s.size for s in segs]
+        self.offsets = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        self.theta = torch.as_tensor(np.concatenate(segs), dtype=dtype, device=device)
+        self.nparams = int(self.offsets[-1])
+        eps = (optimizer or ADAGrad()).epsilon
+        self.acc = torch.full_like(self.theta, eps)  # Optimisers.init(ADAGrad) = onevalue(epsilon, x)
+        self._layers = self._make_layers()
+
+    def _make_layers(self):
+        arr = (_lib.Layer * len(self.trafos))()
+        esz = self.theta.element_size()
+        base = self.theta.data_ptr()
+        seg = 0
+        for i, t in enumerate(self.trafos):
+            arr[i].op = t.OP
+            arr[i].k = t._k()
+            for q in range(len(t.FIELDS)):
+                arr[i].p[q] = base + int(self.offsets[seg]) * esz
+                seg += 1
+        return arr
+
+    def layers(self):
+        return self._layers
+
+    def householder_columns(self):
+        """(offset, k) of every Householder V in theta."""
+        out, seg = [], 0
+        for t in self.trafos:
+            for _ in t.FIELDS:
+                if isinstance(t, HouseholderTrafo):
+                    out.append((int(self.offsets[seg]), t._k()))
+                seg += 1
+        return out
+
+    def to_trafo(self):
+        """Rebuild the composed transform from the device parameters (Functors reconstruction)."""
+        th = self.theta.detach().cpu().numpy()
+        rebuilt, seg = [], 0
+        for t in self.trafos:
+            vals = []
+            for name in t.FIELDS:
+                a = th[self.offsets[seg]:self.offsets[seg + 1]]
+                _, shape = self.shapes[seg]
+                if isinstance(t, HouseholderTrafo):
+                    a = a.reshape(self.D, -1, order="F")
+                    if len(shape) == 1:
+                        a = a[:, 0]
+                    vals.append(a.copy())
+                elif self.trainable[seg]:
+                    vals.append(a.copy())
+                else:
+                    vals.append(getattr(t, name))
+                seg += 1
+            rebuilt.append(type(t)(*vals))
+        return compose(*reversed(rebuilt))
+
+
+def _dtype_of(trafo, X):
+    return _promote(_kind(X), *[_kind(p) for t in leaves(trafo) for p in t.params()])
+
+
+def _grad_call(state: FlowState, X: torch.Tensor, out: torch.Tensor, ws: torch.Tensor):
+    D, N = X.shape
+    L = _lib.lib()
+    dt = _lib.ENF_F64 if state.dtype == torch.float64 else _lib.ENF_F32
+    with torch.cuda.device(X.device):
+        stream = torch.cuda.current_stream(X.device).cuda_stream
+        _lib.check(L.enf_flow_negll_grad(dt, D, N, X.data_ptr(), _ld(X), state.layers(), len(state.trafos),
+                                         out.data_ptr(), ws.data_ptr(), ws.numel() * ws.element_size(), stream))
+
+
+def _workspace(state: FlowState, N: int):
+    nb = ctypes.c_size_t()
+    dt = _lib.ENF_F64 if state.dtype == torch.float64 else _lib.ENF_F32
+    _lib.check(_lib.lib().enf_flow_negll_grad_workspace(dt, state.D, max(N, 1), state.layers(), len(state.trafos),
+                                                        ctypes.byref(nb)))
+    return torch.empty(max(1, nb.value // 8), dtype=torch.float64, device=state.device)
+
+
+def _scaleshift_ladj_const(state: FlowState) -> float:
+    c, seg = 0.0, 0
+    th = None
+    for t in state.trafos:
+        for _ in t.FIELDS:
+            if isinstance(t, ScaleShiftTrafo) and _ == "a":
+                th = state.theta.detach().cpu().numpy() if th is None else th
+                c += float(np.sum(np.log(np.abs(th[state.offsets[seg]:state.offsets[seg + 1]]))))
+            seg += 1
+    return c
+
+
+def mvnormal_negll_trafograd(trafo, X, similar_fill_quirk: bool = False):
+    """(negll, gradient) of mvnormal_negll_trafo (src/optimize_whitening.jl:18-22).
+
+    The gradient is returned as a list per transform (application order) of per-field arrays."""
+    M, _, _ = _to_device_matrix(X)
+    dtype = _dtype_of(trafo, M)
+    M = _colmajor(M, dtype)
+    state = FlowState(trafo, M.shape[0], dtype, M.device)
+    out = torch.zeros(1 + state.nparams, dtype=dtype, device=M.device)
+    _grad_call(state, M, out, _workspace(state, M.shape[1]))
+    N = M.shape[1]
+    res = (out / N).cpu().numpy()
+    negll = float(res[0]) + (_scaleshift_ladj_const(state) if similar_fill_quirk else 0.0)
+    grads, seg = [], 0
+    g = res[1:]
+    for t in state.trafos:
+        per = []
+        for _ in t.FIELDS:
+            a = g[state.offsets[seg]:state.offsets[seg + 1]]
+            if isinstance(t, HouseholderTrafo):
+                a = a.reshape(state.D, -1, order="F")
+            per.append(a)
+            seg += 1
+        grads.append(per)
+    return negll, grads
+
+
+def mvnormal_negll_trafo(trafo, X) -> float:
+    """-(sum(std_normal_logpdf.(Y)) + sum(ladj)) / nsamples (src/optimize_whitening.jl:7-15)."""
+    return mvnormal_negll_trafograd(trafo, X)[0]
+
+
+def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None, nbatches: int = 100,
+                       nepochs: int = 100, optstate: Optional[FlowState] = None,
+                       negll_history: Optional[List[float]] = None, process_group=None) -> WhiteningResult:
+    """src/optimize_whitening.jl:25-45 on the device (see module docstring)."""
+    import torch.distributed as dist
+
+    optimizer = optimizer or ADAGrad()
+    M, _, _ = _to_device_matrix(smpls)
+    D, N = M.shape
+    dtype = _dtype_of(initial_trafo, M)
+    M = _colmajor(M, dtype)
+    if optstate is None:
+        state = FlowState(initial_trafo, D, dtype, M.device, optimizer)
+    else:  # continue from a previous optimizer state (optimize_whitening.jl:28, 44)
+        state = optstate
+    world, rank = 1, 0
+    if process_group is not None or (dist.is_available() and dist.is_initialized()):
+        world = dist.get_world_size(process_group)
+        rank = dist.get_rank(process_group)
+    batchsize = int(round(N / nbatches))
+    batchsize = max(batchsize, 1)
+    starts = list(range(0, N, batchsize))
+    L = _lib.lib()
+    dt = _lib.ENF_F64 if dtype == torch.float64 else _lib.ENF_F32
+    out = torch.zeros(1 + state.nparams, dtype=dtype, device=M.device)
+    ws = _workspace(state, batchsize)
+    hist = torch.zeros(nepochs * len(starts), dtype=torch.float64, device=M.device)
+    hcols = state.householder_columns()
+    segs = [(int(state.offsets[i]), int(state.offsets[i + 1])) for i, tr in enumerate(state.trainable) if tr]
+    step = 0
+    with torch.cuda.device(M.device):
+        stream = torch.cuda.current_stream(M.device).cuda_stream
+        for _ in range(nepochs):
+            for b0 in starts:
+                b1 = min(b0 + batchsize, N)
+                B = b1 - b0
+                lo = b0 + (B * rank) // world
+                hi = b0 + (B * (rank + 1)) // world
+                out.zero_()
+                if hi > lo:
+                    Xb = M[:, lo:hi]
+                    _lib.check(L.enf_flow_negll_grad(dt, D, hi - lo, Xb.data_ptr(), _ld(M), state.layers(),
+                                                     len(state.trafos), out.data_ptr(), ws.data_ptr(),
+                                                     ws.numel() * 8, stream))
+                if world > 1:
+                    dist.all_reduce(out, group=process_group)
+                hist[step:step + 1].copy_(out[0:1] / B)
+                g = out[1:]
+                for s0, s1 in segs:
+                    _lib.check(L.enf_adagrad_step(dt, s1 - s0, state.theta[s0:].data_ptr(), state.acc[s0:].data_ptr(),
+                                                  g[s0:].data_ptr(), 1.0 / B, optimizer.eta, optimizer.epsilon,
+                                                  stream))
+                for off, k in hcols:
+                    _lib.check(L.enf_householder_normalize(dt, D, k, state.theta[off:].data_ptr(), stream))
+                step += 1
+    h = hist.cpu().numpy().tolist()
+    prev = list(negll_history) if negll_history is not None else []
+    return WhiteningResult(state.to_trafo(), state, prev + h)
