@@ -234,7 +234,9 @@ __device__ __forceinline__ int64_t frag_col(int64_t col0, int u, int lane) {
 }
 
 // One wave tile = U fully coalesced 1-KiB wave-instructions (ldx == D, 16-B aligned).
-template <typename T, int D, int U, bool TAIL>
+// DBG (diagnostic builds only, ENF_DEBUG_MODE): 1 = synthesize the tile instead of loading it,
+// 2 = also skip the stores (compute-only timing).
+template <typename T, int D, int U, bool TAIL, int DBG = 0>
 __device__ __forceinline__ void load_tile(const FlowArgs& a, int64_t col0, T (&x)[U][Frag<T, D>::V]) {
   using F = Frag<T, D>;
   constexpr int V = F::V, G = F::G, SEG = F::SEG;
@@ -245,7 +247,10 @@ __device__ __forceinline__ void load_tile(const FlowArgs& a, int64_t col0, T (&x
   for (int u = 0; u < U; ++u) {
     const int64_t cf = frag_col<T, D>(col0, u, lane);
     const int64_t eoff = cf * D + r0;
-    if (!TAIL) {
+    if (DBG >= 1) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) x[u][e] = (T)(lane + 3 * u + e) * (T)0.03125 - (T)1;
+    } else if (!TAIL) {
       const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X + eoff));
       __builtin_memcpy(&x[u][0], &v4, 16);
     } else {
@@ -293,77 +298,82 @@ __device__ __forceinline__ void load_ladj_old(const FlowArgs& a, int64_t col0, T
     for (int w = 0; w < LO::W; ++w) old[k][w] = LM == 2 ? ladj[LO::col(col0, k, lane) + w] : (T)0;
 }
 
-template <typename T, int D, int U, int LM, bool TAIL>
-__device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict__ rec, T ctot,
-                                          int64_t col0, T (&x)[U][Frag<T, D>::V],
-                                          const T (&old)[LadjOut<T, D, U>::NLS][LadjOut<T, D, U>::W],
-                                          T* __restrict__ stage) {
-  constexpr bool LADJ = LM > 0;
-  using F = Frag<T, D>;
-  constexpr int V = F::V, G = F::G, CPF = F::CPF, SEG = F::SEG;
-  const int lane = threadIdx.x & 63;
-  T* __restrict__ Y = (T*)a.Y;
-  const int64_t N = a.N;
-  const int r0 = D >= V ? V * (lane % G) : 0;
-  const int grp = D >= V ? lane % G : 0;  // parameter-record group of this lane
-  int64_t colf[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) colf[u] = frag_col<T, D>(col0, u, lane);
-  T acc[U][CPF];
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int c = 0; c < CPF; ++c) acc[u][c] = (T)0;
-  // make the vmcnt wait for THIS tile's loads happen here, with the next tile's loads still in
-  // flight (inside the runtime step loop the compiler would otherwise drain vmcnt to 0)
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int e = 0; e < V; ++e) asm volatile("" : "+v"(x[u][e]));
+// register tile types (aliases avoid a clang parse ambiguity of T (&x)[U][Frag<T, D>::V] params)
+template <typename T, int D, int U>
+using Tile = T[U][Frag<T, D>::V];
+template <typename T, int D, int U>
+using Acc = T[U][Frag<T, D>::CPF];
+#define ENF_FRAG_CONSTS                                   \
+  using F = Frag<T, D>;                                   \
+  constexpr int V = F::V, G = F::G, CPF = F::CPF, SEG = F::SEG; \
+  (void)G; (void)CPF; (void)SEG;
 
-  int desc = a.desc[0];  // op | record offset << 4; a.desc[nsteps] is a sentinel
-  for (int s = 0; s < a.nsteps; ++s) {
-    const int next = a.desc[s + 1];  // scalar load issued a step ahead
-    const int op = desc & 15;
-    const T* __restrict__ r = rec + (desc >> 4) + grp * record_width(op) * V;
-    desc = next;
-    if (op == OP_HOUSEHOLDER) {
-      T vh[V];
-      lds_vec<T, V>(r, vh);
+// ---- step bodies: one transform applied to the wave tile x (U fragments of V values per lane).
+// r points at this lane's record group ([param][element], 16-byte vectors). acc: ladj partials.
+// Column dot products of all U*CPF column segments of the tile with the lane's 16-byte vector v,
+// reduced over the G lanes of each column. Every stage runs across all segments before the next
+// one (U*CPF independent chains), so neither the FMA chain nor the DPP stages stall the wave.
+template <typename T, int D, int U>
+__device__ __forceinline__ void tile_dots(const Tile<T, D, U>& x, const T (&v)[Frag<T, D>::V],
+                                          T (&dot)[U][Frag<T, D>::CPF]) {
+  ENF_FRAG_CONSTS
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
+  for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int c = 0; c < CPF; ++c) {
-          T dot = (T)0;
+    for (int c = 0; c < CPF; ++c) dot[u][c] = v[c * SEG] * x[u][c * SEG];
 #pragma unroll
-          for (int e = 0; e < SEG; ++e) dot = fma(vh[c * SEG + e], x[u][c * SEG + e], dot);
-          dot = group_sum<G>(dot);
+  for (int e = 1; e < SEG; ++e)
 #pragma unroll
-          for (int e = 0; e < SEG; ++e) x[u][c * SEG + e] = fma(-dot, vh[c * SEG + e], x[u][c * SEG + e]);
-        }
-      }
-    } else if (op == OP_JOHNSON) {
-      T pg[V], pd[V], px[V], pl[V];
-      lds_vec<T, V>(r, pg);
-      lds_vec<T, V>(r + V, pd);
-      lds_vec<T, V>(r + 2 * V, px);
-      lds_vec<T, V>(r + 3 * V, pl);
-      if constexpr (std::is_same_v<T, float>) {
-        // y = gamma + delta*asinh(z), asinh|z| = ln2*log2(|z| + sqrt(1+z^2))  (johnson_trafo.jl:31)
-        // ladj: log|delta/lambda| - log(1+z^2)/2, one log2 of the product of the q = 1+z^2 of a
-        // fragment's rows                                                    (johnson_trafo.jl:41,51)
-        // Pass 1: z for the whole tile (in place) and its largest |z|; the product of <= 4 q stays
-        // finite for |z| <= 2^15, larger or infinite |z| take the exact elementwise path (one
-        // uniform branch per tile, so the fast path interleaves all U*V elements). NaN needs no
-        // special path: it propagates through the fast formulas as through the reference's.
-        float zmax = 0.f;
+    for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+      for (int c = 0; c < CPF; ++c) dot[u][c] = fma(v[c * SEG + e], x[u][c * SEG + e], dot[u][c]);
+  if constexpr (G >= 2) {
 #pragma unroll
-          for (int e = 0; e < V; ++e) {
-            x[u][e] = (x[u][e] - px[e]) * pl[e];
-            zmax = fmaxf(zmax, fabsf(x[u][e]));
-          }
+    for (int u = 0; u < U; ++u) dot[u][0] += dpp<0xB1>(dot[u][0]);
+  }
+  if constexpr (G >= 4) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) dot[u][0] += dpp<0x4E>(dot[u][0]);
+  }
+  if constexpr (G >= 8) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) dot[u][0] += dpp<0x141>(dot[u][0]);
+  }
+  if constexpr (G >= 16) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) dot[u][0] += dpp<0x140>(dot[u][0]);
+  }
+  if constexpr (G >= 32) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) dot[u][0] += __shfl_xor(dot[u][0], 16);
+  }
+  if constexpr (G >= 64) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) dot[u][0] += __shfl_xor(dot[u][0], 32);
+  }
+}
+
+// y = x - vh (vh'x), vh = v*sqrt(2/v'v): householder_trafo!(y, v, x) (householder_trafo.jl:8-11)
+template <typename T, int D, int U>
+__device__ __forceinline__ void step_householder(Tile<T, D, U>& x, const T* __restrict__ r) {
+  ENF_FRAG_CONSTS
+  T vh[V];
+  lds_vec<T, V>(r, vh);
+  T dot[U][CPF];
+  tile_dots<T, D, U>(x, vh, dot);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < V; ++e) x[u][e] = fma(-dot[u][e / SEG], vh[e], x[u][e]);
+}
+
+// fp32 Johnson layer from z (in x): y = gamma + delta*asinh(z), ladj += log|delta/lambda| -
+// log(1+z^2)/2 (the constant part is in ctot). zmax = max |z| over the tile.
+template <int D, int U, bool LADJ>
+__device__ __forceinline__ void johnson_from_z(Tile<float, D, U>& x, Acc<float, D, U>& acc,
+                                               const float (&pg)[4], const float (&pd)[4], float zmax) {
+  using T = float;
+  ENF_FRAG_CONSTS
         if (__builtin_expect(!(zmax <= 32768.f), 0)) {
 #pragma unroll
           for (int u = 0; u < U; ++u)
@@ -392,6 +402,34 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
               for (int c = 0; c < CPF; ++c) acc[u][c] = fmaf(-0.5f, hw_log2(prod[c]), acc[u][c]);
           }
         }
+}
+
+template <typename T, int D, int U, bool LADJ>
+__device__ __forceinline__ void step_johnson(Tile<T, D, U>& x, Acc<T, D, U>& acc,
+                                             const T* __restrict__ r) {
+  ENF_FRAG_CONSTS
+  T pg[V], pd[V], px[V], pl[V];
+  lds_vec<T, V>(r, pg);
+  lds_vec<T, V>(r + V, pd);
+  lds_vec<T, V>(r + 2 * V, px);
+  lds_vec<T, V>(r + 3 * V, pl);
+      if constexpr (std::is_same_v<T, float>) {
+        // y = gamma + delta*asinh(z), asinh|z| = ln2*log2(|z| + sqrt(1+z^2))  (johnson_trafo.jl:31)
+        // ladj: log|delta/lambda| - log(1+z^2)/2, one log2 of the product of the q = 1+z^2 of a
+        // fragment's rows                                                    (johnson_trafo.jl:41,51)
+        // Pass 1: z for the whole tile (in place) and its largest |z|; the product of <= 4 q stays
+        // finite for |z| <= 2^15, larger or infinite |z| take the exact elementwise path (one
+        // uniform branch per tile, so the fast path interleaves all U*V elements). NaN needs no
+        // special path: it propagates through the fast formulas as through the reference's.
+        float zmax = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            x[u][e] = (x[u][e] - px[e]) * pl[e];
+            zmax = fmaxf(zmax, fabsf(x[u][e]));
+          }
+        johnson_from_z<D, U, LADJ>(x, acc, pg, pd, zmax);
       } else {
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -402,12 +440,52 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
             if (LADJ) acc[u][e / SEG] -= 0.5 * log1p(z * z);
           }
       }
-    } else if (op == OP_JOHNSON_INV) {
-      T pg[V], pd[V], px[V], pl[V];
-      lds_vec<T, V>(r, pg);
-      lds_vec<T, V>(r + V, pd);
-      lds_vec<T, V>(r + 2 * V, px);
-      lds_vec<T, V>(r + 3 * V, pl);
+}
+
+// Compiled-program fusion of a reflection and the Johnson layer after it: the reflected value
+// x' = x - vh (vh'x) only enters J through z = (x' - xi)/lambda, so z is formed directly as
+// fma(-dot, vh/lambda, fma(x, 1/lambda, -xi/lambda)) -- two FMAs per element instead of the
+// update, the subtraction and the scaling. (fp32 path; same normwise rounding class as the
+// unfused sequence.)
+template <typename T, int D, int U, bool LADJ>
+__device__ __forceinline__ void step_hj_fused(Tile<T, D, U>& x, Acc<T, D, U>& acc, const T* __restrict__ rh,
+                                              const T* __restrict__ rj) {
+  ENF_FRAG_CONSTS
+  static_assert(std::is_same_v<T, float>, "fp32 only");
+  T vh[V], pg[V], pd[V], px[V], pl[V];
+  lds_vec<T, V>(rh, vh);
+  lds_vec<T, V>(rj, pg);
+  lds_vec<T, V>(rj + V, pd);
+  lds_vec<T, V>(rj + 2 * V, px);
+  lds_vec<T, V>(rj + 3 * V, pl);
+  T dot[U][CPF];
+  tile_dots<T, D, U>(x, vh, dot);
+  float w[V], c[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    w[e] = vh[e] * pl[e];
+    c[e] = -px[e] * pl[e];
+  }
+  float zmax = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      x[u][e] = fmaf(-dot[u][e / SEG], w[e], fmaf(x[u][e], pl[e], c[e]));  // z
+      zmax = fmaxf(zmax, fabsf(x[u][e]));
+    }
+  johnson_from_z<D, U, LADJ>(x, acc, pg, pd, zmax);
+}
+
+template <typename T, int D, int U, bool LADJ>
+__device__ __forceinline__ void step_johnson_inv(Tile<T, D, U>& x, Acc<T, D, U>& acc,
+                                                 const T* __restrict__ r) {
+  ENF_FRAG_CONSTS
+  T pg[V], pd[V], px[V], pl[V];
+  lds_vec<T, V>(r, pg);
+  lds_vec<T, V>(r + V, pd);
+  lds_vec<T, V>(r + 2 * V, px);
+  lds_vec<T, V>(r + 3 * V, pl);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -436,7 +514,11 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
           }
         }
       }
-    } else if (op == OP_SCALESHIFT) {
+}
+
+template <typename T, int D, int U>
+__device__ __forceinline__ void step_scaleshift(Tile<T, D, U>& x, const T* __restrict__ r) {
+  ENF_FRAG_CONSTS
       // y = muladd(x, a, b) (scale_shift_trafo.jl:16); ladj = sum log|a| (constant, in ctot)
       T pa[V], pb[V];
       lds_vec<T, V>(r, pa);
@@ -445,7 +527,12 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int e = 0; e < V; ++e) x[u][e] = fma(x[u][e], pa[e], pb[e]);
-    } else if (op == OP_CENTER_STRETCH) {
+}
+
+template <typename T, int D, int U, bool LADJ>
+__device__ __forceinline__ void step_center_stretch(Tile<T, D, U>& x, Acc<T, D, U>& acc,
+                                                    const T* __restrict__ r) {
+  ENF_FRAG_CONSTS
       T rr[8][V];
 #pragma unroll
       for (int q = 0; q < 8; ++q) lds_vec<T, V>(r + q * V, rr[q]);
@@ -489,7 +576,12 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
           }
         }
       }
-    } else {  // OP_CENTER_CONTRACT
+}
+
+template <typename T, int D, int U, bool LADJ>
+__device__ __forceinline__ void step_center_contract(Tile<T, D, U>& x, Acc<T, D, U>& acc,
+                                                     const T* __restrict__ r) {
+  ENF_FRAG_CONSTS
       T rr[8][V];
 #pragma unroll
       for (int q = 0; q < 8; ++q) lds_vec<T, V>(r + q * V, rr[q]);
@@ -521,14 +613,29 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
           }
         }
       }
-    }
-  }
+}
 
-  // ---- store Y and ladj
+// ---- tile epilogue: store Y and the ladj
+template <typename T, int D, int U, int LM, bool TAIL, int DBG>
+__device__ __forceinline__ void store_tile(const FlowArgs& a, T ctot, int64_t col0, Tile<T, D, U>& x,
+                                           Acc<T, D, U>& acc,
+                                           const T (&old)[LadjOut<T, D, U>::NLS][LadjOut<T, D, U>::W],
+                                           T* __restrict__ stage) {
+  ENF_FRAG_CONSTS
+  constexpr bool LADJ = LM > 0;
+  const int lane = threadIdx.x & 63;
+  T* __restrict__ Y = (T*)a.Y;
+  const int64_t N = a.N;
+  const int r0 = D >= V ? V * (lane % G) : 0;
+  int64_t colf[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) colf[u] = frag_col<T, D>(col0, u, lane);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t eoff = colf[u] * D + r0;
-    if (!TAIL) {
+    if (DBG == 2) {
+      if (x[u][0] == (T)1234.5) Y[eoff] = x[u][1];  // keeps the compute alive, never true in practice
+    } else if (!TAIL) {
       u32x4 v4;
       __builtin_memcpy(&v4, &x[u][0], 16);
       __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(Y + eoff));
@@ -571,8 +678,58 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
   }
 }
 
+// Program: PROG == 0 interprets the step table of the kernel arguments; PROG == n > 0 is the
+// compile-time program (H o J)^n -- the config 3/4/5 flows -- with the same parameter records at
+// compile-time offsets, so the per-step dispatch disappears and the compiler schedules across
+// steps (parameter LDS reads hoisted ahead of the preceding step's arithmetic).
+template <typename T, int D, int U, int LM, bool TAIL, int DBG, int PROG>
+__device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict__ rec, T ctot,
+                                          int64_t col0, Tile<T, D, U>& x,
+                                          const T (&old)[LadjOut<T, D, U>::NLS][LadjOut<T, D, U>::W],
+                                          T* __restrict__ stage) {
+  ENF_FRAG_CONSTS
+  constexpr bool LADJ = LM > 0;
+  const int lane = threadIdx.x & 63;
+  const int grp = D >= V ? lane % G : 0;  // parameter-record group of this lane
+  T acc[U][CPF];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int c = 0; c < CPF; ++c) acc[u][c] = (T)0;
+  // make the vmcnt wait for THIS tile's loads happen here, with the next tile's loads still in
+  // flight (inside a runtime step loop the compiler would otherwise drain vmcnt to 0)
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < V; ++e) asm volatile("" : "+v"(x[u][e]));
+
+  if constexpr (PROG > 0) {
+    constexpr int NE = D > V ? D : V;       // record entries per parameter
+    constexpr int HREC = NE, JREC = 4 * NE;  // record sizes (multiples of V)
+#pragma unroll
+    for (int p = 0; p < PROG; ++p)
+      step_hj_fused<T, D, U, LADJ>(x, acc, rec + p * (HREC + JREC) + grp * V,
+                                   rec + p * (HREC + JREC) + HREC + grp * 4 * V);
+  } else {
+    int desc = a.desc[0];  // op | record offset << 4; a.desc[nsteps] is a sentinel
+    for (int s = 0; s < a.nsteps; ++s) {
+      const int next = a.desc[s + 1];  // scalar load issued a step ahead
+      const int op = desc & 15;
+      const T* __restrict__ r = rec + (desc >> 4) + grp * record_width(op) * V;
+      desc = next;
+      if (op == OP_HOUSEHOLDER) step_householder<T, D, U>(x, r);
+      else if (op == OP_JOHNSON) step_johnson<T, D, U, LADJ>(x, acc, r);
+      else if (op == OP_JOHNSON_INV) step_johnson_inv<T, D, U, LADJ>(x, acc, r);
+      else if (op == OP_SCALESHIFT) step_scaleshift<T, D, U>(x, r);
+      else if (op == OP_CENTER_STRETCH) step_center_stretch<T, D, U, LADJ>(x, acc, r);
+      else step_center_contract<T, D, U, LADJ>(x, acc, r);
+    }
+  }
+  store_tile<T, D, U, LM, TAIL, DBG>(a, ctot, col0, x, acc, old, stage);
+}
+
 // OCC: minimum waves per SIMD the register allocation must allow (launch-bounds occupancy hint)
-template <typename T, int D, int U, int LM, int OCC>
+template <typename T, int D, int U, int LM, int OCC, int DBG = 0, int PROG = 0>
 __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* stepc = reinterpret_cast<double*>(smem);
@@ -604,21 +761,21 @@ __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
   OT old;
   const int64_t t = wave_id;
   if (t < ntiles_full) {
-    load_tile<T, D, U, false>(a, t * COLS_PER_TILE, xa);
+    load_tile<T, D, U, false, DBG>(a, t * COLS_PER_TILE, xa);
     int64_t t1 = t + nwaves;
     load_ladj_old<T, D, U, LM>(a, t * COLS_PER_TILE, old);
-    load_tile<T, D, U, false>(a, (t1 < ntiles_full ? t1 : t) * COLS_PER_TILE, xb);
-    flow_tile<T, D, U, LM, false>(a, rec, ctot, t * COLS_PER_TILE, xa, old, stage);
+    load_tile<T, D, U, false, DBG>(a, (t1 < ntiles_full ? t1 : t) * COLS_PER_TILE, xb);
+    flow_tile<T, D, U, LM, false, DBG, PROG>(a, rec, ctot, t * COLS_PER_TILE, xa, old, stage);
     while (t1 < ntiles_full) {
       const int64_t t2 = t1 + nwaves;
       load_ladj_old<T, D, U, LM>(a, t1 * COLS_PER_TILE, old);
-      load_tile<T, D, U, false>(a, (t2 < ntiles_full ? t2 : t1) * COLS_PER_TILE, xa);
-      flow_tile<T, D, U, LM, false>(a, rec, ctot, t1 * COLS_PER_TILE, xb, old, stage);
+      load_tile<T, D, U, false, DBG>(a, (t2 < ntiles_full ? t2 : t1) * COLS_PER_TILE, xa);
+      flow_tile<T, D, U, LM, false, DBG, PROG>(a, rec, ctot, t1 * COLS_PER_TILE, xb, old, stage);
       if (t2 >= ntiles_full) break;
       const int64_t t3 = t2 + nwaves;
       load_ladj_old<T, D, U, LM>(a, t2 * COLS_PER_TILE, old);
-      load_tile<T, D, U, false>(a, (t3 < ntiles_full ? t3 : t2) * COLS_PER_TILE, xb);
-      flow_tile<T, D, U, LM, false>(a, rec, ctot, t2 * COLS_PER_TILE, xa, old, stage);
+      load_tile<T, D, U, false, DBG>(a, (t3 < ntiles_full ? t3 : t2) * COLS_PER_TILE, xb);
+      flow_tile<T, D, U, LM, false, DBG, PROG>(a, rec, ctot, t2 * COLS_PER_TILE, xa, old, stage);
       t1 = t3;
     }
   }
@@ -634,7 +791,7 @@ __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
         const int64_t c = LO::col(c0, k, lane) + w;
         old[k][w] = (LM == 2 && c < a.N) ? ((const T*)a.ladj)[c] : (T)0;
       }
-    flow_tile<T, D, U, LM, true>(a, rec, ctot, c0, xa, old, stage);
+    flow_tile<T, D, U, LM, true, 0, PROG>(a, rec, ctot, c0, xa, old, stage);
   }
 }
 
@@ -748,12 +905,12 @@ static int env_int(const char* name, int dflt) {
   return v && *v ? atoi(v) : dflt;
 }
 
-template <typename T, int D, int U, int LM, int OCC = 1>
+template <typename T, int D, int U, int LM, int OCC = 1, int DBG = 0, int PROG = 0>
 static hipError_t launch_frag(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
   using F = Frag<T, D>;
   const int64_t cols_per_block = (int64_t)F::COLS_PER_INSTR * U * 4;
   int per_cu = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flow_frag_kernel<T, D, U, LM, OCC>, 256, lds);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flow_frag_kernel<T, D, U, LM, OCC, DBG, PROG>, 256, lds);
   if (e != hipSuccess) return e;
   static const int cap_env = env_int("ENF_BLOCKS_PER_CU", 0);
   if (cap_env > 0 && per_cu > cap_env) per_cu = cap_env;
@@ -762,13 +919,47 @@ static hipError_t launch_frag(const FlowArgs& a, size_t lds, hipStream_t st, con
   const int64_t cap = (int64_t)dev.num_cu * per_cu;
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL((flow_frag_kernel<T, D, U, LM, OCC>), dim3((unsigned)blocks), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((flow_frag_kernel<T, D, U, LM, OCC, DBG, PROG>), dim3((unsigned)blocks), dim3(256), lds, st, a);
   return hipGetLastError();
+}
+
+// n if the step program is (H o J)^n (Householder first, one reflection per H) with the records at
+// the offsets the compiled program assumes, else 0.
+static int hj_pairs(const FlowArgs& a, int V) {
+  if (a.nsteps < 2 || (a.nsteps & 1)) return 0;
+  const int NE = a.D > V ? a.D : V;
+  for (int s = 0; s < a.nsteps; ++s) {
+    const int p = s / 2;
+    const int want_op = (s & 1) ? OP_JOHNSON : OP_HOUSEHOLDER;
+    const int want_off = p * 5 * NE + ((s & 1) ? NE : 0);
+    if (a.steps[s].op != want_op || a.steps[s].off != want_off || a.desc[s] != (want_op | (want_off << 4))) return 0;
+  }
+  return a.nsteps / 2;
+}
+
+template <typename T, int D, int LADJ>
+static hipError_t launch_hj(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev, int n) {
+  switch (n) {
+    case 1: return launch_frag<T, D, 4, LADJ, 1, 0, 1>(a, lds, st, dev);
+    case 2: return launch_frag<T, D, 4, LADJ, 1, 0, 2>(a, lds, st, dev);
+    case 3: return launch_frag<T, D, 4, LADJ, 1, 0, 3>(a, lds, st, dev);
+    case 4: return launch_frag<T, D, 4, LADJ, 1, 0, 4>(a, lds, st, dev);
+    default: return launch_frag<T, D, 4, LADJ>(a, lds, st, dev);
+  }
 }
 
 template <typename T, int LADJ>
 static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
   constexpr bool f32 = std::is_same_v<T, float>;
+  // compiled (H o J)^n programs (fp32, D = 32 / 64): ENF_NO_SPECIALIZE=1 forces the interpreter
+  static const int nospec = env_int("ENF_NO_SPECIALIZE", 0);
+  if constexpr (f32) {
+    const int n = nospec ? 0 : hj_pairs(a, 4);
+    if (n >= 1 && n <= 4 && env_int("ENF_DEBUG_MODE", 0) == 0) {
+      if (a.D == 32) return launch_hj<T, 32, LADJ>(a, lds, st, dev, n);
+      if (a.D == 64) return launch_hj<T, 64, LADJ>(a, lds, st, dev, n);
+    }
+  }
   switch (a.D) {
     case 1: return launch_frag<T, 1, 4, LADJ>(a, lds, st, dev);
     case 2: return launch_frag<T, 2, 4, LADJ>(a, lds, st, dev);
@@ -779,6 +970,9 @@ static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, cons
       // tuning variants (ENF_FRAG_U / ENF_FRAG_OCC), default U=4 without an occupancy bound
       static const int u = env_int("ENF_FRAG_U", 4);
       static const int occ = env_int("ENF_FRAG_OCC", 1);
+      static const int dbg = env_int("ENF_DEBUG_MODE", 0);
+      if (dbg == 1) return launch_frag<T, 32, 4, LADJ, 1, 1>(a, lds, st, dev);
+      if (dbg == 2) return launch_frag<T, 32, 4, LADJ, 1, 2>(a, lds, st, dev);
       if (u == 2 && occ == 6) return launch_frag<T, 32, 2, LADJ, 6>(a, lds, st, dev);
       if (u == 2 && occ == 8) return launch_frag<T, 32, 2, LADJ, 8>(a, lds, st, dev);
       if (u == 2) return launch_frag<T, 32, 2, LADJ>(a, lds, st, dev);

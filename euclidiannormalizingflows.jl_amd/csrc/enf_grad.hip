@@ -11,7 +11,7 @@
 // Householder pullback instead recomputes inputs by re-reflection, householder_trafo.jl:88-103;
 // storing is exact and costs 1 KiB of LDS per step per wave). The backward pass walks the steps
 // in reverse with the cotangent g = dS/du (starting at g = y), accumulating per-row parameter
-// gradients into LDS (fp32 LDS atomics, summed per block), and writes one partial gradient
+// gradients into LDS (double LDS atomics, summed per block), and writes one partial gradient
 // vector per block; a second kernel sums the block partials in double, in block order, applies
 // the Householder direction projection (householder_trafo.jl:22-40) and adds into out.
 //
@@ -156,7 +156,7 @@ __device__ __forceinline__ T bwd_elem(int op, T x, T g, const T* p, T* dp) {
       const T s1 = sigm(t1), s2 = sigm(t2), ss = s1 + s2;
       const T y = (log1p(exp(t1)) - log1p(exp(t2))) / b;
       const T q1 = s1 * ((T)1 - s1), q2 = s2 * ((T)1 - s2);
-      const T dydx = ss, dyda = s2 - s1, dydb = (s1 * (xu - a) - s2 * (xu + a)) / b - y / b;
+      const T dydx = ss, dyda = s2 - s1, dydb = (s1 * (xu - a) + s2 * (xu + a)) / b - y / b;
       const T dldx = (q1 * b - q2 * b) / ss, dlda = -(q1 + q2) * b / ss, dldb = (q1 * (xu - a) - q2 * (xu + a)) / ss;
       dp[0] += g * dyda - dlda;
       dp[1] += g * dydb - dldb;
@@ -174,7 +174,7 @@ __device__ __forceinline__ T bwd_elem(int op, T x, T g, const T* p, T* dp) {
       const T s1 = sigm(t1), s2 = sigm(t2), ss = s1 + s2;
       const T ccv = (log1p(exp(t1)) - log1p(exp(t2))) / b;  // = x (up to rounding)
       const T q1 = s1 * ((T)1 - s1), q2 = s2 * ((T)1 - s2);
-      const T cc_a = s2 - s1, cc_b = (s1 * (yu - a) - s2 * (yu + a)) / b - ccv / b, cc_c = -ss;
+      const T cc_a = s2 - s1, cc_b = (s1 * (yu - a) + s2 * (yu + a)) / b - ccv / b, cc_c = -ss;
       const T lcc_y = (q1 * b - q2 * b) / ss, lcc_a = -(q1 + q2) * b / ss, lcc_b = (q1 * (yu - a) - q2 * (yu + a)) / ss,
               lcc_c = -lcc_y;
       const T dydx = (T)1 / ss;
@@ -198,9 +198,9 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
   constexpr int SEG = D >= V ? V : D;
   constexpr int COLS = 64 / G * CPF;  // columns per wave tile (one fragment per lane)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // LDS: [grad accumulators: nparams floats][loss: 4 waves x double][records][activations]
-  float* gacc = reinterpret_cast<float*>(smem);
-  const int gbytes = ((a.nparams * 4 + 15) / 16) * 16;
+  // LDS: [grad accumulators: nparams doubles][loss: 4 waves x double][records][activations]
+  double* gacc = reinterpret_cast<double*>(smem);
+  const int gbytes = ((a.nparams * 8 + 15) / 16) * 16;
   double* lossw = reinterpret_cast<double*>(smem + gbytes);
   T* rec = reinterpret_cast<T*>(smem + gbytes + 64);
   int nrec = 0;
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
   T* act = rec + ((nrec + 3) / 4) * 4 + (threadIdx.x >> 6) * (a.nsteps * 64 * V);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < a.nparams; i += blockDim.x) gacc[i] = 0.f;
+  for (int i = tid; i < a.nparams; i += blockDim.x) gacc[i] = 0.0;
   // raw parameter records, layout [group][param][element] as the forward kernel (RV = V)
   for (int s = 0; s < a.nsteps; ++s) {
     const LayerDesc& L = a.layers[a.layer[s]];
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
           for (int e = 0; e < SEG; ++e) {
             const int row = r0 + e;
             const T contrib = g[c * SEG + e] * vx + xin[c * SEG + e] * vg;
-            if (valid[c * SEG + e]) atomicAdd(&gacc[a.goff[s] + row], (float)contrib);
+            if (valid[c * SEG + e]) atomicAdd(&gacc[a.goff[s] + row], (double)contrib);
             g[c * SEG + e] = fma(-vg, r[c * SEG + e], g[c * SEG + e]);
           }
         }
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
           const T gx = bwd_elem<T>(op, xin[e], g[e], p, dp);
           if (valid[e]) {
             const int row = r0 + e % SEG;
-            for (int q = 0; q < np; ++q) atomicAdd(&gacc[a.goff[s] + q * D + row], (float)dp[q]);
+            for (int q = 0; q < np; ++q) atomicAdd(&gacc[a.goff[s] + q * D + row], (double)dp[q]);
           }
           g[e] = valid[e] ? gx : (T)0;
         }
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
   __syncthreads();
   double* out = (double*)a.partial + (int64_t)blockIdx.x * (1 + a.nparams);
   if (tid == 0) out[0] = lossw[0] + lossw[1] + lossw[2] + lossw[3];
-  for (int i = tid; i < a.nparams; i += blockDim.x) out[1 + i] = (double)gacc[i];
+  for (int i = tid; i < a.nparams; i += blockDim.x) out[1 + i] = gacc[i];
 }
 
 // Sum the block partials (double, block order), project Householder direction gradients, add to out.
@@ -447,7 +447,7 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
   P.ga.nlayers = nlayers;
   P.ga.nparams = goff;
   const size_t esz = f64 ? 8 : 4;
-  const size_t gbytes = ((size_t)goff * 4 + 15) / 16 * 16;
+  const size_t gbytes = ((size_t)goff * 8 + 15) / 16 * 16;
   const size_t rbytes = ((size_t)(roff + 3) / 4) * 4 * esz;
   const size_t abytes = (size_t)4 * s * 64 * V * esz;
   P.lds = gbytes + 64 + rbytes + abytes;
