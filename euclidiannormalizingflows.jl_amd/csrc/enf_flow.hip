@@ -34,51 +34,9 @@
 
 #include "enf_internal.h"
 
+#include "enf_frag.h"
+
 namespace enf {
-
-// ------------------------------------------------------------------------------------------
-// device math
-// ------------------------------------------------------------------------------------------
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-constexpr double kLn2 = 0.69314718055994530942;
-constexpr double kLog2e = 1.44269504088896340736;
-
-__device__ __forceinline__ float hw_log2(float x) { return __builtin_amdgcn_logf(x); }
-__device__ __forceinline__ float hw_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
-__device__ __forceinline__ float hw_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
-__device__ __forceinline__ float hw_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
-
-// DPP cross-lane sum over aligned groups of G lanes (G <= 64, power of two). All 64 lanes must
-// be active. quad_perm(1,0,3,2) = 0xB1, quad_perm(2,3,0,1) = 0x4E, row_half_mirror = 0x141,
-// row_mirror = 0x140: after the quad steps every lane of a quad holds the quad sum, so a
-// mirror partner always lies in the other quad / half-row.
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float x) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL,
-                                                               0xF, 0xF, false));
-}
-template <int CTRL>
-__device__ __forceinline__ double dpp_d(double x) {
-  const uint64_t u = __builtin_bit_cast(uint64_t, x);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
-  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-template <int CTRL, typename T>
-__device__ __forceinline__ T dpp(T x) {
-  if constexpr (std::is_same_v<T, float>) return dpp_f<CTRL>(x);
-  else return dpp_d<CTRL>(x);
-}
-template <int G, typename T>
-__device__ __forceinline__ T group_sum(T x) {
-  if constexpr (G >= 2) x += dpp<0xB1>(x);
-  if constexpr (G >= 4) x += dpp<0x4E>(x);
-  if constexpr (G >= 8) x += dpp<0x141>(x);
-  if constexpr (G >= 16) x += dpp<0x140>(x);
-  if constexpr (G >= 32) x += __shfl_xor(x, 16);
-  if constexpr (G >= 64) x += __shfl_xor(x, 32);
-  return x;
-}
 
 // ------------------------------------------------------------------------------------------
 // parameter records in LDS
@@ -190,168 +148,6 @@ __device__ void build_program(const FlowArgs& a, T* __restrict__ rec, double* __
   __syncthreads();
 }
 
-// ------------------------------------------------------------------------------------------
-// per-element transforms. acc is the running per-lane ladj partial of one column, in units of
-// log2 (fp32) or natural log (fp64): ladj = C_total + UNIT * acc.
-// ------------------------------------------------------------------------------------------
-template <typename T>
-struct Unit;
-template <>
-struct Unit<float> { static constexpr float v = (float)kLn2; };
-template <>
-struct Unit<double> { static constexpr double v = 1.0; };
-
-// fp32 robust Johnson element (huge |z|, Inf, NaN): the rare path of the fragment kernel and the
-// generic kernel's form. asinh stays finite for |z| up to FLT_MAX; log(1+z^2) overflows to +Inf
-// exactly where the reference's fp32 `1 + ((x-xi)/lambda)^2` does (johnson_trafo.jl:41), so
-// the ladj is -Inf there, as in the reference.
-struct YL { float y, l; };
-__device__ __forceinline__ YL johnson_fwd_f32_slow(float z, float g, float d2) {
-  const float t = fabsf(z);
-  const float q = fmaf(z, z, 1.0f);
-  const float L = t > 1e18f ? hw_log2(t) + 1.0f : hw_log2(t + hw_sqrt(q));  // log2(2|z|) when huge
-  return {fmaf(d2, copysignf(L, z), g), -0.5f * hw_log2(q)};             // ladj part in log2 units
-}
-
-// ------------------------------------------------------------------------------------------
-// the fragment kernel
-// ------------------------------------------------------------------------------------------
-template <typename T, int D>
-struct Frag {
-  static constexpr int V = 16 / (int)sizeof(T);        // elements per 16-B fragment
-  static constexpr int G = D >= V ? D / V : 1;         // lanes per column
-  static constexpr int CPF = D >= V ? 1 : V / D;       // columns per fragment
-  static constexpr int SEG = D >= V ? V : D;           // elements of one column in a fragment
-  static constexpr int COLS_PER_INSTR = 64 / G * CPF;  // columns per wave-instruction
-  static_assert(D >= V ? (D % V == 0 && G <= 64) : (V % D == 0), "unsupported D");
-};
-
-// fragment u of this lane holds rows r0 .. r0+SEG-1 of columns colf(u) .. colf(u)+CPF-1
-template <typename T, int D>
-__device__ __forceinline__ int64_t frag_col(int64_t col0, int u, int lane) {
-  using F = Frag<T, D>;
-  return col0 + (int64_t)u * F::COLS_PER_INSTR + (lane / F::G) * F::CPF;
-}
-
-// One wave tile = U fully coalesced 1-KiB wave-instructions (ldx == D, 16-B aligned).
-// DBG (diagnostic builds only, ENF_DEBUG_MODE): 1 = synthesize the tile instead of loading it,
-// 2 = also skip the stores (compute-only timing).
-template <typename T, int D, int U, bool TAIL, int DBG = 0>
-__device__ __forceinline__ void load_tile(const FlowArgs& a, int64_t col0, T (&x)[U][Frag<T, D>::V]) {
-  using F = Frag<T, D>;
-  constexpr int V = F::V, G = F::G, SEG = F::SEG;
-  const int lane = threadIdx.x & 63;
-  const int r0 = D >= V ? V * (lane % G) : 0;
-  const T* __restrict__ X = (const T*)a.X;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t cf = frag_col<T, D>(col0, u, lane);
-    const int64_t eoff = cf * D + r0;
-    if (DBG >= 1) {
-#pragma unroll
-      for (int e = 0; e < V; ++e) x[u][e] = (T)(lane + 3 * u + e) * (T)0.03125 - (T)1;
-    } else if (!TAIL) {
-      const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X + eoff));
-      __builtin_memcpy(&x[u][0], &v4, 16);
-    } else {
-#pragma unroll
-      for (int e = 0; e < V; ++e) x[u][e] = (cf + e / SEG) < a.N ? X[eoff + e] : (T)0;
-    }
-  }
-}
-
-// 16-byte LDS read of V parameter values
-template <typename T, int V>
-__device__ __forceinline__ void lds_vec(const T* __restrict__ p, T (&v)[V]) {
-  static_assert(V * sizeof(T) == 16, "16-byte vectors");
-  const u32x4 w = *reinterpret_cast<const u32x4*>(p);
-  __builtin_memcpy(&v[0], &w, 16);
-}
-
-// Run the step program on one wave tile held in registers (x), then store Y and ladj.
-// ladj output of a wave tile. G == 1: a lane owns whole columns (CPF per fragment) and stores
-// them as one CPF-vector per fragment. G > 1: column totals are staged through the wave's LDS
-// slots and written by NLS = ceil(TC/64) full-wave stores (TC = columns per tile; when TC < 64
-// the upper lanes store duplicates of the same values to the same addresses, so no lane mask
-// and no branch is needed: the vmcnt accounting of the tile loop stays static).
-template <typename T, int D, int U>
-struct LadjOut {
-  using F = Frag<T, D>;
-  static constexpr int TC = F::COLS_PER_INSTR * U;
-  static constexpr int NLS = F::G == 1 ? U : (TC + 63) / 64;
-  static constexpr int W = F::G == 1 ? F::CPF : 1;  // values per lane per store
-  __device__ static __forceinline__ int64_t col(int64_t col0, int k, int lane) {
-    if constexpr (F::G == 1) return frag_col<T, D>(col0, k, lane);
-    else return col0 + (int64_t)k * 64 + (TC >= 64 ? lane : lane % TC);
-  }
-};
-
-// LM: 0 no ladj, 1 write ladj, 2 add to ladj (accumulate_ladj)
-template <typename T, int D, int U, int LM>
-__device__ __forceinline__ void load_ladj_old(const FlowArgs& a, int64_t col0, T (&old)[LadjOut<T, D, U>::NLS][LadjOut<T, D, U>::W]) {
-  using LO = LadjOut<T, D, U>;
-  const int lane = threadIdx.x & 63;
-  const T* __restrict__ ladj = (const T*)a.ladj;
-#pragma unroll
-  for (int k = 0; k < LO::NLS; ++k)
-#pragma unroll
-    for (int w = 0; w < LO::W; ++w) old[k][w] = LM == 2 ? ladj[LO::col(col0, k, lane) + w] : (T)0;
-}
-
-// register tile types (aliases avoid a clang parse ambiguity of T (&x)[U][Frag<T, D>::V] params)
-template <typename T, int D, int U>
-using Tile = T[U][Frag<T, D>::V];
-template <typename T, int D, int U>
-using Acc = T[U][Frag<T, D>::CPF];
-#define ENF_FRAG_CONSTS                                   \
-  using F = Frag<T, D>;                                   \
-  constexpr int V = F::V, G = F::G, CPF = F::CPF, SEG = F::SEG; \
-  (void)G; (void)CPF; (void)SEG;
-
-// ---- step bodies: one transform applied to the wave tile x (U fragments of V values per lane).
-// r points at this lane's record group ([param][element], 16-byte vectors). acc: ladj partials.
-// Column dot products of all U*CPF column segments of the tile with the lane's 16-byte vector v,
-// reduced over the G lanes of each column. Every stage runs across all segments before the next
-// one (U*CPF independent chains), so neither the FMA chain nor the DPP stages stall the wave.
-template <typename T, int D, int U>
-__device__ __forceinline__ void tile_dots(const Tile<T, D, U>& x, const T (&v)[Frag<T, D>::V],
-                                          T (&dot)[U][Frag<T, D>::CPF]) {
-  ENF_FRAG_CONSTS
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int c = 0; c < CPF; ++c) dot[u][c] = v[c * SEG] * x[u][c * SEG];
-#pragma unroll
-  for (int e = 1; e < SEG; ++e)
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int c = 0; c < CPF; ++c) dot[u][c] = fma(v[c * SEG + e], x[u][c * SEG + e], dot[u][c]);
-  if constexpr (G >= 2) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) dot[u][0] += dpp<0xB1>(dot[u][0]);
-  }
-  if constexpr (G >= 4) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) dot[u][0] += dpp<0x4E>(dot[u][0]);
-  }
-  if constexpr (G >= 8) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) dot[u][0] += dpp<0x141>(dot[u][0]);
-  }
-  if constexpr (G >= 16) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) dot[u][0] += dpp<0x140>(dot[u][0]);
-  }
-  if constexpr (G >= 32) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) dot[u][0] += __shfl_xor(dot[u][0], 16);
-  }
-  if constexpr (G >= 64) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) dot[u][0] += __shfl_xor(dot[u][0], 32);
-  }
-}
 
 // y = x - vh (vh'x), vh = v*sqrt(2/v'v): householder_trafo!(y, v, x) (householder_trafo.jl:8-11)
 template <typename T, int D, int U>
@@ -440,41 +236,6 @@ __device__ __forceinline__ void step_johnson(Tile<T, D, U>& x, Acc<T, D, U>& acc
             if (LADJ) acc[u][e / SEG] -= 0.5 * log1p(z * z);
           }
       }
-}
-
-// Compiled-program fusion of a reflection and the Johnson layer after it: the reflected value
-// x' = x - vh (vh'x) only enters J through z = (x' - xi)/lambda, so z is formed directly as
-// fma(-dot, vh/lambda, fma(x, 1/lambda, -xi/lambda)) -- two FMAs per element instead of the
-// update, the subtraction and the scaling. (fp32 path; same normwise rounding class as the
-// unfused sequence.)
-template <typename T, int D, int U, bool LADJ>
-__device__ __forceinline__ void step_hj_fused(Tile<T, D, U>& x, Acc<T, D, U>& acc, const T* __restrict__ rh,
-                                              const T* __restrict__ rj) {
-  ENF_FRAG_CONSTS
-  static_assert(std::is_same_v<T, float>, "fp32 only");
-  T vh[V], pg[V], pd[V], px[V], pl[V];
-  lds_vec<T, V>(rh, vh);
-  lds_vec<T, V>(rj, pg);
-  lds_vec<T, V>(rj + V, pd);
-  lds_vec<T, V>(rj + 2 * V, px);
-  lds_vec<T, V>(rj + 3 * V, pl);
-  T dot[U][CPF];
-  tile_dots<T, D, U>(x, vh, dot);
-  float w[V], c[V];
-#pragma unroll
-  for (int e = 0; e < V; ++e) {
-    w[e] = vh[e] * pl[e];
-    c[e] = -px[e] * pl[e];
-  }
-  float zmax = 0.f;
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int e = 0; e < V; ++e) {
-      x[u][e] = fmaf(-dot[u][e / SEG], w[e], fmaf(x[u][e], pl[e], c[e]));  // z
-      zmax = fmaxf(zmax, fabsf(x[u][e]));
-    }
-  johnson_from_z<D, U, LADJ>(x, acc, pg, pd, zmax);
 }
 
 template <typename T, int D, int U, bool LADJ>
@@ -615,74 +376,9 @@ __device__ __forceinline__ void step_center_contract(Tile<T, D, U>& x, Acc<T, D,
       }
 }
 
-// ---- tile epilogue: store Y and the ladj
-template <typename T, int D, int U, int LM, bool TAIL, int DBG>
-__device__ __forceinline__ void store_tile(const FlowArgs& a, T ctot, int64_t col0, Tile<T, D, U>& x,
-                                           Acc<T, D, U>& acc,
-                                           const T (&old)[LadjOut<T, D, U>::NLS][LadjOut<T, D, U>::W],
-                                           T* __restrict__ stage) {
-  ENF_FRAG_CONSTS
-  constexpr bool LADJ = LM > 0;
-  const int lane = threadIdx.x & 63;
-  T* __restrict__ Y = (T*)a.Y;
-  const int64_t N = a.N;
-  const int r0 = D >= V ? V * (lane % G) : 0;
-  int64_t colf[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) colf[u] = frag_col<T, D>(col0, u, lane);
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t eoff = colf[u] * D + r0;
-    if (DBG == 2) {
-      if (x[u][0] == (T)1234.5) Y[eoff] = x[u][1];  // keeps the compute alive, never true in practice
-    } else if (!TAIL) {
-      u32x4 v4;
-      __builtin_memcpy(&v4, &x[u][0], 16);
-      __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(Y + eoff));
-    } else {
-#pragma unroll
-      for (int e = 0; e < V; ++e)
-        if (colf[u] + e / SEG < N) Y[eoff + e] = x[u][e];
-    }
-  }
-  if constexpr (LADJ) {
-    using LO = LadjOut<T, D, U>;
-    T* __restrict__ ladj = (T*)a.ladj;
-    if constexpr (G == 1) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-#pragma unroll
-        for (int c = 0; c < CPF; ++c) {
-          const int64_t col = colf[u] + c;
-          const T v = fma(Unit<T>::v, acc[u][c], ctot) + old[u][c];
-          if (!TAIL) ladj[col] = v;
-          else if (col < N) ladj[col] = v;
-        }
-      }
-    } else {
-      // group totals -> the wave's LDS slots (leaders only) -> full-wave coalesced stores
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const T tot = group_sum<G>(acc[u][0]);
-        if ((lane % G) == 0) stage[u * F::COLS_PER_INSTR + lane / G] = tot;
-      }
-#pragma unroll
-      for (int k = 0; k < LO::NLS; ++k) {
-        const int c = k * 64 + (LO::TC >= 64 ? lane : lane % LO::TC);
-        const T v = fma(Unit<T>::v, stage[c], ctot) + old[k][0];
-        const int64_t col = col0 + c;
-        if (!TAIL) ladj[col] = v;
-        else if (col < N) ladj[col] = v;
-      }
-    }
-  }
-}
 
-// Program: PROG == 0 interprets the step table of the kernel arguments; PROG == n > 0 is the
-// compile-time program (H o J)^n -- the config 3/4/5 flows -- with the same parameter records at
-// compile-time offsets, so the per-step dispatch disappears and the compiler schedules across
-// steps (parameter LDS reads hoisted ahead of the preceding step's arithmetic).
-template <typename T, int D, int U, int LM, bool TAIL, int DBG, int PROG>
+// Interpreter: runs the step table of the kernel arguments on one register tile, then stores it.
+template <typename T, int D, int U, int LM, bool TAIL, int DBG>
 __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict__ rec, T ctot,
                                           int64_t col0, Tile<T, D, U>& x,
                                           const T (&old)[LadjOut<T, D, U>::NLS][LadjOut<T, D, U>::W],
@@ -703,33 +399,37 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
 #pragma unroll
     for (int e = 0; e < V; ++e) asm volatile("" : "+v"(x[u][e]));
 
-  if constexpr (PROG > 0) {
-    constexpr int NE = D > V ? D : V;       // record entries per parameter
-    constexpr int HREC = NE, JREC = 4 * NE;  // record sizes (multiples of V)
-#pragma unroll
-    for (int p = 0; p < PROG; ++p)
-      step_hj_fused<T, D, U, LADJ>(x, acc, rec + p * (HREC + JREC) + grp * V,
-                                   rec + p * (HREC + JREC) + HREC + grp * 4 * V);
-  } else {
-    int desc = a.desc[0];  // op | record offset << 4; a.desc[nsteps] is a sentinel
-    for (int s = 0; s < a.nsteps; ++s) {
-      const int next = a.desc[s + 1];  // scalar load issued a step ahead
-      const int op = desc & 15;
-      const T* __restrict__ r = rec + (desc >> 4) + grp * record_width(op) * V;
-      desc = next;
-      if (op == OP_HOUSEHOLDER) step_householder<T, D, U>(x, r);
-      else if (op == OP_JOHNSON) step_johnson<T, D, U, LADJ>(x, acc, r);
-      else if (op == OP_JOHNSON_INV) step_johnson_inv<T, D, U, LADJ>(x, acc, r);
-      else if (op == OP_SCALESHIFT) step_scaleshift<T, D, U>(x, r);
-      else if (op == OP_CENTER_STRETCH) step_center_stretch<T, D, U, LADJ>(x, acc, r);
-      else step_center_contract<T, D, U, LADJ>(x, acc, r);
-    }
+  int desc = a.desc[0];  // op | record offset << 4; a.desc[nsteps] is a sentinel
+  for (int s = 0; s < a.nsteps; ++s) {
+    const int next = a.desc[s + 1];  // scalar load issued a step ahead
+    const int op = desc & 15;
+    const T* __restrict__ r = rec + (desc >> 4) + grp * record_width(op) * V;
+    desc = next;
+    if (op == OP_HOUSEHOLDER) step_householder<T, D, U>(x, r);
+    else if (op == OP_JOHNSON) step_johnson<T, D, U, LADJ>(x, acc, r);
+    else if (op == OP_JOHNSON_INV) step_johnson_inv<T, D, U, LADJ>(x, acc, r);
+    else if (op == OP_SCALESHIFT) step_scaleshift<T, D, U>(x, r);
+    else if (op == OP_CENTER_STRETCH) step_center_stretch<T, D, U, LADJ>(x, acc, r);
+    else step_center_contract<T, D, U, LADJ>(x, acc, r);
   }
   store_tile<T, D, U, LM, TAIL, DBG>(a, ctot, col0, x, acc, old, stage);
 }
 
+template <typename T, int D, int U, int LM>
+struct InterpBody {
+  const FlowArgs& a;
+  const T* rec;
+  T ctot;
+  T* stage;
+  template <bool TAIL, int DBG>
+  __device__ __forceinline__ void tile(int64_t col0, Tile<T, D, U>& x,
+                                       const T (&old)[LadjOut<T, D, U>::NLS][LadjOut<T, D, U>::W]) {
+    flow_tile<T, D, U, LM, TAIL, DBG>(a, rec, ctot, col0, x, old, stage);
+  }
+};
+
 // OCC: minimum waves per SIMD the register allocation must allow (launch-bounds occupancy hint)
-template <typename T, int D, int U, int LM, int OCC, int DBG = 0, int PROG = 0>
+template <typename T, int D, int U, int LM, int OCC, int DBG = 0>
 __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* stepc = reinterpret_cast<double*>(smem);
@@ -737,62 +437,8 @@ __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
   T* stage = reinterpret_cast<T*>(smem + kLdsScalars) + (threadIdx.x >> 6) * kStagePerWave;
   T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
   build_program<T, D, Frag<T, D>::V>(a, rec, stepc, ctotp);
-  const T ctot = (T)*ctotp;
-
-  using F = Frag<T, D>;
-  using LO = LadjOut<T, D, U>;
-  static_assert(F::G == 1 || LO::TC <= kStagePerWave, "ladj staging area too small");
-  constexpr int64_t COLS_PER_TILE = (int64_t)F::COLS_PER_INSTR * U;
-  const int64_t ntiles_full = a.N / COLS_PER_TILE;
-  // wave-uniform tile indices (readfirstlane: scalar registers, uniform branches)
-  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) +
-                          __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  // software pipeline: the next tile's loads are in flight while this tile computes. Memory
-  // operations per iteration are branch-free and in a fixed order (old ladj, prefetch, stores):
-  // past the last tile the prefetch re-reads the current tile instead of being skipped, so the
-  // compiler's vmcnt waits only ever cover the current tile.
-  // The first half-iteration is peeled so that the loop header is reached from the entry and from
-  // the back edge with the same outstanding memory operations (the previous tile's stores behind
-  // the current tile's loads): the compiler's static vmcnt waits then leave the stores in flight.
-  using XT = T[U][F::V];
-  using OT = T[LO::NLS][LO::W];
-  XT xa, xb;
-  OT old;
-  const int64_t t = wave_id;
-  if (t < ntiles_full) {
-    load_tile<T, D, U, false, DBG>(a, t * COLS_PER_TILE, xa);
-    int64_t t1 = t + nwaves;
-    load_ladj_old<T, D, U, LM>(a, t * COLS_PER_TILE, old);
-    load_tile<T, D, U, false, DBG>(a, (t1 < ntiles_full ? t1 : t) * COLS_PER_TILE, xb);
-    flow_tile<T, D, U, LM, false, DBG, PROG>(a, rec, ctot, t * COLS_PER_TILE, xa, old, stage);
-    while (t1 < ntiles_full) {
-      const int64_t t2 = t1 + nwaves;
-      load_ladj_old<T, D, U, LM>(a, t1 * COLS_PER_TILE, old);
-      load_tile<T, D, U, false, DBG>(a, (t2 < ntiles_full ? t2 : t1) * COLS_PER_TILE, xa);
-      flow_tile<T, D, U, LM, false, DBG, PROG>(a, rec, ctot, t1 * COLS_PER_TILE, xb, old, stage);
-      if (t2 >= ntiles_full) break;
-      const int64_t t3 = t2 + nwaves;
-      load_ladj_old<T, D, U, LM>(a, t2 * COLS_PER_TILE, old);
-      load_tile<T, D, U, false, DBG>(a, (t3 < ntiles_full ? t3 : t2) * COLS_PER_TILE, xb);
-      flow_tile<T, D, U, LM, false, DBG, PROG>(a, rec, ctot, t2 * COLS_PER_TILE, xa, old, stage);
-      t1 = t3;
-    }
-  }
-  if (ntiles_full * COLS_PER_TILE < a.N && wave_id == ntiles_full % nwaves) {
-    const int64_t c0 = ntiles_full * COLS_PER_TILE;
-    load_tile<T, D, U, true>(a, c0, xa);
-    // tail: old ladj only for existing columns
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < LO::NLS; ++k)
-#pragma unroll
-      for (int w = 0; w < LO::W; ++w) {
-        const int64_t c = LO::col(c0, k, lane) + w;
-        old[k][w] = (LM == 2 && c < a.N) ? ((const T*)a.ladj)[c] : (T)0;
-      }
-    flow_tile<T, D, U, LM, true, 0, PROG>(a, rec, ctot, c0, xa, old, stage);
-  }
+  InterpBody<T, D, U, LM> body{a, rec, (T)*ctotp, stage};
+  frag_stream<T, D, U, LM, DBG>(a, body);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -899,65 +545,56 @@ size_t program_lds_bytes(const FlowArgs& a, size_t elem) {
 }
 
 // Tuning knobs (development only): ENF_BLOCKS_PER_CU caps resident blocks per CU in the grid size,
-// ENF_FRAG_U selects the tile depth U for D >= 16.
-static int env_int(const char* name, int dflt) {
+// ENF_FRAG_U / ENF_FRAG_OCC select fp32 D = 32 interpreter variants, ENF_DEBUG_MODE the diagnostic
+// builds (1: synthesized tile instead of loads, 2: also no stores), ENF_NO_SPECIALIZE=1 disables the
+// compiled (H o J)^n programs (enf_flow_hj.hip).
+int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v && *v ? atoi(v) : dflt;
 }
 
-template <typename T, int D, int U, int LM, int OCC = 1, int DBG = 0, int PROG = 0>
-static hipError_t launch_frag(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
-  using F = Frag<T, D>;
-  const int64_t cols_per_block = (int64_t)F::COLS_PER_INSTR * U * 4;
+hipError_t frag_grid(const void* kernel, int64_t N, int64_t cols_per_block, size_t lds, const DeviceInfo& dev,
+                     int64_t* blocks) {
   int per_cu = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, flow_frag_kernel<T, D, U, LM, OCC, DBG, PROG>, 256, lds);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds);
   if (e != hipSuccess) return e;
   static const int cap_env = env_int("ENF_BLOCKS_PER_CU", 0);
   if (cap_env > 0 && per_cu > cap_env) per_cu = cap_env;
   if (per_cu < 1) per_cu = 1;
-  int64_t blocks = (a.N + cols_per_block - 1) / cols_per_block;
+  int64_t b = (N + cols_per_block - 1) / cols_per_block;
   const int64_t cap = (int64_t)dev.num_cu * per_cu;
-  if (blocks > cap) blocks = cap;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL((flow_frag_kernel<T, D, U, LM, OCC, DBG, PROG>), dim3((unsigned)blocks), dim3(256), lds, st, a);
+  if (b > cap) b = cap;
+  *blocks = b < 1 ? 1 : b;
+  return hipSuccess;
+}
+
+template <typename T, int D, int U, int LM, int OCC = 1, int DBG = 0>
+static hipError_t launch_frag(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
+  using F = Frag<T, D>;
+  const void* k = reinterpret_cast<const void*>(&flow_frag_kernel<T, D, U, LM, OCC, DBG>);
+  int64_t blocks = 0;
+  hipError_t e = frag_grid(k, a.N, (int64_t)F::COLS_PER_INSTR * U * 4, lds, dev, &blocks);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((flow_frag_kernel<T, D, U, LM, OCC, DBG>), dim3((unsigned)blocks), dim3(256), lds, st, a);
   return hipGetLastError();
-}
-
-// n if the step program is (H o J)^n (Householder first, one reflection per H) with the records at
-// the offsets the compiled program assumes, else 0.
-static int hj_pairs(const FlowArgs& a, int V) {
-  if (a.nsteps < 2 || (a.nsteps & 1)) return 0;
-  const int NE = a.D > V ? a.D : V;
-  for (int s = 0; s < a.nsteps; ++s) {
-    const int p = s / 2;
-    const int want_op = (s & 1) ? OP_JOHNSON : OP_HOUSEHOLDER;
-    const int want_off = p * 5 * NE + ((s & 1) ? NE : 0);
-    if (a.steps[s].op != want_op || a.steps[s].off != want_off || a.desc[s] != (want_op | (want_off << 4))) return 0;
-  }
-  return a.nsteps / 2;
-}
-
-template <typename T, int D, int LADJ>
-static hipError_t launch_hj(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev, int n) {
-  switch (n) {
-    case 1: return launch_frag<T, D, 4, LADJ, 1, 0, 1>(a, lds, st, dev);
-    case 2: return launch_frag<T, D, 4, LADJ, 1, 0, 2>(a, lds, st, dev);
-    case 3: return launch_frag<T, D, 4, LADJ, 1, 0, 3>(a, lds, st, dev);
-    case 4: return launch_frag<T, D, 4, LADJ, 1, 0, 4>(a, lds, st, dev);
-    default: return launch_frag<T, D, 4, LADJ>(a, lds, st, dev);
-  }
 }
 
 template <typename T, int LADJ>
 static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
-  constexpr bool f32 = std::is_same_v<T, float>;
-  // compiled (H o J)^n programs (fp32, D = 32 / 64): ENF_NO_SPECIALIZE=1 forces the interpreter
-  static const int nospec = env_int("ENF_NO_SPECIALIZE", 0);
-  if constexpr (f32) {
-    const int n = nospec ? 0 : hj_pairs(a, 4);
-    if (n >= 1 && n <= 4 && env_int("ENF_DEBUG_MODE", 0) == 0) {
-      if (a.D == 32) return launch_hj<T, 32, LADJ>(a, lds, st, dev, n);
-      if (a.D == 64) return launch_hj<T, 64, LADJ>(a, lds, st, dev, n);
+  if constexpr (std::is_same_v<T, float>) {
+    static const int nospec = env_int("ENF_NO_SPECIALIZE", 0);
+    static const int dbg = env_int("ENF_DEBUG_MODE", 0);
+    if (!nospec && hj_program_pairs(a) > 0) {
+      hipError_t e = launch_hj_program(a, LADJ, dbg, st, dev);
+      if (e != hipErrorNotSupported) return e;
+    }
+    if (a.D == 32) {
+      static const int u = env_int("ENF_FRAG_U", 4);
+      static const int occ = env_int("ENF_FRAG_OCC", 1);
+      if (dbg == 1) return launch_frag<T, 32, 4, LADJ, 1, 1>(a, lds, st, dev);
+      if (dbg == 2) return launch_frag<T, 32, 4, LADJ, 1, 2>(a, lds, st, dev);
+      if (u == 2) return launch_frag<T, 32, 2, LADJ>(a, lds, st, dev);
+      if (u == 4 && occ == 5) return launch_frag<T, 32, 4, LADJ, 5>(a, lds, st, dev);
     }
   }
   switch (a.D) {
@@ -966,20 +603,10 @@ static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, cons
     case 4: return launch_frag<T, 4, 4, LADJ>(a, lds, st, dev);
     case 8: return launch_frag<T, 8, 4, LADJ>(a, lds, st, dev);
     case 16: return launch_frag<T, 16, 4, LADJ>(a, lds, st, dev);
-    case 32: {
-      // tuning variants (ENF_FRAG_U / ENF_FRAG_OCC), default U=4 without an occupancy bound
-      static const int u = env_int("ENF_FRAG_U", 4);
-      static const int occ = env_int("ENF_FRAG_OCC", 1);
-      static const int dbg = env_int("ENF_DEBUG_MODE", 0);
-      if (dbg == 1) return launch_frag<T, 32, 4, LADJ, 1, 1>(a, lds, st, dev);
-      if (dbg == 2) return launch_frag<T, 32, 4, LADJ, 1, 2>(a, lds, st, dev);
-      if (u == 2 && occ == 6) return launch_frag<T, 32, 2, LADJ, 6>(a, lds, st, dev);
-      if (u == 2 && occ == 8) return launch_frag<T, 32, 2, LADJ, 8>(a, lds, st, dev);
-      if (u == 2) return launch_frag<T, 32, 2, LADJ>(a, lds, st, dev);
-      if (u == 4 && occ == 5) return launch_frag<T, 32, 4, LADJ, 5>(a, lds, st, dev);
-      return launch_frag<T, 32, 4, LADJ>(a, lds, st, dev);
-    }
-    case 64: return f32 ? launch_frag<T, 64, 4, LADJ>(a, lds, st, dev) : launch_frag<T, 64, 2, LADJ>(a, lds, st, dev);
+    case 32: return launch_frag<T, 32, 4, LADJ>(a, lds, st, dev);
+    case 64:
+      if constexpr (std::is_same_v<T, float>) return launch_frag<T, 64, 4, LADJ>(a, lds, st, dev);
+      else return launch_frag<T, 64, 2, LADJ>(a, lds, st, dev);
     default: break;
   }
   return hipErrorInvalidValue;

@@ -86,4 +86,10 @@ size_t program_lds_bytes(const FlowArgs& a, size_t elem);
 bool frag_supported(const FlowArgs& a, size_t elem);
 hipError_t launch_flow(const FlowArgs& a, bool f64, hipStream_t st, const DeviceInfo& dev);
 
+// Compiled (J o H)^n program (enf_flow_hj.hip): n if the fp32 step table is H, J, H, J, ... (one
+// reflection per H, Johnson forward) on the fragment path with D in {32, 64}, else 0.
+int hj_program_pairs(const FlowArgs& a);
+// lm: 0 no ladj, 1 write, 2 accumulate; dbg: ENF_DEBUG_MODE. hipErrorNotSupported: not a program.
+hipError_t launch_hj_program(const FlowArgs& a, int lm, int dbg, hipStream_t st, const DeviceInfo& dev);
+
 }  // namespace enf
