@@ -44,6 +44,16 @@ def build_flow(D, pairs, np_dtype, seed=42, pattern=None):
     return layers
 
 
+def max_over_ranks(values, device, world):
+    """Element-wise max over ranks of per-rank values (the timed region's wall time and kernel
+    time): the whole job is as slow as its slowest GPU. torch.distributed all-reduce(MAX)
+    (RCCL between GPUs; gloo in the CPU tests)."""
+    t = torch.tensor(values, device=device, dtype=torch.float64)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return [float(v) for v in t]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -119,13 +129,7 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # HIP events on the launch stream
-    t_local = wall
-    if world > 1:
-        tt = torch.tensor([t_local, kern_ms], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        t_local, kern_ms_max = float(tt[0]), float(tt[1])
-    else:
-        kern_ms_max = kern_ms
+    t_local, kern_ms_max = max_over_ranks([wall, kern_ms], dev, world)
     ms_per_step = t_local / args.steps * 1e3
     total_samples = N * world * args.steps
     value = total_samples / t_local

@@ -26,13 +26,15 @@ from .train import (  # noqa: F401
     ADAGrad,
     FlowState,
     WhiteningResult,
+    allreduce_sum_,
+    minibatch_plan,
     mvnormal_negll_trafo,
     mvnormal_negll_trafograd,
     optimize_whitening,
 )
 
 __all__ = [
-    "ADAGrad", "FlowState", "WhiteningResult", "mvnormal_negll_trafo", "mvnormal_negll_trafograd",
+    "ADAGrad", "FlowState", "WhiteningResult", "allreduce_sum_", "minibatch_plan", "mvnormal_negll_trafo", "mvnormal_negll_trafograd",
     "optimize_whitening",
     "ScaleShiftTrafo", "CenterStretch", "CenterContract", "JohnsonTrafo", "JohnsonTrafoInv",
     "HouseholderTrafo", "ComposedFunction", "compose", "inverse", "with_logabsdet_jacobian",

@@ -201,6 +201,29 @@ def mvnormal_negll_trafo(trafo, X) -> float:
     return mvnormal_negll_trafograd(trafo, X)[0]
 
 
+def minibatch_plan(N: int, nbatches: int, rank: int = 0, world: int = 1):
+    """Minibatches of optimize_whitening (src/optimize_whitening.jl:31-32: batchsize =
+    round(Int, N/nbatches), Iterators.partition, the last batch possibly shorter) and this rank's
+    contiguous share of each: a list of (B, lo, hi) with the batch size B and the column range
+    [lo, hi) this rank processes. The shares of all ranks tile every batch exactly once."""
+    batchsize = max(int(round(N / nbatches)), 1)
+    plan = []
+    for b0 in range(0, N, batchsize):
+        B = min(b0 + batchsize, N) - b0
+        plan.append((B, b0 + (B * rank) // world, b0 + (B * (rank + 1)) // world))
+    return plan
+
+
+def allreduce_sum_(buf: torch.Tensor, world: int, group=None) -> torch.Tensor:
+    """In-place cross-rank sum of the (1 + P) loss/gradient sums (torch.distributed: RCCL on ROCm,
+    gloo on CPU); a no-op at world size 1. Every rank then normalises by the GLOBAL batch size."""
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    return buf
+
+
 def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None, nbatches: int = 100,
                        nepochs: int = 100, optstate: Optional[FlowState] = None,
                        negll_history: Optional[List[float]] = None, process_group=None) -> WhiteningResult:
@@ -220,33 +243,27 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
     if process_group is not None or (dist.is_available() and dist.is_initialized()):
         world = dist.get_world_size(process_group)
         rank = dist.get_rank(process_group)
-    batchsize = int(round(N / nbatches))
-    batchsize = max(batchsize, 1)
-    starts = list(range(0, N, batchsize))
+    plan = minibatch_plan(N, nbatches, rank, world)
+    batchsize = max(B for B, _, _ in plan)
     L = _lib.lib()
     dt = _lib.ENF_F64 if dtype == torch.float64 else _lib.ENF_F32
     out = torch.zeros(1 + state.nparams, dtype=dtype, device=M.device)
     ws = _workspace(state, batchsize)
-    hist = torch.zeros(nepochs * len(starts), dtype=torch.float64, device=M.device)
+    hist = torch.zeros(nepochs * len(plan), dtype=torch.float64, device=M.device)
     hcols = state.householder_columns()
     segs = [(int(state.offsets[i]), int(state.offsets[i + 1])) for i, tr in enumerate(state.trainable) if tr]
     step = 0
     with torch.cuda.device(M.device):
         stream = torch.cuda.current_stream(M.device).cuda_stream
         for _ in range(nepochs):
-            for b0 in starts:
-                b1 = min(b0 + batchsize, N)
-                B = b1 - b0
-                lo = b0 + (B * rank) // world
-                hi = b0 + (B * (rank + 1)) // world
+            for B, lo, hi in plan:
                 out.zero_()
                 if hi > lo:
                     Xb = M[:, lo:hi]
                     _lib.check(L.enf_flow_negll_grad(dt, D, hi - lo, Xb.data_ptr(), _ld(M), state.layers(),
                                                      len(state.trafos), out.data_ptr(), ws.data_ptr(),
                                                      ws.numel() * 8, stream))
-                if world > 1:
-                    dist.all_reduce(out, group=process_group)
+                allreduce_sum_(out, world, process_group)
                 hist[step:step + 1].copy_(out[0:1] / B)
                 g = out[1:]
                 for s0, s1 in segs:
