@@ -44,13 +44,124 @@ constexpr size_t kHjHeader = kHjScratch + 4 * kStagePerWave * sizeof(float);
 
 static size_t hj_lds_bytes(int D, int n) { return kHjHeader + (size_t)(n + 1) * 4 * D * sizeof(float); }
 
-// Records, pair p < n: [group g = d / 4][param q in (a, P, Q, R)][e = d % 4]; record n (final):
-// same layout with (gamma_{n-1}, delta'_{n-1}, 0, 0). A lane of group g reads each parameter of its
-// four rows with one 16-byte LDS read.
-template <int D>
+// Register layout of the compiled program: a lane owns R rows of ONE column as NF = R/4 16-byte
+// fragments; fragment h holds rows h*(D/NF) + 4*g .. +3 with g = lane % G the lane's row group and
+// G = D/R lanes per column (adjacent lanes). A slab is one load instruction per fragment and
+// covers CPS = 64/G columns; a wave tile is U slabs. R = 8 halves the DPP reduction stages of the
+// Householder dot and the ladj column sum against R = 4 and gives one ladj log2 per 8 rows; the
+// price is that a D = 32 load instruction covers half of each 128-byte column line (16 lines, the
+// other halves follow in the next instruction).
+template <int D, int R, int U>
+struct HJLay {
+  static constexpr int NF = R / 4;
+  static constexpr int G = D / R;
+  static constexpr int CPS = 64 / G;
+  static constexpr int TC = CPS * U;  // columns per wave tile
+  static constexpr int NLS = (TC + 63) / 64;
+  static_assert(R % 4 == 0 && D % R == 0 && G >= 2 && G <= 64, "layout");
+  static_assert(TC <= kStagePerWave, "ladj staging");
+  __device__ static __forceinline__ int64_t col(int64_t col0, int u, int lane) {
+    return col0 + (int64_t)u * CPS + lane / G;
+  }
+  __device__ static __forceinline__ int row(int h, int lane) { return h * (D / NF) + 4 * (lane % G); }
+  __device__ static __forceinline__ int64_t ladj_col(int64_t col0, int k, int lane) {
+    return col0 + (int64_t)k * 64 + (TC >= 64 ? lane : lane % TC);
+  }
+};
+
+template <int D, int R, int U>
+using HJTile = float[U][R];
+
+// DBG (diagnostic builds, ENF_DEBUG_MODE): 1 = synthesize the tile instead of loading it, 2 = also
+// skip the stores (compute-only timing).
+template <int D, int R, int U, bool TAIL, int DBG>
+__device__ __forceinline__ void hj_load(const FlowArgs& a, int64_t col0, float (&x)[U][R]) {
+  using L = HJLay<D, R, U>;
+  const int lane = threadIdx.x & 63;
+  const float* __restrict__ X = (const float*)a.X;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t c = L::col(col0, u, lane);
+#pragma unroll
+    for (int h = 0; h < L::NF; ++h) {
+      const int64_t off = c * D + L::row(h, lane);
+      if (DBG >= 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[u][4 * h + e] = (float)(lane + 3 * u + 5 * h + e) * 0.03125f - 1.f;
+      } else if (!TAIL) {
+        const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X + off));
+        __builtin_memcpy(&x[u][4 * h], &v4, 16);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[u][4 * h + e] = c < a.N ? X[off + e] : 0.f;
+      }
+    }
+  }
+}
+
+template <int D, int R, int U, int LM>
+__device__ __forceinline__ void hj_load_old(const FlowArgs& a, int64_t col0, float (&old)[HJLay<D, R, U>::NLS],
+                                            bool tail) {
+  using L = HJLay<D, R, U>;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < L::NLS; ++k) {
+    const int64_t c = L::ladj_col(col0, k, lane);
+    old[k] = (LM == 2 && (!tail || c < a.N)) ? ((const float*)a.ladj)[c] : 0.f;
+  }
+}
+
+// Y fragments, then the ladj: column totals (group sums over the G lanes of a column) staged
+// through the wave's LDS slots and written by NLS full-wave coalesced stores.
+template <int D, int R, int U, int LM, bool TAIL, int DBG>
+__device__ __forceinline__ void hj_store(const FlowArgs& a, float ctot, int64_t col0, float (&x)[U][R],
+                                         const float (&acc)[U], const float (&old)[HJLay<D, R, U>::NLS],
+                                         float* __restrict__ stage) {
+  using L = HJLay<D, R, U>;
+  const int lane = threadIdx.x & 63;
+  float* __restrict__ Y = (float*)a.Y;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t c = L::col(col0, u, lane);
+#pragma unroll
+    for (int h = 0; h < L::NF; ++h) {
+      const int64_t off = c * D + L::row(h, lane);
+      if (DBG == 2) {
+        if (x[u][4 * h] == 1234.5f) Y[off] = x[u][4 * h + 1];  // keeps the compute alive
+      } else if (!TAIL) {
+        u32x4 v4;
+        __builtin_memcpy(&v4, &x[u][4 * h], 16);
+        __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(Y + off));
+      } else if (c < a.N) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Y[off + e] = x[u][4 * h + e];
+      }
+    }
+  }
+  if constexpr (LM > 0) {
+    float* __restrict__ ladj = (float*)a.ladj;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float tot = group_sum<L::G>(acc[u]);
+      if ((lane % L::G) == 0) stage[u * L::CPS + lane / L::G] = tot;
+    }
+#pragma unroll
+    for (int k = 0; k < L::NLS; ++k) {
+      const int c = k * 64 + (L::TC >= 64 ? lane : lane % L::TC);
+      const float v = fmaf((float)kLn2, stage[c], ctot) + old[k];
+      const int64_t col = col0 + c;
+      if (!TAIL || col < a.N) ladj[col] = v;
+    }
+  }
+}
+
+// Records, pair p < n: [group g][param q in (a, P, Q, R)][R values, value 4h+e = row h*D/NF+4g+e];
+// record n (final): same layout with (gamma_{n-1}, delta'_{n-1}, 0, 0). A lane reads each
+// parameter of its rows with NF 16-byte LDS reads.
+template <int D, int R>
 __device__ void build_hj_program(const FlowArgs& a, int n, float* __restrict__ rec, double* __restrict__ scr,
                                  float* ctot) {
-  constexpr int V = 4;
+  constexpr int NF = R / 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   // pass 1 (one wave per pair): v'v, sum_d v_d gamma_{p-1,d}, and the constant ladj part
   // sum_d log|delta/lambda| (johnson_trafo.jl:41) in double
@@ -83,7 +194,8 @@ __device__ void build_hj_program(const FlowArgs& a, int n, float* __restrict__ r
   // pass 2: folded records
   for (int i = threadIdx.x; i < (n + 1) * D; i += blockDim.x) {
     const int p = i / D, d = i % D;
-    float* r = rec + (size_t)p * 4 * D + (d / V) * 4 * V + (d % V);
+    const int h = d / (D / NF), w = d % (D / NF), g = w / 4, e = w % 4;
+    float* r = rec + (size_t)p * 4 * D + g * 4 * R + 4 * h + e;
     double q0, q1, q2, q3;
     if (p < n) {
       const Step& sh = a.steps[2 * p];
@@ -111,9 +223,9 @@ __device__ void build_hj_program(const FlowArgs& a, int n, float* __restrict__ r
       q2 = q3 = 0.0;
     }
     r[0] = (float)q0;
-    r[V] = (float)q1;
-    r[2 * V] = (float)q2;
-    r[3 * V] = (float)q3;
+    r[R] = (float)q1;
+    r[2 * R] = (float)q2;
+    r[3 * R] = (float)q3;
   }
   if (threadIdx.x == 0) {
     double c = 0.0;
@@ -123,60 +235,123 @@ __device__ void build_hj_program(const FlowArgs& a, int n, float* __restrict__ r
   __syncthreads();
 }
 
+template <int R>
+struct HJParams {
+  float a[R], P[R], Q[R], Rv[R];
+  __device__ __forceinline__ void load(const float* r) {
+#pragma unroll
+    for (int h = 0; h < R / 4; ++h) {
+      lds_vec<float, 4>(r + 4 * h, *reinterpret_cast<float(*)[4]>(&a[4 * h]));
+      lds_vec<float, 4>(r + R + 4 * h, *reinterpret_cast<float(*)[4]>(&P[4 * h]));
+      lds_vec<float, 4>(r + 2 * R + 4 * h, *reinterpret_cast<float(*)[4]>(&Q[4 * h]));
+      lds_vec<float, 4>(r + 3 * R + 4 * h, *reinterpret_cast<float(*)[4]>(&Rv[4 * h]));
+    }
+  }
+};
+
+// Householder dot of every column of the tile: in-lane FMA chains over the lane's R rows, then
+// log2(G) DPP stages across the G lanes of the column.
+template <int D, int R, int U>
+__device__ __forceinline__ void hj_dots(const float (&x)[U][R], const float (&w)[R], float (&dot)[U]) {
+  constexpr int G = HJLay<D, R, U>::G;
+#pragma unroll
+  for (int u = 0; u < U; ++u) dot[u] = w[0] * x[u][0];
+#pragma unroll
+  for (int e = 1; e < R; ++e)
+#pragma unroll
+    for (int u = 0; u < U; ++u) dot[u] = fmaf(w[e], x[u][e], dot[u]);
+  if constexpr (G >= 2) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) dot[u] += dpp<0xB1>(dot[u]);
+  }
+  if constexpr (G >= 4) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) dot[u] += dpp<0x4E>(dot[u]);
+  }
+  if constexpr (G >= 8) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) dot[u] += dpp<0x141>(dot[u]);
+  }
+  if constexpr (G >= 16) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) dot[u] += dpp<0x140>(dot[u]);
+  }
+  if constexpr (G >= 32) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) dot[u] += __shfl_xor(dot[u], 16);
+  }
+  if constexpr (G >= 64) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) dot[u] += __shfl_xor(dot[u], 32);
+  }
+}
+
+// Product of the R values of a row of q, as a balanced tree.
+template <int R>
+__device__ __forceinline__ float prod_tree(const float (&q)[R]) {
+  float t[R / 2];
+#pragma unroll
+  for (int i = 0; i < R / 2; ++i) t[i] = q[2 * i] * q[2 * i + 1];
+  if constexpr (R == 4) {
+    return t[0] * t[1];
+  } else if constexpr (R == 8) {
+    return (t[0] * t[1]) * (t[2] * t[3]);
+  } else {
+    float s = 1.f;
+#pragma unroll
+    for (int i = 0; i < R / 2; ++i) s *= t[i];
+    return s;
+  }
+}
+
 // One pair (reflection + Johnson) on the register tile, fast form. x holds L (pair 0: the input x)
 // on entry and the new L on exit; r points at the lane's record group of this pair and is advanced
-// to the next record (the parameter registers are reloaded for it). Returns the largest product of
-// a fragment's four q = 1 + z^2 of this lane (+Inf / NaN: the fast form is not valid for the tile).
-template <int D, int U, bool LADJ>
-__device__ __forceinline__ float hj_pair_fast(Tile<float, D, U>& x, float (&acc)[U][1], const float*& r,
-                                              float (&pa)[4], float (&pP)[4], float (&pQ)[4], float (&pR)[4]) {
-  using T = float;
-  constexpr int V = 4;
-  T dot[U][1];
-  tile_dots<T, D, U>(x, pa, dot);
+// to the next record (prm is reloaded for it). Returns the largest product of q = 1 + z^2 over a
+// lane's R rows of one column (+Inf / NaN: the fast form is not valid for the tile).
+template <int D, int R, int U, bool LADJ>
+__device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U], const float*& r, HJParams<R>& prm) {
+  float dot[U];
+  hj_dots<D, R, U>(x, prm.a, dot);
   // z = L P + Q - dotL R (in place; the first FMA does not wait for the dot reduction)
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < V; ++e) x[u][e] = fmaf(x[u][e], pP[e], pQ[e]);
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.P[e], prm.Q[e]);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < V; ++e) x[u][e] = fmaf(-dot[u][0], pR[e], x[u][e]);
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(-dot[u], prm.Rv[e], x[u][e]);
   // next pair's records (record n holds gamma_n, delta'_n for the output)
   r += 4 * D;
-  lds_vec<T, V>(r, pa);
-  lds_vec<T, V>(r + V, pP);
-  lds_vec<T, V>(r + 2 * V, pQ);
-  lds_vec<T, V>(r + 3 * V, pR);
-  // stage by stage over the whole tile (U*V independent chains per stage)
-  T q[U][V], t[U][V], pr[U];
+  prm.load(r);
+  // stage by stage over the whole tile (U*R independent chains per stage)
+  float q[U][R], t[U][R], pr[U];
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < V; ++e) q[u][e] = fmaf(x[u][e], x[u][e], 1.0f);
+    for (int e = 0; e < R; ++e) q[u][e] = fmaf(x[u][e], x[u][e], 1.0f);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < V; ++e) t[u][e] = hw_sqrt(q[u][e]);
+    for (int e = 0; e < R; ++e) t[u][e] = hw_sqrt(q[u][e]);
 #pragma unroll
-  for (int u = 0; u < U; ++u) pr[u] = (q[u][0] * q[u][1]) * (q[u][2] * q[u][3]);
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int e = 0; e < V; ++e) t[u][e] = fabsf(x[u][e]) + t[u][e];
+  for (int u = 0; u < U; ++u) pr[u] = prod_tree<R>(q[u]);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < V; ++e) t[u][e] = hw_log2(t[u][e]);
+    for (int e = 0; e < R; ++e) t[u][e] = fabsf(x[u][e]) + t[u][e];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < R; ++e) t[u][e] = hw_log2(t[u][e]);
   if (LADJ)
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc[u][0] = fmaf(-0.5f, hw_log2(pr[u]), acc[u][0]);
+    for (int u = 0; u < U; ++u) acc[u] = fmaf(-0.5f, hw_log2(pr[u]), acc[u]);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < V; ++e) x[u][e] = copysignf(t[u][e], x[u][e]);
-  T m = pr[0];
+    for (int e = 0; e < R; ++e) x[u][e] = copysignf(t[u][e], x[u][e]);
+  float m = pr[0];
 #pragma unroll
   for (int u = 1; u < U; ++u) m = fmaxf(m, pr[u]);
   return m;
@@ -184,31 +359,24 @@ __device__ __forceinline__ float hj_pair_fast(Tile<float, D, U>& x, float (&acc)
 
 // The same pair in the exact-range elementwise form (johnson_fwd_f32_slow): asinh finite up to
 // FLT_MAX, ladj -Inf where the reference's fp32 1 + z^2 overflows.
-template <int D, int U, bool LADJ>
-__device__ __forceinline__ void hj_pair_exact(Tile<float, D, U>& x, float (&acc)[U][1], const float*& r,
-                                              float (&pa)[4], float (&pP)[4], float (&pQ)[4], float (&pR)[4]) {
-  using T = float;
-  constexpr int V = 4;
-  T dot[U][1];
-  tile_dots<T, D, U>(x, pa, dot);
+template <int D, int R, int U, bool LADJ>
+__device__ __forceinline__ void hj_pair_exact(float (&x)[U][R], float (&acc)[U], const float*& r, HJParams<R>& prm) {
+  float dot[U];
+  hj_dots<D, R, U>(x, prm.a, dot);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < V; ++e) {
-      const YL yl = johnson_fwd_f32_slow(fmaf(-dot[u][0], pR[e], fmaf(x[u][e], pP[e], pQ[e])), 0.f, 1.f);
+    for (int e = 0; e < R; ++e) {
+      const YL yl = johnson_fwd_f32_slow(fmaf(-dot[u], prm.Rv[e], fmaf(x[u][e], prm.P[e], prm.Q[e])), 0.f, 1.f);
       x[u][e] = yl.y;
-      if (LADJ) acc[u][0] += yl.l;
+      if (LADJ) acc[u] += yl.l;
     }
   r += 4 * D;
-  lds_vec<T, V>(r, pa);
-  lds_vec<T, V>(r + V, pP);
-  lds_vec<T, V>(r + 2 * V, pQ);
-  lds_vec<T, V>(r + 3 * V, pR);
+  prm.load(r);
 }
 
-template <int D, int U, int LM>
+template <int D, int R, int U, int LM>
 struct HJBody {
-  using T = float;
   const FlowArgs& a;
   const float* rec;  // this lane's record group
   float ctot;
@@ -216,57 +384,86 @@ struct HJBody {
   int n;
 
   template <bool TAIL, int DBG>
-  __device__ __forceinline__ void tile(int64_t col0, Tile<T, D, U>& x,
-                                       const T (&old)[LadjOut<T, D, U>::NLS][LadjOut<T, D, U>::W]) {
-    ENF_FRAG_CONSTS
-    static_assert(CPF == 1 && SEG == V, "D >= 4 layout");
+  __device__ __forceinline__ void tile(int64_t col0, float (&x)[U][R], const float (&old)[HJLay<D, R, U>::NLS]) {
     constexpr bool LADJ = LM > 0;
-    T acc[U][1];
+    float acc[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc[u][0] = 0.f;
-    // No "+v" asm fence on x here (the interpreter uses one to pin the vmcnt wait): with the
-    // runtime pair loop below it made the register allocator reuse live tile registers (hipcc 7.2,
-    // wrong results). The compiler's own counted waits keep the next tile's loads in flight.
+    for (int u = 0; u < U; ++u) acc[u] = 0.f;
+    // No "+v" asm fence on x here (the interpreter uses one to pin the vmcnt wait): with a runtime
+    // pair loop it made hipcc 7.2's register allocator reuse live tile registers (wrong results).
+    // The compiler's own counted waits keep the next tile's loads in flight.
     const float* r = rec;
-    T pa[V], pP[V], pQ[V], pR[V];
-    lds_vec<T, V>(r, pa);
-    lds_vec<T, V>(r + V, pP);
-    lds_vec<T, V>(r + 2 * V, pQ);
-    lds_vec<T, V>(r + 3 * V, pR);
-    // branch-free pair loop; the rare tile with |z| >= 2^16 (or Inf / NaN) is redone below
-    T m = 0.f;
-    for (int p = 0; p < n; ++p) m = fmaxf(m, hj_pair_fast<D, U, LADJ>(x, acc, r, pa, pP, pQ, pR));
+    HJParams<R> prm;
+    prm.load(r);
+    // branch-free pair loop; a tile with a product overflow (|z| large, Inf, NaN) is redone below
+    float m = 0.f;
+    for (int p = 0; p < n; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ>(x, acc, r, prm));
     if (__builtin_expect(!(m <= FLT_MAX), 0)) {
-      load_tile<T, D, U, TAIL, DBG>(a, col0, x);
+      hj_load<D, R, U, TAIL, DBG>(a, col0, x);
 #pragma unroll
-      for (int u = 0; u < U; ++u) acc[u][0] = 0.f;
+      for (int u = 0; u < U; ++u) acc[u] = 0.f;
       r = rec;
-      lds_vec<T, V>(r, pa);
-      lds_vec<T, V>(r + V, pP);
-      lds_vec<T, V>(r + 2 * V, pQ);
-      lds_vec<T, V>(r + 3 * V, pR);
-      for (int p = 0; p < n; ++p) hj_pair_exact<D, U, LADJ>(x, acc, r, pa, pP, pQ, pR);
+      prm.load(r);
+      for (int p = 0; p < n; ++p) hj_pair_exact<D, R, U, LADJ>(x, acc, r, prm);
     }
     // y = gamma_n + delta'_n L
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int e = 0; e < V; ++e) x[u][e] = fmaf(x[u][e], pP[e], pa[e]);
-    store_tile<T, D, U, LM, TAIL, DBG>(a, ctot, col0, x, acc, old, stage);
+      for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.P[e], prm.a[e]);
+    hj_store<D, R, U, LM, TAIL, DBG>(a, ctot, col0, x, acc, old, stage);
   }
 };
 
-template <int D, int U, int LM, int OCC, int DBG>
+// Persistent, software-pipelined tile loop (as frag_stream in enf_frag.h, for the HJLay layout).
+template <int D, int R, int U, int LM, int DBG, typename Body>
+__device__ __forceinline__ void hj_stream(const FlowArgs& a, Body& body) {
+  using L = HJLay<D, R, U>;
+  constexpr int64_t CT = L::TC;
+  const int64_t ntiles_full = a.N / CT;
+  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) +
+                          __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  float xa[U][R], xb[U][R], old[L::NLS];
+  const int64_t t = wave_id;
+  if (t < ntiles_full) {
+    hj_load<D, R, U, false, DBG>(a, t * CT, xa);
+    int64_t t1 = t + nwaves;
+    hj_load_old<D, R, U, LM>(a, t * CT, old, false);
+    hj_load<D, R, U, false, DBG>(a, (t1 < ntiles_full ? t1 : t) * CT, xb);
+    body.template tile<false, DBG>(t * CT, xa, old);
+    while (t1 < ntiles_full) {
+      const int64_t t2 = t1 + nwaves;
+      hj_load_old<D, R, U, LM>(a, t1 * CT, old, false);
+      hj_load<D, R, U, false, DBG>(a, (t2 < ntiles_full ? t2 : t1) * CT, xa);
+      body.template tile<false, DBG>(t1 * CT, xb, old);
+      if (t2 >= ntiles_full) break;
+      const int64_t t3 = t2 + nwaves;
+      hj_load_old<D, R, U, LM>(a, t2 * CT, old, false);
+      hj_load<D, R, U, false, DBG>(a, (t3 < ntiles_full ? t3 : t2) * CT, xb);
+      body.template tile<false, DBG>(t2 * CT, xa, old);
+      t1 = t3;
+    }
+  }
+  if (ntiles_full * CT < a.N && wave_id == ntiles_full % nwaves) {
+    const int64_t c0 = ntiles_full * CT;
+    hj_load<D, R, U, true, 0>(a, c0, xa);
+    hj_load_old<D, R, U, LM>(a, c0, old, true);
+    body.template tile<true, 0>(c0, xa, old);
+  }
+}
+
+template <int D, int R, int U, int LM, int OCC, int DBG>
 __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(FlowArgs a, int n) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* scr = reinterpret_cast<double*>(smem);
   float* ctotp = reinterpret_cast<float*>(scr + 3 * kHjMaxPairs);
   float* stage = reinterpret_cast<float*>(smem + kHjScratch) + (threadIdx.x >> 6) * kStagePerWave;
   float* rec = reinterpret_cast<float*>(smem + kHjHeader);
-  build_hj_program<D>(a, n, rec, scr, ctotp);
-  constexpr int G = Frag<float, D>::G;
-  HJBody<D, U, LM> body{a, rec + ((threadIdx.x & 63) % G) * 16, *ctotp, stage, n};
-  frag_stream<float, D, U, LM, DBG>(a, body);
+  build_hj_program<D, R>(a, n, rec, scr, ctotp);
+  constexpr int G = HJLay<D, R, U>::G;
+  HJBody<D, R, U, LM> body{a, rec + ((threadIdx.x & 63) % G) * 4 * R, *ctotp, stage, n};
+  hj_stream<D, R, U, LM, DBG>(a, body);
 }
 
 int hj_program_pairs(const FlowArgs& a) {
@@ -278,34 +475,34 @@ int hj_program_pairs(const FlowArgs& a) {
   return a.nsteps / 2;
 }
 
-template <int D, int U, int LM, int OCC = 1, int DBG = 0>
+template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0>
 static hipError_t launch_hj(const FlowArgs& a, int n, hipStream_t st, const DeviceInfo& dev) {
   const size_t lds = hj_lds_bytes(D, n);
-  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, U, LM, OCC, DBG>);
+  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG>);
   int64_t blocks = 0;
-  hipError_t e = frag_grid(k, a.N, (int64_t)Frag<float, D>::COLS_PER_INSTR * U * 4, lds, dev, &blocks);
+  hipError_t e = frag_grid(k, a.N, (int64_t)HJLay<D, R, U>::TC * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_hj_kernel<D, U, LM, OCC, DBG>), dim3((unsigned)blocks), dim3(256), lds, st, a, n);
+  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG>), dim3((unsigned)blocks), dim3(256), lds, st, a, n);
   return hipGetLastError();
 }
 
-// Tuning variants (development only, fp32 D = 32 with ladj): ENF_HJ_U in {2, 4, 8}, ENF_HJ_OCC in {1, 5, 6}.
+// Default R = 8 rows per lane, U = 2 slabs (16 values per lane). Tuning variants (development only,
+// fp32 D = 32 with ladj): ENF_HJ_R in {4, 8, 16} (U = 16 / R), ENF_HJ_U2 = 1 doubles U.
 template <int LM>
 static hipError_t dispatch_hj(const FlowArgs& a, int n, int dbg, hipStream_t st, const DeviceInfo& dev) {
   if (a.D == 32) {
     if constexpr (LM == 1) {
-      static const int u = env_int("ENF_HJ_U", 4);
-      static const int occ = env_int("ENF_HJ_OCC", 1);
-      if (dbg == 1) return launch_hj<32, 4, 1, 1, 1>(a, n, st, dev);
-      if (dbg == 2) return launch_hj<32, 4, 1, 1, 2>(a, n, st, dev);
-      if (u == 2) return launch_hj<32, 2, 1>(a, n, st, dev);
-      if (u == 8) return launch_hj<32, 8, 1>(a, n, st, dev);
-      if (occ == 5) return launch_hj<32, 4, 1, 5>(a, n, st, dev);
-      if (occ == 6) return launch_hj<32, 4, 1, 6>(a, n, st, dev);
+      static const int r = env_int("ENF_HJ_R", 8);
+      static const int u2 = env_int("ENF_HJ_U2", 0);
+      if (dbg == 1) return launch_hj<32, 8, 2, 1, 1, 1>(a, n, st, dev);
+      if (dbg == 2) return launch_hj<32, 8, 2, 1, 1, 2>(a, n, st, dev);
+      if (r == 4) return u2 ? launch_hj<32, 4, 8, 1>(a, n, st, dev) : launch_hj<32, 4, 4, 1>(a, n, st, dev);
+      if (r == 16) return launch_hj<32, 16, 1, 1>(a, n, st, dev);
+      if (u2) return launch_hj<32, 8, 4, 1>(a, n, st, dev);
     }
-    return launch_hj<32, 4, LM>(a, n, st, dev);
+    return launch_hj<32, 8, 2, LM>(a, n, st, dev);
   }
-  return launch_hj<64, 4, LM>(a, n, st, dev);
+  return launch_hj<64, 8, 2, LM>(a, n, st, dev);
 }
 
 hipError_t launch_hj_program(const FlowArgs& a, int lm, int dbg, hipStream_t st, const DeviceInfo& dev) {
