@@ -31,13 +31,31 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 
 #include "enf_frag.h"
 #include "enf_internal.h"
 
 namespace enf {
 
-constexpr int kHjMaxPairs = kMaxSteps / 2;
+constexpr int kHjMaxPairs = 8;
+
+// Kernel arguments of the compiled program: the pair parameter vectors only (376 bytes; the
+// generic FlowArgs table is ~2 KB, and kernel arguments that large are staged with an extra
+// copy kernel per launch).
+struct HJArgs {
+  const void* X;
+  void* Y;
+  void* ladj;
+  int64_t N;
+  int32_t n;        // pairs
+  int32_t pad_;
+  const float* v[kHjMaxPairs];  // reflection vector (column of V) of pair p
+  const float* g[kHjMaxPairs];  // Johnson gamma, delta, xi, lambda of pair p
+  const float* d[kHjMaxPairs];
+  const float* xi[kHjMaxPairs];
+  const float* lam[kHjMaxPairs];
+};
 // LDS: [per pair {hs, c, cl} + ctot: doubles][ladj staging: 4 waves x kStagePerWave floats][records]
 constexpr size_t kHjScratch = ((3 * kHjMaxPairs + 1) * sizeof(double) + 15) / 16 * 16;
 constexpr size_t kHjHeader = kHjScratch + 4 * kStagePerWave * sizeof(float);
@@ -75,7 +93,7 @@ using HJTile = float[U][R];
 // DBG (diagnostic builds, ENF_DEBUG_MODE): 1 = synthesize the tile instead of loading it, 2 = also
 // skip the stores (compute-only timing).
 template <int D, int R, int U, bool TAIL, int DBG>
-__device__ __forceinline__ void hj_load(const FlowArgs& a, int64_t col0, float (&x)[U][R]) {
+__device__ __forceinline__ void hj_load(const HJArgs& a, int64_t col0, float (&x)[U][R]) {
   using L = HJLay<D, R, U>;
   const int lane = threadIdx.x & 63;
   const float* __restrict__ X = (const float*)a.X;
@@ -100,7 +118,7 @@ __device__ __forceinline__ void hj_load(const FlowArgs& a, int64_t col0, float (
 }
 
 template <int D, int R, int U, int LM>
-__device__ __forceinline__ void hj_load_old(const FlowArgs& a, int64_t col0, float (&old)[HJLay<D, R, U>::NLS],
+__device__ __forceinline__ void hj_load_old(const HJArgs& a, int64_t col0, float (&old)[HJLay<D, R, U>::NLS],
                                             bool tail) {
   using L = HJLay<D, R, U>;
   const int lane = threadIdx.x & 63;
@@ -114,7 +132,7 @@ __device__ __forceinline__ void hj_load_old(const FlowArgs& a, int64_t col0, flo
 // Y fragments, then the ladj: column totals (group sums over the G lanes of a column) staged
 // through the wave's LDS slots and written by NLS full-wave coalesced stores.
 template <int D, int R, int U, int LM, bool TAIL, int DBG>
-__device__ __forceinline__ void hj_store(const FlowArgs& a, float ctot, int64_t col0, float (&x)[U][R],
+__device__ __forceinline__ void hj_store(const HJArgs& a, float ctot, int64_t col0, float (&x)[U][R],
                                          const float (&acc)[U], const float (&old)[HJLay<D, R, U>::NLS],
                                          float* __restrict__ stage) {
   using L = HJLay<D, R, U>;
@@ -159,24 +177,21 @@ __device__ __forceinline__ void hj_store(const FlowArgs& a, float ctot, int64_t 
 // record n (final): same layout with (gamma_{n-1}, delta'_{n-1}, 0, 0). A lane reads each
 // parameter of its rows with NF 16-byte LDS reads.
 template <int D, int R>
-__device__ void build_hj_program(const FlowArgs& a, int n, float* __restrict__ rec, double* __restrict__ scr,
+__device__ void build_hj_program(const HJArgs& a, int n, float* __restrict__ rec, double* __restrict__ scr,
                                  float* ctot) {
   constexpr int NF = R / 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   // pass 1 (one wave per pair): v'v, sum_d v_d gamma_{p-1,d}, and the constant ladj part
   // sum_d log|delta/lambda| (johnson_trafo.jl:41) in double
   for (int p = wave; p < n; p += nw) {
-    const Step& sh = a.steps[2 * p];
-    const LayerDesc& H = a.layers[sh.layer];
-    const LayerDesc& J = a.layers[a.steps[2 * p + 1].layer];
-    const float* v = (const float*)H.p[0] + (int64_t)sh.col * D;
-    const float* gprev = p > 0 ? (const float*)a.layers[a.steps[2 * p - 1].layer].p[0] : nullptr;
+    const float* v = a.v[p];
+    const float* gprev = p > 0 ? a.g[p - 1] : nullptr;
     double vv = 0.0, cg = 0.0, cl = 0.0;
     for (int d = lane; d < D; d += 64) {
       const double vd = v[d];
       vv += vd * vd;
       if (gprev) cg += vd * (double)gprev[d];
-      cl += log(fabs((double)((const float*)J.p[1])[d])) - log(fabs((double)((const float*)J.p[3])[d]));
+      cl += log(fabs((double)a.d[p][d])) - log(fabs((double)a.lam[p][d]));
     }
     for (int m = 32; m >= 1; m >>= 1) {
       vv += __shfl_xor(vv, m);
@@ -198,28 +213,24 @@ __device__ void build_hj_program(const FlowArgs& a, int n, float* __restrict__ r
     float* r = rec + (size_t)p * 4 * D + g * 4 * R + 4 * h + e;
     double q0, q1, q2, q3;
     if (p < n) {
-      const Step& sh = a.steps[2 * p];
-      const LayerDesc& J = a.layers[a.steps[2 * p + 1].layer];
-      const double vh = (double)((const float*)a.layers[sh.layer].p[0])[(int64_t)sh.col * D + d] * scr[3 * p];
-      const double xi = ((const float*)J.p[2])[d];
-      const double il = 1.0 / (double)((const float*)J.p[3])[d];
+      const double vh = (double)a.v[p][d] * scr[3 * p];
+      const double xi = a.xi[p][d];
+      const double il = 1.0 / (double)a.lam[p][d];
       if (p == 0) {
         q0 = vh;
         q1 = il;
         q2 = -xi * il;
       } else {
-        const LayerDesc& Jp = a.layers[a.steps[2 * p - 1].layer];
-        const double gp = ((const float*)Jp.p[0])[d];
-        const double dp = (double)((const float*)Jp.p[1])[d] * kLn2;
+        const double gp = a.g[p - 1][d];
+        const double dp = (double)a.d[p - 1][d] * kLn2;
         q0 = vh * dp;
         q1 = dp * il;
         q2 = (gp - xi - scr[3 * p + 1] * vh) * il;
       }
       q3 = vh * il;
     } else {
-      const LayerDesc& Jl = a.layers[a.steps[2 * n - 1].layer];
-      q0 = ((const float*)Jl.p[0])[d];
-      q1 = (double)((const float*)Jl.p[1])[d] * kLn2;
+      q0 = a.g[n - 1][d];
+      q1 = (double)a.d[n - 1][d] * kLn2;
       q2 = q3 = 0.0;
     }
     r[0] = (float)q0;
@@ -377,7 +388,7 @@ __device__ __forceinline__ void hj_pair_exact(float (&x)[U][R], float (&acc)[U],
 
 template <int D, int R, int U, int LM>
 struct HJBody {
-  const FlowArgs& a;
+  const HJArgs& a;
   const float* rec;  // this lane's record group
   float ctot;
   float* stage;
@@ -417,7 +428,7 @@ struct HJBody {
 
 // Persistent, software-pipelined tile loop (as frag_stream in enf_frag.h, for the HJLay layout).
 template <int D, int R, int U, int LM, int DBG, typename Body>
-__device__ __forceinline__ void hj_stream(const FlowArgs& a, Body& body) {
+__device__ __forceinline__ void hj_stream(const HJArgs& a, Body& body) {
   using L = HJLay<D, R, U>;
   constexpr int64_t CT = L::TC;
   const int64_t ntiles_full = a.N / CT;
@@ -454,7 +465,8 @@ __device__ __forceinline__ void hj_stream(const FlowArgs& a, Body& body) {
 }
 
 template <int D, int R, int U, int LM, int OCC, int DBG>
-__global__ __launch_bounds__(256, OCC) void flow_hj_kernel(FlowArgs a, int n) {
+__global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
+  const int n = a.n;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* scr = reinterpret_cast<double*>(smem);
   float* ctotp = reinterpret_cast<float*>(scr + 3 * kHjMaxPairs);
@@ -476,41 +488,57 @@ int hj_program_pairs(const FlowArgs& a) {
 }
 
 template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0>
-static hipError_t launch_hj(const FlowArgs& a, int n, hipStream_t st, const DeviceInfo& dev) {
-  const size_t lds = hj_lds_bytes(D, n);
+static hipError_t launch_hj(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
+  const size_t lds = hj_lds_bytes(D, h.n);
   const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG>);
   int64_t blocks = 0;
-  hipError_t e = frag_grid(k, a.N, (int64_t)HJLay<D, R, U>::TC * 4, lds, dev, &blocks);
+  hipError_t e = frag_grid(k, h.N, (int64_t)HJLay<D, R, U>::TC * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG>), dim3((unsigned)blocks), dim3(256), lds, st, a, n);
+  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG>), dim3((unsigned)blocks), dim3(256), lds, st, h);
   return hipGetLastError();
 }
 
 // Default R = 8 rows per lane, U = 2 slabs (16 values per lane). Tuning variants (development only,
 // fp32 D = 32 with ladj): ENF_HJ_R in {4, 8, 16} (U = 16 / R), ENF_HJ_U2 = 1 doubles U.
 template <int LM>
-static hipError_t dispatch_hj(const FlowArgs& a, int n, int dbg, hipStream_t st, const DeviceInfo& dev) {
-  if (a.D == 32) {
+static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, const DeviceInfo& dev) {
+  if (D == 32) {
     if constexpr (LM == 1) {
       static const int r = env_int("ENF_HJ_R", 8);
       static const int u2 = env_int("ENF_HJ_U2", 0);
-      if (dbg == 1) return launch_hj<32, 8, 2, 1, 1, 1>(a, n, st, dev);
-      if (dbg == 2) return launch_hj<32, 8, 2, 1, 1, 2>(a, n, st, dev);
-      if (r == 4) return u2 ? launch_hj<32, 4, 8, 1>(a, n, st, dev) : launch_hj<32, 4, 4, 1>(a, n, st, dev);
-      if (r == 16) return launch_hj<32, 16, 1, 1>(a, n, st, dev);
-      if (u2) return launch_hj<32, 8, 4, 1>(a, n, st, dev);
+      if (dbg == 1) return launch_hj<32, 8, 2, 1, 1, 1>(a, st, dev);
+      if (dbg == 2) return launch_hj<32, 8, 2, 1, 1, 2>(a, st, dev);
+      if (r == 4) return u2 ? launch_hj<32, 4, 8, 1>(a, st, dev) : launch_hj<32, 4, 4, 1>(a, st, dev);
+      if (r == 16) return launch_hj<32, 16, 1, 1>(a, st, dev);
+      if (u2) return launch_hj<32, 8, 4, 1>(a, st, dev);
     }
-    return launch_hj<32, 8, 2, LM>(a, n, st, dev);
+    return launch_hj<32, 8, 2, LM>(a, st, dev);
   }
-  return launch_hj<64, 8, 2, LM>(a, n, st, dev);
+  return launch_hj<64, 8, 2, LM>(a, st, dev);
 }
 
 hipError_t launch_hj_program(const FlowArgs& a, int lm, int dbg, hipStream_t st, const DeviceInfo& dev) {
   const int n = hj_program_pairs(a);
   if (n < 1 || n > kHjMaxPairs) return hipErrorNotSupported;
-  if (lm == 0) return dispatch_hj<0>(a, n, dbg, st, dev);
-  if (lm == 1) return dispatch_hj<1>(a, n, dbg, st, dev);
-  return dispatch_hj<2>(a, n, dbg, st, dev);
+  HJArgs h;
+  memset(&h, 0, sizeof h);
+  h.X = a.X;
+  h.Y = a.Y;
+  h.ladj = a.ladj;
+  h.N = a.N;
+  h.n = n;
+  for (int p = 0; p < n; ++p) {
+    const Step& sh = a.steps[2 * p];
+    const LayerDesc& J = a.layers[a.steps[2 * p + 1].layer];
+    h.v[p] = (const float*)a.layers[sh.layer].p[0] + (int64_t)sh.col * a.D;
+    h.g[p] = (const float*)J.p[0];
+    h.d[p] = (const float*)J.p[1];
+    h.xi[p] = (const float*)J.p[2];
+    h.lam[p] = (const float*)J.p[3];
+  }
+  if (lm == 0) return dispatch_hj<0>(h, a.D, dbg, st, dev);
+  if (lm == 1) return dispatch_hj<1>(h, a.D, dbg, st, dev);
+  return dispatch_hj<2>(h, a.D, dbg, st, dev);
 }
 
 }  // namespace enf
