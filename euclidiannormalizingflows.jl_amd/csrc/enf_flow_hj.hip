@@ -409,6 +409,8 @@ struct HJBody {
     // branch-free pair loop; a tile with a product overflow (|z| large, Inf, NaN) is redone below
     float m = 0.f;
     for (int p = 0; p < n; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ>(x, acc, r, prm));
+    // column-uniform: the exact form's dot products read every lane of a column (DPP)
+    m = group_max<HJLay<D, R, U>::G>(m);
     if (__builtin_expect(!(m <= FLT_MAX), 0)) {
       hj_load<D, R, U, TAIL, DBG>(a, col0, x);
 #pragma unroll

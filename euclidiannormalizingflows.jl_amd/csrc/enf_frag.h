@@ -58,6 +58,18 @@ __device__ __forceinline__ T group_sum(T x) {
   return x;
 }
 
+// DPP max over aligned groups of G lanes (as group_sum)
+template <int G>
+__device__ __forceinline__ float group_max(float x) {
+  if constexpr (G >= 2) x = fmaxf(x, dpp<0xB1>(x));
+  if constexpr (G >= 4) x = fmaxf(x, dpp<0x4E>(x));
+  if constexpr (G >= 8) x = fmaxf(x, dpp<0x141>(x));
+  if constexpr (G >= 16) x = fmaxf(x, dpp<0x140>(x));
+  if constexpr (G >= 32) x = fmaxf(x, __shfl_xor(x, 16));
+  if constexpr (G >= 64) x = fmaxf(x, __shfl_xor(x, 32));
+  return x;
+}
+
 // ------------------------------------------------------------------------------------------
 // per-element transforms. acc is the running per-lane ladj partial of one column, in units of
 // log2 (fp32) or natural log (fp64): ladj = C_total + UNIT * acc.

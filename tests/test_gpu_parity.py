@@ -270,3 +270,72 @@ def test_full_size_round_trip_config3(enf, gpu):
     Xs = np.asfortranarray(X[:, idx].cpu().numpy())
     check_vs_oracle(orc, layers, Xs, Y[:, idx].cpu().numpy(), L[0, idx].cpu().numpy(), np.float32,
                     what="config3 sample")
+
+
+def _hj_layers(rng, D, pairs):
+    layers = []
+    for _ in range(pairs):
+        layers += [(5, rand_params(rng, 5, D, np.float32)), (3, rand_params(rng, 3, D, np.float32))]
+    return layers
+
+
+@pytest.mark.parametrize("D", [32, 64])
+@pytest.mark.parametrize("pairs", [1, 2, 3, 4, 8, 9])
+def test_hj_program_pairs_vs_oracle(enf, gpu, oracle, D, pairs):
+    """The compiled (J∘H)^n program (enf_flow_hj.hip; n <= 8, n = 9 runs on the interpreter):
+    forward + ladj, plain call f(X) and multi-tile waves (N > resident tiles) against the oracle."""
+    rng = np.random.default_rng(100 * D + pairs)
+    layers = _hj_layers(rng, D, pairs)
+    N = 300_007
+    X = np.asfortranarray(rng.standard_normal((D, N)).astype(np.float32))
+    f = make_flow(enf, layers)
+    Y, L = enf.with_logabsdet_jacobian(f, colmajor_cuda(X))
+    check_vs_oracle(oracle, layers, X, to_np(Y), to_np(L), np.float32, what=f"hj D{D} n{pairs}")
+    assert np.array_equal(to_np(f(colmajor_cuda(X))), to_np(Y))
+
+
+def test_hj_program_accumulate_inplace(enf, gpu, oracle):
+    """accumulate_ladj = 1 and Y aliasing X through the raw C ABI on the compiled program."""
+    import torch
+
+    rng = np.random.default_rng(5)
+    D, N = 32, 50_001
+    layers = _hj_layers(rng, D, 4)
+    X = np.asfortranarray(rng.standard_normal((D, N)).astype(np.float32))
+    Yr, Lr = oracle.flow_apply(layers, X)
+    dev = [[torch.from_numpy(np.ascontiguousarray(p)).cuda() for p in ps] for _, ps in layers]
+    lt = [(op, 1 if op == 5 else 0, [t.data_ptr() for t in ts]) for (op, _), ts in zip(layers, dev)]
+    buf = colmajor_cuda(X).t().contiguous()  # N x D row-major == D x N column-major
+    L0 = torch.full((N,), 3.25, dtype=torch.float32, device="cuda")
+    assert _raw_apply(enf, 0, D, N, buf.data_ptr(), D, buf.data_ptr(), D, L0.data_ptr(), 1, lt) == 0
+    torch.cuda.synchronize()
+    assert col_err(buf.cpu().numpy().T, Yr) < 1e-5
+    assert ladj_err(L0.cpu().numpy() - 3.25, Lr) < 1e-5
+
+
+@pytest.mark.parametrize("D", [32, 64])
+def test_hj_program_exact_redo_edge_values(enf, gpu, oracle, D):
+    """Columns with huge, infinite and NaN entries inside the compiled program: the tile is redone
+    with the exact-range form; everything else in the batch is unaffected."""
+    rng = np.random.default_rng(11)
+    layers = _hj_layers(rng, D, 4)
+    N = 4096
+    X = rng.standard_normal((D, N)).astype(np.float32)
+    bad = [7, 100, 101, 2000, 4095]
+    X[3, 7] = 3e30
+    X[0, 100] = -1e25
+    X[5, 101] = np.inf
+    X[D - 1, 2000] = np.nan
+    X[:, 4095] = 1e3  # moderate but large |z|: product of q overflows, the fast form would lose it
+    X = np.asfortranarray(X)
+    Yr, Lr = oracle.flow_apply(layers, X)
+    Y, L = enf.with_logabsdet_jacobian(make_flow(enf, layers), colmajor_cuda(X))
+    Y, L = to_np(Y), to_np(L).reshape(-1)
+    assert np.array_equal(np.isnan(Y), np.isnan(Yr)) and np.array_equal(np.isnan(L), np.isnan(Lr))
+    assert np.array_equal(np.isinf(Y), np.isinf(Yr)) and np.array_equal(np.isinf(L), np.isinf(Lr))
+    fin = np.isfinite(Yr)
+    assert col_err(np.where(fin, Y, 0), np.where(fin, Yr, 0)) < 1e-5
+    finl = np.isfinite(Lr)
+    assert ladj_err(L[finl], Lr[finl]) < 1e-5
+    good = np.setdiff1d(np.arange(N), bad)
+    check_vs_oracle(oracle, layers, np.asfortranarray(X[:, good]), Y[:, good], L[good], np.float32, what="redo")
