@@ -1,0 +1,145 @@
+"""Config 5 benchmark: optimize_whitening training steps.
+
+Data: X = f_true^{-1}(Z), Z ~ N(0,1) (D = 32, N = 1e7 columns, fp32), generated on the device with
+the library's own inverse flow; trainable: a differently seeded J4∘H4∘…∘J1∘H1 flow; ADAGrad
+(eta = 0.1); nbatches = 100 -> global minibatch B = 1e5. A step is one minibatch of
+src/optimize_whitening.jl:37-41: the fused forward+backward negll gradient over this rank's share
+(enf_flow_negll_grad), the cross-rank sum (torch.distributed all-reduce = RCCL; none at world 1),
+ADAGrad on every trainable vector (enf_adagrad_step) and the Householder re-normalisation.
+
+    python bench_train.py [--steps 100 --warmup 5 --D 32 --N 10000000 --nbatches 100]
+    torchrun --nproc-per-node N bench_train.py ...       (one process per GPU)
+
+Prints one JSON line (rank 0): steps/s, samples/s (global minibatch samples per second), the
+per-step time of the gradient kernel pair (HIP events) and the negll trajectory endpoints.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from bench import build_flow, max_over_ranks  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--D", type=int, default=32)
+    ap.add_argument("--N", type=int, default=10_000_000, help="total samples (all ranks)")
+    ap.add_argument("--nbatches", type=int, default=100)
+    ap.add_argument("--pairs", type=int, default=4)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from enf_pkg import load
+
+    enf = load()
+    lib = enf._lib
+    from euclidiannormalizingflows_jl_amd.train import FlowState, _workspace, trainable_runs  # noqa: E402
+
+    D, N = args.D, args.N
+    mk = lambda layers: enf.compose(*[enf.HouseholderTrafo(ps[0]) if op == 5 else enf.JohnsonTrafo(*ps)
+                                      for op, ps in reversed(layers)])
+    # the data-generating flow's inverse (sinh layers) must stay finite over 4 layers: delta in [3, 5]
+    ltrue = build_flow(D, args.pairs, np.float32, seed=7)
+    rs = np.random.default_rng(7)
+    for op, ps in ltrue:
+        if op == 3:
+            ps[1] = rs.uniform(3, 5, D).astype(np.float32)
+    f_true = mk(ltrue)
+    f0 = mk(build_flow(D, args.pairs, np.float32, seed=42))
+    # every rank holds the whole sample set (columns are read by rank shares of each minibatch)
+    g = torch.Generator(device=dev).manual_seed(0x5EED)
+    Z = torch.randn((N, D), generator=g, device=dev, dtype=torch.float32).t()
+    X = enf.inverse(f_true)(Z)
+    del Z
+    plan = enf.minibatch_plan(N, args.nbatches, rank, world)
+    state = FlowState(f0, D, torch.float32, dev, enf.ADAGrad())
+    out = torch.zeros(1 + state.nparams, dtype=torch.float32, device=dev)
+    ws = _workspace(state, max(B for B, _, _ in plan))
+    segs = trainable_runs(state)
+    hcols = state.householder_columns()
+    L = lib.lib()
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    ldx = X.stride(1)
+    opt = enf.ADAGrad()
+    hist = []
+
+    def step(i, ev=None):
+        B, lo, hi = plan[i % len(plan)]
+        out.zero_()
+        if ev is not None:
+            ev[0].record(stream)
+        if hi > lo:
+            lib.check(L.enf_flow_negll_grad(lib.ENF_F32, D, hi - lo, X[:, lo:hi].data_ptr(), ldx, state.layers(),
+                                            len(state.trafos), out.data_ptr(), ws.data_ptr(), ws.numel() * 8, sh))
+        if ev is not None:
+            ev[1].record(stream)
+        enf.allreduce_sum_(out, world)
+        g_ = out[1:]
+        for s0, s1 in segs:
+            lib.check(L.enf_adagrad_step(lib.ENF_F32, s1 - s0, state.theta[s0:].data_ptr(), state.acc[s0:].data_ptr(),
+                                         g_[s0:].data_ptr(), 1.0 / B, opt.eta, opt.epsilon, sh))
+        for off, k in hcols:
+            lib.check(L.enf_householder_normalize(lib.ENF_F32, D, k, state.theta[off:].data_ptr(), sh))
+        return out[0:1] / B
+
+    for i in range(args.warmup):
+        hist.append(step(i))
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        hist.append(step(args.warmup + i, evs[i]))
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    grad_ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+    wall, grad_ms_max = max_over_ranks([wall, grad_ms], dev, world)
+    samples = sum(plan[(args.warmup + i) % len(plan)][0] for i in range(args.steps))
+    negll = [float(h) for h in torch.cat(hist).cpu()]
+    if rank == 0:
+        print(json.dumps({
+            "metric": "optimize_whitening training steps/s (config 5)",
+            "value": args.steps / wall, "unit": "steps/s", "samples_per_s": samples / wall,
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
+            "grad_kernel_ms_median": grad_ms, "grad_kernel_ms_max_rank": grad_ms_max, "dtype": "f32",
+            "data": "synthetic: X = f_true^-1(Z), Z ~ N(0,1) (torch Philox 0x5EED), f_true seed 7, init seed 42",
+            "config": {"workload": f"optimize_whitening D={D}, N={N}, nbatches={args.nbatches} "
+                                   f"(B={plan[0][0]}), {args.pairs}x(J∘H), ADAGrad(0.1)",
+                       "per_rank_share": plan[0][2] - plan[0][1], "parallelism": f"dp{world}"},
+            "negll_first": negll[0], "negll_last": negll[-1],
+        }))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -77,6 +77,19 @@ __device__ __forceinline__ T gsum(T x) {
   return x;
 }
 
+// Add a per-lane contribution to the wave's double accumulator of row `row`: the lanes holding the
+// same row (all column slots of the wave) are summed with cross-lane shuffles first, then one lane
+// per row does a plain (non-atomic) read-modify-write -- every address has exactly one writer.
+// D >= V (CPF == 1): lanes with equal lane % G share rows; D < V: every lane holds all D rows.
+template <int G, int CPF, int SEG, typename T>
+__device__ __forceinline__ void wave_accumulate(double* __restrict__ acc, int row, T v, int lane) {
+  (void)CPF;
+  (void)SEG;
+#pragma unroll
+  for (int m = G; m < 64; m <<= 1) v += __shfl_xor(v, m);
+  if (lane < G) acc[row] += (double)v;
+}
+
 template <typename T>
 __device__ __forceinline__ T sigm(T t) { return (T)1 / ((T)1 + exp(-t)); }
 
@@ -198,17 +211,17 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
   constexpr int SEG = D >= V ? V : D;
   constexpr int COLS = 64 / G * CPF;  // columns per wave tile (one fragment per lane)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // LDS: [grad accumulators: nparams doubles][loss: 4 waves x double][records][activations]
-  double* gacc = reinterpret_cast<double*>(smem);
+  // LDS: [grad accumulators: 4 waves x nparams doubles][loss: 4 waves x double][records][activations]
   const int gbytes = ((a.nparams * 8 + 15) / 16) * 16;
-  double* lossw = reinterpret_cast<double*>(smem + gbytes);
-  T* rec = reinterpret_cast<T*>(smem + gbytes + 64);
+  double* gacc = reinterpret_cast<double*>(smem + (threadIdx.x >> 6) * gbytes);  // this wave's
+  double* lossw = reinterpret_cast<double*>(smem + 4 * gbytes);
+  T* rec = reinterpret_cast<T*>(smem + 4 * gbytes + 64);
   int nrec = 0;
   for (int s = 0; s < a.nsteps; ++s) nrec += grad_nparams(a.op[s]) * (D > V ? D : V);
   T* act = rec + ((nrec + 3) / 4) * 4 + (threadIdx.x >> 6) * (a.nsteps * 64 * V);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < a.nparams; i += blockDim.x) gacc[i] = 0.0;
+  for (int i = lane; i < a.nparams; i += 64) gacc[i] = 0.0;
   // raw parameter records, layout [group][param][element] as the forward kernel (RV = V)
   for (int s = 0; s < a.nsteps; ++s) {
     const LayerDesc& L = a.layers[a.layer[s]];
@@ -321,9 +334,8 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
           vg = gsum<G>(vg);
 #pragma unroll
           for (int e = 0; e < SEG; ++e) {
-            const int row = r0 + e;
-            const T contrib = g[c * SEG + e] * vx + xin[c * SEG + e] * vg;
-            if (valid[c * SEG + e]) atomicAdd(&gacc[a.goff[s] + row], (double)contrib);
+            const T contrib = valid[c * SEG + e] ? g[c * SEG + e] * vx + xin[c * SEG + e] * vg : (T)0;
+            wave_accumulate<G, CPF, SEG>(gacc + a.goff[s], r0 + e, contrib, lane);
             g[c * SEG + e] = fma(-vg, r[c * SEG + e], g[c * SEG + e]);
           }
         }
@@ -333,10 +345,9 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
           T p[4], dp[4] = {0, 0, 0, 0};
           for (int q = 0; q < np; ++q) p[q] = r[q * V + e];
           const T gx = bwd_elem<T>(op, xin[e], g[e], p, dp);
-          if (valid[e]) {
-            const int row = r0 + e % SEG;
-            for (int q = 0; q < np; ++q) atomicAdd(&gacc[a.goff[s] + q * D + row], (double)dp[q]);
-          }
+          const int row = r0 + e % SEG;
+          for (int q = 0; q < np; ++q)
+            wave_accumulate<G, CPF, SEG>(gacc + a.goff[s] + q * D, row, valid[e] ? dp[q] : (T)0, lane);
           g[e] = valid[e] ? gx : (T)0;
         }
       }
@@ -348,7 +359,11 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
   __syncthreads();
   double* out = (double*)a.partial + (int64_t)blockIdx.x * (1 + a.nparams);
   if (tid == 0) out[0] = lossw[0] + lossw[1] + lossw[2] + lossw[3];
-  for (int i = tid; i < a.nparams; i += blockDim.x) out[1 + i] = gacc[i];
+  const double* g0 = reinterpret_cast<const double*>(smem);
+  for (int i = tid; i < a.nparams; i += blockDim.x) {
+    const int w = gbytes / 8;
+    out[1 + i] = ((g0[i] + g0[w + i]) + g0[2 * w + i]) + g0[3 * w + i];
+  }
 }
 
 // Sum the block partials (double, block order), project Householder direction gradients, add to out.
@@ -359,21 +374,31 @@ struct ReduceArgs {
   int32_t D;
   int32_t nh;  // Householder columns
   void* out;
+  double* tot;  // 1 + nparams totals (workspace tail)
   // per Householder column: offset of its gradient vector and its device column pointer
   int32_t hoff[kMaxGradSteps];
   const void* hcol[kMaxGradSteps];
 };
 
-template <typename T>
-__global__ __launch_bounds__(256) void grad_reduce_kernel(ReduceArgs r) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* tot = reinterpret_cast<double*>(smem);  // 1 + nparams
-  for (int i = threadIdx.x; i < 1 + r.nparams; i += blockDim.x) {
-    double s = 0.0;
-    for (int b = 0; b < r.nblocks; ++b) s += r.partial[(int64_t)b * (1 + r.nparams) + i];
-    tot[i] = s;
-  }
+// Sum of the block partials, in block order per wave (b = w, w + 4, ...) and then over the 4 waves,
+// in double: tot[i] for the loss (i = 0) and every gradient entry. 64 entries per block.
+__global__ __launch_bounds__(256) void grad_sum_kernel(ReduceArgs r) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t n = 1 + (int64_t)r.nparams;
+  double s = 0.0;
+  if (i < n)
+    for (int b = w; b < r.nblocks; b += 4) s += r.partial[(int64_t)b * n + i];
+  red[w][lane] = s;
   __syncthreads();
+  if (w == 0 && i < n) r.tot[i] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+// Householder direction projection and accumulation into out (one block).
+template <typename T>
+__global__ __launch_bounds__(256) void grad_finalize_kernel(ReduceArgs r) {
+  double* tot = r.tot;
   // Householder: dS/dw = -sqrt2 * G;  dS/dv = (dS/dw - w (dS/dw . w)) / |v|  (householder_trafo.jl:32)
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
@@ -450,7 +475,7 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
   const size_t gbytes = ((size_t)goff * 8 + 15) / 16 * 16;
   const size_t rbytes = ((size_t)(roff + 3) / 4) * 4 * esz;
   const size_t abytes = (size_t)4 * s * 64 * V * esz;
-  P.lds = gbytes + 64 + rbytes + abytes;
+  P.lds = 4 * gbytes + 64 + rbytes + abytes;
   if (P.lds > 160 * 1024) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: flow too large for LDS");
   const int cols = (int)(64 / (D >= V ? D / V : 1) * (D >= V ? 1 : V / D));
   const int64_t tiles = (N + cols - 1) / cols;
@@ -488,7 +513,8 @@ hipError_t launch_grad(const Plan& P, hipStream_t st) {
     default: return hipErrorInvalidValue;
   }
   if (e0 != hipSuccess) return e0;
-  hipLaunchKernelGGL((grad_reduce_kernel<T>), dim3(1), dim3(256), (size_t)(1 + P.ra.nparams) * 8, st, P.ra);
+  hipLaunchKernelGGL(grad_sum_kernel, dim3((unsigned)((1 + P.ra.nparams + 63) / 64)), dim3(256), 0, st, P.ra);
+  hipLaunchKernelGGL((grad_finalize_kernel<T>), dim3(1), dim3(256), 0, st, P.ra);
   return hipGetLastError();
 }
 
@@ -499,7 +525,7 @@ enf_status negll_grad_workspace(bool f64, int64_t D, int64_t N, const enf_layer*
   Plan P;
   enf_status s = make_plan(f64, D, N > 0 ? N : 1, layers, nlayers, P);
   if (s != ENF_OK) return s;
-  *bytes = (size_t)P.blocks * (1 + (size_t)P.ga.nparams) * sizeof(double);
+  *bytes = ((size_t)P.blocks + 1) * (1 + (size_t)P.ga.nparams) * sizeof(double);
   return ENF_OK;
 }
 
@@ -508,12 +534,13 @@ enf_status negll_grad(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx
   Plan P;
   enf_status s = make_plan(f64, D, N, layers, nlayers, P);
   if (s != ENF_OK) return s;
-  const size_t need = (size_t)P.blocks * (1 + (size_t)P.ga.nparams) * sizeof(double);
+  const size_t need = ((size_t)P.blocks + 1) * (1 + (size_t)P.ga.nparams) * sizeof(double);
   if (!workspace || workspace_bytes < need) return set_error(ENF_ERR_INVALID, "enf_flow_negll_grad: workspace too small");
   P.ga.X = X;
   P.ga.ldx = ldx;
   P.ga.partial = workspace;
   P.ra.partial = (const double*)workspace;
+  P.ra.tot = (double*)workspace + (size_t)P.blocks * (1 + (size_t)P.ga.nparams);
   P.ra.out = out;
   hipError_t e = f64 ? launch_grad<double>(P, st) : launch_grad<float>(P, st);
   if (e != hipSuccess) return set_error(ENF_ERR_HIP, hipGetErrorString(e));

@@ -201,6 +201,21 @@ def mvnormal_negll_trafo(trafo, X) -> float:
     return mvnormal_negll_trafograd(trafo, X)[0]
 
 
+def trainable_runs(state: "FlowState"):
+    """[start, end) ranges of theta holding trainable parameters, adjacent segments merged (one
+    enf_adagrad_step launch per run instead of one per parameter vector)."""
+    runs = []
+    for i, tr in enumerate(state.trainable):
+        if not tr:
+            continue
+        s0, s1 = int(state.offsets[i]), int(state.offsets[i + 1])
+        if runs and runs[-1][1] == s0:
+            runs[-1] = (runs[-1][0], s1)
+        else:
+            runs.append((s0, s1))
+    return runs
+
+
 def minibatch_plan(N: int, nbatches: int, rank: int = 0, world: int = 1):
     """Minibatches of optimize_whitening (src/optimize_whitening.jl:31-32: batchsize =
     round(Int, N/nbatches), Iterators.partition, the last batch possibly shorter) and this rank's
@@ -251,7 +266,7 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
     ws = _workspace(state, batchsize)
     hist = torch.zeros(nepochs * len(plan), dtype=torch.float64, device=M.device)
     hcols = state.householder_columns()
-    segs = [(int(state.offsets[i]), int(state.offsets[i + 1])) for i, tr in enumerate(state.trainable) if tr]
+    segs = trainable_runs(state)
     step = 0
     with torch.cuda.device(M.device):
         stream = torch.cuda.current_stream(M.device).cuda_stream
