@@ -56,7 +56,7 @@ def main():
 
     enf = load()
     lib = enf._lib
-    from euclidiannormalizingflows_jl_amd.train import FlowState, _workspace, trainable_runs  # noqa: E402
+    from euclidiannormalizingflows_jl_amd.train import FlowState, _workspace, householder_batches, trainable_runs  # noqa: E402,E501
 
     D, N = args.D, args.N
     mk = lambda layers: enf.compose(*[enf.HouseholderTrafo(ps[0]) if op == 5 else enf.JohnsonTrafo(*ps)
@@ -79,7 +79,7 @@ def main():
     out = torch.zeros(1 + state.nparams, dtype=torch.float32, device=dev)
     ws = _workspace(state, max(B for B, _, _ in plan))
     segs = trainable_runs(state)
-    hcols = state.householder_columns()
+    hbatches = householder_batches(state)
     L = lib.lib()
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
@@ -102,8 +102,8 @@ def main():
         for s0, s1 in segs:
             lib.check(L.enf_adagrad_step(lib.ENF_F32, s1 - s0, state.theta[s0:].data_ptr(), state.acc[s0:].data_ptr(),
                                          g_[s0:].data_ptr(), 1.0 / B, opt.eta, opt.epsilon, sh))
-        for off, k in hcols:
-            lib.check(L.enf_householder_normalize(lib.ENF_F32, D, k, state.theta[off:].data_ptr(), sh))
+        for off, k, ldv in hbatches:
+            lib.check(L.enf_householder_normalize_strided(lib.ENF_F32, D, k, state.theta[off:].data_ptr(), ldv, sh))
         return out[0:1] / B
 
     for i in range(args.warmup):

@@ -22,7 +22,7 @@ EXPORTED = (
     "enf_version", "enf_last_error", "enf_device_count", "enf_set_device", "enf_get_device",
     "enf_malloc", "enf_free", "enf_memcpy", "enf_stream_synchronize", "enf_flow_apply",
     "enf_flow_param_count", "enf_flow_negll_grad_workspace", "enf_flow_negll_grad",
-    "enf_adagrad_step", "enf_householder_normalize", "enf_comm_unique_id", "enf_comm_init",
+    "enf_adagrad_step", "enf_householder_normalize", "enf_householder_normalize_strided", "enf_comm_unique_id", "enf_comm_init",
     "enf_comm_destroy", "enf_allreduce_sum",
 )
 
@@ -63,6 +63,7 @@ _SIGS = {
                                            _vp, _vp, _sz, _vp]),
     "enf_adagrad_step": (ctypes.c_int, [ctypes.c_int, _i64, _vp, _vp, _vp, _dbl, _dbl, _dbl, _vp]),
     "enf_householder_normalize": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _vp, _vp]),
+    "enf_householder_normalize_strided": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _vp, _i64, _vp]),
     "enf_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "enf_comm_init": (ctypes.c_int, [ctypes.POINTER(_vp), _i32, ctypes.c_char_p, _i32]),
     "enf_comm_destroy": (ctypes.c_int, [_vp]),

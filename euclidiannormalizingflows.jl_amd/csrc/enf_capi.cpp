@@ -330,7 +330,19 @@ enf_status enf_householder_normalize(enf_dtype dtype, int64_t D, int64_t k, void
   if (D < 0 || k < 0) return fail(ENF_ERR_INVALID, "D and k must be >= 0");
   if (D == 0 || k == 0) return ENF_OK;
   if (!V) return fail(ENF_ERR_INVALID, "V is NULL");
-  return enf::householder_normalize(dtype == ENF_F64, D, k, V, (hipStream_t)hip_stream);
+  return enf::householder_normalize(dtype == ENF_F64, D, k, V, D, (hipStream_t)hip_stream);
+  ENF_CATCH
+}
+
+enf_status enf_householder_normalize_strided(enf_dtype dtype, int64_t D, int64_t k, void* V, int64_t ldv,
+                                             void* hip_stream) {
+  ENF_TRY
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
+  if (D < 0 || k < 0) return fail(ENF_ERR_INVALID, "D and k must be >= 0");
+  if (k > 1 && ldv < D) return fail(ENF_ERR_INVALID, "ldv < D");
+  if (D == 0 || k == 0) return ENF_OK;
+  if (!V) return fail(ENF_ERR_INVALID, "V is NULL");
+  return enf::householder_normalize(dtype == ENF_F64, D, k, V, ldv, (hipStream_t)hip_stream);
   ENF_CATCH
 }
 

@@ -360,6 +360,5 @@ __device__ __forceinline__ void frag_stream(const FlowArgs& a, Body& body) {
 // resident blocks per CU (hipOccupancy; ENF_BLOCKS_PER_CU lowers it for tuning) times the CUs.
 hipError_t frag_grid(const void* kernel, int64_t N, int64_t cols_per_block, size_t lds, const DeviceInfo& dev,
                      int64_t* blocks);
-int env_int(const char* name, int dflt);
 
 }  // namespace enf

@@ -24,6 +24,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "enf_grad_hj.h"
 #include "enf_internal.h"
 #include "enf_train.h"
 
@@ -387,9 +388,16 @@ __global__ __launch_bounds__(256) void grad_sum_kernel(ReduceArgs r) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 64 + lane;
   const int64_t n = 1 + (int64_t)r.nparams;
-  double s = 0.0;
-  if (i < n)
-    for (int b = w; b < r.nblocks; b += 4) s += r.partial[(int64_t)b * n + i];
+  // 8 independent accumulators (loads in flight together), combined in a fixed order
+  double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (i < n) {
+    int b = w;
+    for (; b + 28 < r.nblocks; b += 32)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s8[k] += r.partial[(int64_t)(b + 4 * k) * n + i];
+    for (; b < r.nblocks; b += 4) s8[0] += r.partial[(int64_t)b * n + i];
+  }
+  const double s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
   red[w][lane] = s;
   __syncthreads();
   if (w == 0 && i < n) r.tot[i] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
@@ -475,8 +483,7 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
   const size_t gbytes = ((size_t)goff * 8 + 15) / 16 * 16;
   const size_t rbytes = ((size_t)(roff + 3) / 4) * 4 * esz;
   const size_t abytes = (size_t)4 * s * 64 * V * esz;
-  P.lds = 4 * gbytes + 64 + rbytes + abytes;
-  if (P.lds > 160 * 1024) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: flow too large for LDS");
+  P.lds = 4 * gbytes + 64 + rbytes + abytes;  // generic kernel; checked where it is launched
   const int cols = (int)(64 / (D >= V ? D / V : 1) * (D >= V ? 1 : V / D));
   const int64_t tiles = (N + cols - 1) / cols;
   int64_t blocks = (tiles + 3) / 4;
@@ -542,7 +549,19 @@ enf_status negll_grad(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx
   P.ra.partial = (const double*)workspace;
   P.ra.tot = (double*)workspace + (size_t)P.blocks * (1 + (size_t)P.ga.nparams);
   P.ra.out = out;
-  hipError_t e = f64 ? launch_grad<double>(P, st) : launch_grad<float>(P, st);
+  hipError_t e;
+  static const int generic = env_int("ENF_GRAD_GENERIC", 0);
+  if (!f64 && !generic && hj_grad_eligible(D, ldx, X, layers, nlayers)) {
+    e = launch_hj_grad(D, N, X, layers, nlayers, P.ga.nparams, (double*)workspace, P.blocks, st);
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(grad_sum_kernel, dim3((unsigned)((1 + P.ra.nparams + 63) / 64)), dim3(256), 0, st, P.ra);
+      hipLaunchKernelGGL((grad_finalize_kernel<float>), dim3(1), dim3(256), 0, st, P.ra);
+      e = hipGetLastError();
+    }
+  } else {
+    if (P.lds > 160 * 1024) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: flow too large for LDS");
+    e = f64 ? launch_grad<double>(P, st) : launch_grad<float>(P, st);
+  }
   if (e != hipSuccess) return set_error(ENF_ERR_HIP, hipGetErrorString(e));
   return ENF_OK;
 }

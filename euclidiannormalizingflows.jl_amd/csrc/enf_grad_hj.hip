@@ -1,0 +1,347 @@
+// enf_grad_hj.hip -- fused forward + backward of the whitening loss for the config-5 flows
+// J_n o H_n o ... o J_1 o H_1 (fp32, D in {32, 64}, n <= 8, one reflection per H, contiguous
+// 16-byte aligned columns): mvnormal_negll_trafo / mvnormal_negll_trafograd
+// (src/optimize_whitening.jl:7-22) for the N local samples, as per-block partial sums in the
+// layout of enf_grad.hip (reduced and Householder-projected there).
+//
+// Forward (per pair, per element; hardware transcendentals as the forward kernel):
+//   dot = vh'u, h = u - dot vh, z = (h - xi)/lambda, y = gamma + delta asinh z,
+//   ladj += log|delta/lambda| - log(1 + z^2)/2    (householder_trafo.jl:8-11, johnson_trafo.jl:29-52)
+// storing z and dot per pair in LDS (the backward needs nothing else: h = lambda z + xi and
+// u = h + dot vh recover the layer inputs exactly as in the reference's pullback, which recomputes
+// them by re-reflection, householder_trafo.jl:91-101).
+// Backward with g = dS/dy (g = y at the output), s = sqrt(1 + z^2):
+//   dS/dgamma += g, dS/ddelta += g asinh z - 1/delta, dz = g delta/s + z/s^2,
+//   dS/dxi -= dz/lambda, dS/dlambda += -dz z/lambda + 1/lambda, g_h = dz/lambda,
+//   Householder: dS/dvh-direction += g_h (vh'u) + u (vh'g_h) (projected in grad_finalize_kernel),
+//   g_u = g_h - vh (vh'g_h).
+// Per-lane gradient partials of a tile are summed over the lanes holding the same rows (cross-
+// lane shuffles) and added by one lane per row into the wave's LDS accumulators; the block sums
+// its 4 waves in a fixed order (deterministic).
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+
+#include "enf_frag.h"
+#include "enf_grad_hj.h"
+
+namespace enf {
+
+namespace {
+
+constexpr int kU = 2;  // fragments (columns) per lane per tile
+constexpr int kNP = 8;  // records per pair: vh, gamma, delta*ln2, 1/lambda, -xi/lambda, lambda, xi, delta
+
+template <int D>
+struct GL {
+  static constexpr int V = 4;
+  static constexpr int G = D / V;            // lanes per column
+  static constexpr int S = 64 / G;           // column slots per wave instruction
+  static constexpr int TC = S * kU;          // columns per wave tile
+};
+
+// cross-slot sum: lanes with equal lane % G hold the same rows
+template <int G>
+__device__ __forceinline__ float slot_sum(float v) {
+#pragma unroll
+  for (int m = G; m < 64; m <<= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+template <int D, bool TAIL>
+__device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int lane, const float* __restrict__ rec,
+                                          float* __restrict__ zst, float* __restrict__ dst, float* __restrict__ acc,
+                                          double& lossp, int& nvalid, float ctot) {
+  using L = GL<D>;
+  constexpr int V = 4, G = L::G, S = L::S;
+  const int grp = lane % G;
+  const int n = a.n;
+  float x[kU][V];
+  float vm[kU];  // 1 for a valid column, 0 past N
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int64_t c = col0 + (int64_t)u * S + lane / G;
+    const float* src = a.X + c * D + V * grp;
+    vm[u] = (!TAIL || c < a.N) ? 1.f : 0.f;
+    if (!TAIL) {
+      const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
+      __builtin_memcpy(&x[u][0], &v4, 16);
+    } else {
+#pragma unroll
+      for (int e = 0; e < V; ++e) x[u][e] = c < a.N ? src[e] : 0.f;
+    }
+  }
+  // ---- forward
+  float lad[kU] = {};
+  for (int p = 0; p < n; ++p) {
+    const float* r = rec + (size_t)p * kNP * D + grp * kNP * V;
+    float vh[V], gam[V], dl2[V], il[V], nxil[V];
+    lds_vec<float, V>(r, vh);
+    lds_vec<float, V>(r + V, gam);
+    lds_vec<float, V>(r + 2 * V, dl2);
+    lds_vec<float, V>(r + 3 * V, il);
+    lds_vec<float, V>(r + 4 * V, nxil);
+    float dot[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      float t = vh[0] * x[u][0];
+#pragma unroll
+      for (int e = 1; e < V; ++e) t = fmaf(vh[e], x[u][e], t);
+      dot[u] = group_sum<G>(t);
+    }
+    float z[kU][V], q[kU][V];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        z[u][e] = fmaf(fmaf(-dot[u], vh[e], x[u][e]), il[e], nxil[e]);
+        q[u][e] = fmaf(z[u][e], z[u][e], 1.f);
+      }
+      dst[(p * kU + u) * 64 + lane] = dot[u];
+      *reinterpret_cast<u32x4*>(zst + ((size_t)(p * kU + u) * 64 + lane) * V) = *reinterpret_cast<const u32x4*>(&z[u][0]);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float Lz = copysignf(hw_log2(fabsf(z[u][e]) + hw_sqrt(q[u][e])), z[u][e]);
+        x[u][e] = fmaf(dl2[e], Lz, gam[e]);
+      }
+      lad[u] = fmaf(-0.5f, hw_log2((q[u][0] * q[u][1]) * (q[u][2] * q[u][3])), lad[u]);
+    }
+  }
+  // ---- loss: sum_d (y^2 + log 2 pi)/2 - ladj, ladj = ctot + ln2 * lad (valid columns)
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    float t = 0.f;
+#pragma unroll
+    for (int e = 0; e < V; ++e) t = fmaf(x[u][e], x[u][e], t);
+    const float ysq = group_sum<G>(t);
+    const float ltot = group_sum<G>(lad[u]);
+    if (grp == 0 && vm[u] != 0.f) {
+      lossp += 0.5 * (double)ysq + 0.5 * D * 1.8378770664093454836 - ((double)ctot + kLn2 * (double)ltot);
+      ++nvalid;
+    }
+  }
+  // ---- backward, g = dS/dy = y
+  float g[kU][V];
+#pragma unroll
+  for (int u = 0; u < kU; ++u)
+#pragma unroll
+    for (int e = 0; e < V; ++e) g[u][e] = x[u][e] * vm[u];
+  for (int p = n - 1; p >= 0; --p) {
+    const float* r = rec + (size_t)p * kNP * D + grp * kNP * V;
+    float vh[V], il[V], lam[V], xi[V], del[V];
+    lds_vec<float, V>(r, vh);
+    lds_vec<float, V>(r + 3 * V, il);
+    lds_vec<float, V>(r + 5 * V, lam);
+    lds_vec<float, V>(r + 6 * V, xi);
+    lds_vec<float, V>(r + 7 * V, del);
+    float aG[V] = {}, aD[V] = {}, aX[V] = {}, aL[V] = {}, aV[V] = {};
+    float gh[kU][V], u_[kU][V], dot1[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      float z[V];
+      *reinterpret_cast<u32x4*>(&z[0]) = *reinterpret_cast<const u32x4*>(zst + ((size_t)(p * kU + u) * 64 + lane) * V);
+      dot1[u] = dst[(p * kU + u) * 64 + lane];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float q = fmaf(z[e], z[e], 1.f);
+        const float s = hw_sqrt(q);
+        const float rs = hw_rcp(s);
+        const float Lz = copysignf(hw_log2(fabsf(z[e]) + s), z[e]);
+        aG[e] += g[u][e];
+        aD[e] = fmaf(g[u][e], Lz, aD[e]);
+        const float dz = fmaf(g[u][e] * del[e], rs, z[e] * (rs * rs) * vm[u]);
+        gh[u][e] = dz * il[e];
+        aX[e] += gh[u][e];
+        aL[e] = fmaf(gh[u][e], z[e], aL[e]);
+        u_[u][e] = fmaf(dot1[u], vh[e], fmaf(lam[e], z[e], xi[e]));  // layer input u = h + dot vh
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      float t = vh[0] * gh[u][0];
+#pragma unroll
+      for (int e = 1; e < V; ++e) t = fmaf(vh[e], gh[u][e], t);
+      const float vg = group_sum<G>(t);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        aV[e] = fmaf(gh[u][e], dot1[u], fmaf(u_[u][e], vg, aV[e]));
+        g[u][e] = fmaf(-vg, vh[e], gh[u][e]);
+      }
+    }
+    // flush: one lane per row adds the wave's sums (acc layout [pair][param 5][D])
+    float* ap = acc + (size_t)p * 5 * D + V * grp;
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const float sV = slot_sum<G>(aV[e]), sG = slot_sum<G>(aG[e]), sD = slot_sum<G>(aD[e]);
+      const float sX = slot_sum<G>(aX[e]), sL = slot_sum<G>(aL[e]);
+      if (lane < G) {
+        ap[e] += sV;
+        ap[D + e] += sG;
+        ap[2 * D + e] += sD;
+        ap[3 * D + e] += sX;
+        ap[4 * D + e] += sL;
+      }
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void hj_grad_kernel(HJGradArgs a) {
+  using L = GL<D>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int n = a.n;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // LDS: [scratch: per pair {hs, cl}, per wave {loss, nvalid}][records][per wave: acc, z, dot]
+  double* scr = reinterpret_cast<double*>(smem);                       // 2*8 + 8 doubles
+  float* rec = reinterpret_cast<float*>(smem + 256);                  // n * kNP * D floats
+  const size_t recb = (size_t)n * kNP * D * 4;
+  const size_t accb = (size_t)n * 5 * D * 4;
+  const size_t zb = (size_t)n * kU * 64 * 16;
+  const size_t db = (size_t)n * kU * 64 * 4;
+  unsigned char* wbase = smem + 256 + recb + (size_t)wave * (accb + zb + db);
+  float* acc = reinterpret_cast<float*>(wbase);
+  float* zst = reinterpret_cast<float*>(wbase + accb);
+  float* dst = reinterpret_cast<float*>(wbase + accb + zb);
+  for (int i = lane; i < n * 5 * D; i += 64) acc[i] = 0.f;
+  // pass 1: per pair v'v and the constant ladj part sum log|delta/lambda| (double)
+  for (int p = wave; p < n; p += 4) {
+    double vv = 0.0, cl = 0.0;
+    for (int d = lane; d < D; d += 64) {
+      const double vd = a.v[p][d];
+      vv += vd * vd;
+      cl += log(fabs((double)a.d[p][d])) - log(fabs((double)a.lam[p][d]));
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+      vv += __shfl_xor(vv, m);
+      cl += __shfl_xor(cl, m);
+    }
+    if (lane == 0) {
+      scr[2 * p] = sqrt(2.0 / vv);
+      scr[2 * p + 1] = cl;
+    }
+  }
+  __syncthreads();
+  // pass 2: records [pair][group][param][4]
+  for (int i = tid; i < n * D; i += blockDim.x) {
+    const int p = i / D, d = i % D;
+    float* r = rec + (size_t)p * kNP * D + (d / 4) * kNP * 4 + (d % 4);
+    const double lam = a.lam[p][d], xi = a.xi[p][d], del = a.d[p][d];
+    r[0] = (float)((double)a.v[p][d] * scr[2 * p]);
+    r[4] = a.g[p][d];
+    r[8] = (float)(del * kLn2);
+    r[12] = (float)(1.0 / lam);
+    r[16] = (float)(-xi / lam);
+    r[20] = (float)lam;
+    r[24] = (float)xi;
+    r[28] = (float)del;
+  }
+  __syncthreads();
+  float ctot = 0.f;
+  {
+    double c = 0.0;
+    for (int p = 0; p < n; ++p) c += scr[2 * p + 1];
+    ctot = (float)c;
+  }
+  double lossp = 0.0;
+  int nvalid = 0;
+  const int64_t ntiles = (a.N + L::TC - 1) / L::TC;
+  const int64_t full = a.N / L::TC;
+  const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wave);
+  for (int64_t t = wave_id; t < ntiles; t += (int64_t)gridDim.x * 4) {
+    if (t < full) grad_tile<D, false>(a, t * L::TC, lane, rec, zst, dst, acc, lossp, nvalid, ctot);
+    else grad_tile<D, true>(a, t * L::TC, lane, rec, zst, dst, acc, lossp, nvalid, ctot);
+  }
+  // block partial: loss, then the flow gradient (layer order, enf_flow_param_count layout)
+  for (int m = 32; m >= 1; m >>= 1) {
+    lossp += __shfl_xor(lossp, m);
+    nvalid += __shfl_xor(nvalid, m);
+  }
+  double* wl = scr + 2 * kHJGradMaxPairs;
+  if (lane == 0) {
+    wl[2 * wave] = lossp;
+    wl[2 * wave + 1] = (double)nvalid;
+  }
+  __syncthreads();
+  double* out = a.partial + (int64_t)blockIdx.x * (1 + a.nparams);
+  const double nb = wl[1] + wl[3] + wl[5] + wl[7];
+  if (tid == 0) out[0] = ((wl[0] + wl[2]) + wl[4]) + wl[6];
+  const size_t wstride = (accb + zb + db) / 4;  // floats between the waves' acc arrays
+  const float* acc0 = reinterpret_cast<const float*>(smem + 256 + recb);
+  for (int i = tid; i < n * 5 * D; i += blockDim.x) {
+    const int p = i / (5 * D), k = (i / D) % 5, d = i % D;
+    const double s = (((double)acc0[i] + (double)acc0[wstride + i]) + (double)acc0[2 * wstride + i]) +
+                     (double)acc0[3 * wstride + i];
+    const double del = a.d[p][d], lam = a.lam[p][d];
+    double gval;
+    int64_t o;
+    switch (k) {
+      case 0: gval = s; o = a.goffH[p] + d; break;                             // raw Householder sum
+      case 1: gval = s; o = a.goffJ[p] + d; break;                             // gamma
+      case 2: gval = kLn2 * s - nb / del; o = a.goffJ[p] + D + d; break;       // delta
+      case 3: gval = -s; o = a.goffJ[p] + 2 * D + d; break;                    // xi
+      default: gval = -s + nb / lam; o = a.goffJ[p] + 3 * D + d; break;        // lambda
+    }
+    out[1 + o] = gval;
+  }
+}
+
+template <int D>
+size_t hj_grad_lds(int n) {
+  return 256 + (size_t)n * kNP * D * 4 + 4 * ((size_t)n * 5 * D * 4 + (size_t)n * kU * 64 * 16 + (size_t)n * kU * 64 * 4);
+}
+
+}  // namespace
+
+bool hj_grad_eligible(int64_t D, int64_t ldx, const void* X, const enf_layer* layers, int32_t nlayers) {
+  if ((D != 32 && D != 64) || ldx != D || (((uintptr_t)X) & 15) != 0) return false;
+  if (nlayers < 2 || (nlayers & 1) || nlayers / 2 > kHJGradMaxPairs) return false;
+  for (int32_t l = 0; l < nlayers; ++l) {
+    const int want = (l & 1) ? OP_JOHNSON : OP_HOUSEHOLDER;
+    if (layers[l].op != want || (want == OP_HOUSEHOLDER && layers[l].k != 1)) return false;
+  }
+  return true;
+}
+
+hipError_t launch_hj_grad(int64_t D, int64_t N, const void* X, const enf_layer* layers, int32_t nlayers,
+                          int32_t nparams, double* partial, int blocks, hipStream_t st) {
+  HJGradArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.X = (const float*)X;
+  a.N = N;
+  a.n = nlayers / 2;
+  a.D = (int32_t)D;
+  a.partial = partial;
+  a.nparams = nparams;
+  int32_t off = 0;
+  for (int p = 0; p < a.n; ++p) {
+    const enf_layer& H = layers[2 * p];
+    const enf_layer& J = layers[2 * p + 1];
+    a.v[p] = (const float*)H.p[0];
+    a.goffH[p] = off;
+    off += (int32_t)D;
+    a.g[p] = (const float*)J.p[0];
+    a.d[p] = (const float*)J.p[1];
+    a.xi[p] = (const float*)J.p[2];
+    a.lam[p] = (const float*)J.p[3];
+    a.goffJ[p] = off;
+    off += 4 * (int32_t)D;
+  }
+  if (off != nparams) return hipErrorInvalidValue;
+  const size_t lds = D == 32 ? hj_grad_lds<32>(a.n) : hj_grad_lds<64>(a.n);
+  const void* k = D == 32 ? (const void*)&hj_grad_kernel<32> : (const void*)&hj_grad_kernel<64>;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  if (D == 32) hipLaunchKernelGGL(hj_grad_kernel<32>, dim3(blocks), dim3(256), lds, st, a);
+  else hipLaunchKernelGGL(hj_grad_kernel<64>, dim3(blocks), dim3(256), lds, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace enf

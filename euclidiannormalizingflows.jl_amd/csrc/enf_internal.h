@@ -82,6 +82,9 @@ inline size_t record_elems(int op, int64_t D, size_t elem, bool frag) {
   return (n + q - 1) / q * q;
 }
 
+// development knobs read from the environment (enf_flow.hip)
+int env_int(const char* name, int dflt);
+
 size_t program_lds_bytes(const FlowArgs& a, size_t elem);
 bool frag_supported(const FlowArgs& a, size_t elem);
 hipError_t launch_flow(const FlowArgs& a, bool f64, hipStream_t st, const DeviceInfo& dev);

@@ -19,6 +19,6 @@ enf_status negll_grad(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx
                       int32_t nlayers, void* out, void* workspace, size_t workspace_bytes, hipStream_t st);
 enf_status adagrad_step(bool f64, int64_t count, void* params, void* acc, const void* grad, double grad_scale,
                         double eta, double epsilon, hipStream_t st);
-enf_status householder_normalize(bool f64, int64_t D, int64_t k, void* V, hipStream_t st);
+enf_status householder_normalize(bool f64, int64_t D, int64_t k, void* V, int64_t ldv, hipStream_t st);
 
 }  // namespace enf

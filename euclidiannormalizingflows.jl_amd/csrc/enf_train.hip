@@ -40,11 +40,11 @@ enf_status adagrad_step(bool f64, int64_t count, void* params, void* acc, const 
 // LinearAlgebra.normalize! of every column (src/householder_trafo.jl:135-139): v .*= inv(norm(v)).
 // One wave per column; the sum of squares in double.
 template <typename T>
-__global__ void normalize_kernel(int64_t D, int64_t k, T* __restrict__ V) {
+__global__ void normalize_kernel(int64_t D, int64_t k, T* __restrict__ V, int64_t ldv) {
   const int lane = threadIdx.x & 63;
   const int64_t col = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (col >= k) return;  // whole wave exits together
-  T* v = V + col * D;
+  T* v = V + col * ldv;
   double ss = 0.0;
   for (int64_t d = lane; d < D; d += 64) ss += (double)v[d] * (double)v[d];
   for (int m = 32; m >= 1; m >>= 1) ss += __shfl_xor(ss, m);
@@ -52,10 +52,10 @@ __global__ void normalize_kernel(int64_t D, int64_t k, T* __restrict__ V) {
   for (int64_t d = lane; d < D; d += 64) v[d] *= inv;
 }
 
-enf_status householder_normalize(bool f64, int64_t D, int64_t k, void* V, hipStream_t st) {
+enf_status householder_normalize(bool f64, int64_t D, int64_t k, void* V, int64_t ldv, hipStream_t st) {
   const unsigned blocks = (unsigned)((k + 3) / 4);
-  if (f64) hipLaunchKernelGGL(normalize_kernel<double>, dim3(blocks), dim3(256), 0, st, D, k, (double*)V);
-  else hipLaunchKernelGGL(normalize_kernel<float>, dim3(blocks), dim3(256), 0, st, D, k, (float*)V);
+  if (f64) hipLaunchKernelGGL(normalize_kernel<double>, dim3(blocks), dim3(256), 0, st, D, k, (double*)V, ldv);
+  else hipLaunchKernelGGL(normalize_kernel<float>, dim3(blocks), dim3(256), 0, st, D, k, (float*)V, ldv);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? ENF_OK : set_error(ENF_ERR_HIP, hipGetErrorString(e));
 }

@@ -216,6 +216,19 @@ def trainable_runs(state: "FlowState"):
     return runs
 
 
+def householder_batches(state: "FlowState"):
+    """Householder vectors of theta as (offset, count, stride) batches for
+    enf_householder_normalize_strided: single equally spaced columns (the (J∘H)^n flows) become one
+    batch, a HouseholderTrafo with a D x k matrix is one contiguous batch of k columns."""
+    cols = state.householder_columns()
+    if len(cols) > 1 and all(k == 1 for _, k in cols):
+        offs = [o for o, _ in cols]
+        st = offs[1] - offs[0]
+        if st >= state.D and all(offs[i + 1] - offs[i] == st for i in range(len(offs) - 1)):
+            return [(offs[0], len(offs), st)]
+    return [(o, k, state.D) for o, k in cols]
+
+
 def minibatch_plan(N: int, nbatches: int, rank: int = 0, world: int = 1):
     """Minibatches of optimize_whitening (src/optimize_whitening.jl:31-32: batchsize =
     round(Int, N/nbatches), Iterators.partition, the last batch possibly shorter) and this rank's
@@ -265,7 +278,7 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
     out = torch.zeros(1 + state.nparams, dtype=dtype, device=M.device)
     ws = _workspace(state, batchsize)
     hist = torch.zeros(nepochs * len(plan), dtype=torch.float64, device=M.device)
-    hcols = state.householder_columns()
+    hbatches = householder_batches(state)
     segs = trainable_runs(state)
     step = 0
     with torch.cuda.device(M.device):
@@ -285,8 +298,9 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
                     _lib.check(L.enf_adagrad_step(dt, s1 - s0, state.theta[s0:].data_ptr(), state.acc[s0:].data_ptr(),
                                                   g[s0:].data_ptr(), 1.0 / B, optimizer.eta, optimizer.epsilon,
                                                   stream))
-                for off, k in hcols:
-                    _lib.check(L.enf_householder_normalize(dt, D, k, state.theta[off:].data_ptr(), stream))
+                for off, k, ldv in hbatches:
+                    _lib.check(L.enf_householder_normalize_strided(dt, D, k, state.theta[off:].data_ptr(), ldv,
+                                                                   stream))
                 step += 1
     h = hist.cpu().numpy().tolist()
     prev = list(negll_history) if negll_history is not None else []

@@ -124,6 +124,10 @@ enf_status enf_adagrad_step(enf_dtype dtype, int64_t count, void* params, void* 
  * the k columns of the D x k device matrix V to unit 2-norm, in place. */
 enf_status enf_householder_normalize(enf_dtype dtype, int64_t D, int64_t k, void* V,
                                      void* hip_stream);
+/* The same for k columns at a column stride ldv >= D (column j at V + j*ldv): every
+ * HouseholderTrafo vector of a flow's flat parameter vector in one launch. */
+enf_status enf_householder_normalize_strided(enf_dtype dtype, int64_t D, int64_t k, void* V, int64_t ldv,
+                                             void* hip_stream);
 
 /* ---------------------------------------------------------------- RCCL ---------------- */
 /* Opaque communicator for the gradient all-reduce (one rank per GPU, one process each). */

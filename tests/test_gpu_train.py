@@ -149,3 +149,65 @@ def test_grad_rccl_single_rank_allreduce(enf, gpu):
     torch.cuda.synchronize()
     assert torch.equal(buf.cpu(), torch.arange(10, dtype=torch.float32))
     assert L.enf_comm_destroy(comm) == 0
+
+
+@pytest.mark.parametrize("D,pairs", [(32, 1), (32, 3), (32, 8), (64, 1), (64, 4)])
+def test_hj_grad_kernel_vs_fp64(enf, gpu, oracle, D, pairs):
+    """The fused (J∘H)^n fp32 training kernel (enf_grad_hj.hip) against the fp64 generic kernel,
+    whose gradients the finite-difference test pins; ragged N (tail tile), loss vs the oracle."""
+    rng = np.random.default_rng(50 + D + pairs)
+    L64 = []
+    for _ in range(pairs):
+        L64 += [(5, rand_params(rng, 5, D, np.float64)), (3, rand_params(rng, 3, D, np.float64))]
+    L32 = [(op, [np.asarray(p, np.float32) for p in ps]) for op, ps in L64]
+    X = np.asfortranarray(rng.standard_normal((D, 5003)))
+    n64, g64 = enf.mvnormal_negll_trafograd(make_flow(enf, L64), colmajor_cuda(X))
+    X32 = np.asfortranarray(X.astype(np.float32))
+    n32, g32 = enf.mvnormal_negll_trafograd(make_flow(enf, L32), colmajor_cuda(X32))
+    ref = oracle_negll(oracle, L32, X32)
+    assert abs(n32 - ref) < 2e-5 * (abs(ref) + 1)
+    assert abs(n32 - n64) < 1e-4 * (abs(n64) + 1)
+    for p64, p32 in zip(g64, g32):
+        for a, b in zip(p64, p32):
+            a, b = np.ravel(a), np.ravel(b)
+            assert np.max(np.abs(a - b)) < 1e-3 * (np.max(np.abs(a)) + 1e-3), (np.max(np.abs(a - b)), np.max(np.abs(a)))
+
+
+def test_householder_normalize_strided(enf, gpu):
+    """enf_householder_normalize_strided: k columns at stride ldv normalised, the gaps untouched."""
+    import torch
+
+    rng = np.random.default_rng(3)
+    D, k, ldv = 32, 4, 160
+    buf = rng.standard_normal(ldv * k)
+    t = torch.from_numpy(buf.copy()).cuda()
+    enf._lib.check(enf._lib.lib().enf_householder_normalize_strided(enf._lib.ENF_F64, D, k, t.data_ptr(), ldv, None))
+    got = t.cpu().numpy()
+    want = buf.copy()
+    for j in range(k):
+        c = want[j * ldv:j * ldv + D]
+        want[j * ldv:j * ldv + D] = c / np.linalg.norm(c)
+    assert np.allclose(got, want, rtol=1e-14, atol=0)
+
+
+def test_optimize_whitening_hj_flow_matches_manual_step(enf, gpu):
+    """One optimize_whitening step on a (J∘H)^2 fp64 flow (strided Householder batch) == manual
+    ADAGrad + normalisation of every reflection vector."""
+    rng = np.random.default_rng(9)
+    D = 4
+    layers = []
+    for _ in range(2):
+        layers += [(5, rand_params(rng, 5, D, np.float64)), (3, rand_params(rng, 3, D, np.float64))]
+    X = rng.standard_normal((D, 777))
+    f = make_flow(enf, layers)
+    opt = enf.ADAGrad()
+    negll0, grads = enf.mvnormal_negll_trafograd(f, colmajor_cuda(X))
+    res = enf.optimize_whitening(colmajor_cuda(X), f, opt, nbatches=1, nepochs=1)
+    assert abs(res.negll_history[0] - negll0) < 1e-12 * abs(negll0)
+    th = flat(layers, D)
+    g = np.concatenate([np.asarray(a).reshape(-1, order="F") for per in grads for a in per])
+    acc = opt.epsilon + g * g
+    th1 = th - opt.eta * g / (np.sqrt(acc) + opt.epsilon)
+    for o in (0, 5 * D):
+        th1[o:o + D] /= np.linalg.norm(th1[o:o + D])
+    assert np.allclose(res.optimizer_state.theta.cpu().numpy(), th1, rtol=1e-12, atol=1e-14)
