@@ -44,6 +44,35 @@ def build_flow(D, pairs, np_dtype, seed=42, pattern=None):
     return layers
 
 
+def pmc_evidence(D, N, args, kern_ms):
+    """HBM traffic per launch and the VALU issue picture of the same kernel on the same workload,
+    from the committed rocprofv3 PMC passes (profiles/r01_pmc_traffic.json, tools/pmc.sh): traffic =
+    FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE; VALU issue cycles per SIMD = (4 x plain +
+    8 x transcendental wave64 instructions) / 1024 SIMDs (MI355X_MICROARCH.md issue costs)."""
+    prof = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    try:
+        with open(prof) as f:
+            tr = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if not (tr.get("D") == D and tr.get("N") == N and tr.get("dtype") == args.dtype and tr.get("pairs") == args.pairs
+            and args.pattern is None):
+        return None, None
+    c = tr.get("counters", {})
+    valu = None
+    if "SQ_INSTS_VALU" in c and "SQ_INSTS_VALU_TRANS_F32" in c:
+        trans = c["SQ_INSTS_VALU_TRANS_F32"]
+        cyc = (4.0 * (c["SQ_INSTS_VALU"] - trans) + 8.0 * trans) / 1024.0
+        clk = tr.get("effective_clock_ghz")
+        valu = {"insts_per_launch": c["SQ_INSTS_VALU"], "trans_insts_per_launch": trans,
+                "issue_cycles_per_simd": cyc, "pmc_effective_clock_ghz": clk,
+                "pmc_kernel_ms": tr.get("median_duration_ns_profiled", 0) / 1e6,
+                "issue_frac_in_pmc_run": (cyc / (clk * 1e9 * tr["median_duration_ns_profiled"] * 1e-9)
+                                          if clk and tr.get("median_duration_ns_profiled") else None),
+                "source": "profiles/r01_pmc_traffic.json"}
+    return tr.get("hbm_bytes_per_launch"), valu
+
+
 def max_over_ranks(values, device, world):
     """Element-wise max over ranks of per-rank values (the timed region's wall time and kernel
     time): the whole job is as slow as its slowest GPU. torch.distributed all-reduce(MAX)
@@ -136,17 +165,7 @@ def main():
 
     bytes_per_launch = N * (2 * D + 1) * esz  # read X, write Y, write ladj
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    prof = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-    if os.path.exists(prof):
-        try:
-            with open(prof) as f:
-                tr = json.load(f)
-            if tr.get("D") == D and tr.get("N") == N and tr.get("dtype") == args.dtype and tr.get("pairs") == args.pairs:
-                traffic = tr.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
+    traffic, valu = pmc_evidence(D, N, args, kern_ms)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(layers, D, np_dtype, args.cpu_samples)
@@ -172,6 +191,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": kern_ms, "kernel_ms_max_rank": kern_ms_max,
                          "algorithmic_bytes_per_launch": bytes_per_launch},
+            "valu": valu,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
