@@ -139,6 +139,31 @@ end
 
 with_logabsdet_jacobian(f::_Supported, X::HipMatrix) = _apply(f, X, true)
 
-export HipMatrix
+# mvnormal_negll_trafograd (src/optimize_whitening.jl:18-22) for a flow over a HipMatrix batch:
+# (negll, flat gradient in the enf_flow_param_count layout: layer by layer, field by field).
+# Device sums over the batch, normalised here by the batch size; a data-parallel caller sums the
+# unnormalised buffer across ranks first (enf_allreduce_sum) and divides by the global size.
+function mvnormal_negll_trafograd(f::_Supported, X::HipMatrix{T}) where {T}
+    layers, keep = _layers(_leaves(f), X.D, T)
+    dt = T === Float64 ? ENF_F64 : ENF_F32
+    np = Ref{Int64}(0)
+    check(ccall((:enf_flow_param_count, libenf), Cint, (Int64, Ptr{EnfLayer}, Int32, Ref{Int64}),
+                X.D, layers, length(layers), np))
+    wsb = Ref{Csize_t}(0)
+    check(ccall((:enf_flow_negll_grad_workspace, libenf), Cint,
+                (Cint, Int64, Int64, Ptr{EnfLayer}, Int32, Ref{Csize_t}),
+                dt, X.D, X.N, layers, length(layers), wsb))
+    out = HipMatrix(zeros(T, 1 + np[], 1))
+    ws = HipBuffer(max(Int(wsb[]), 1))
+    check(ccall((:enf_flow_negll_grad, libenf), Cint,
+                (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Ptr{EnfLayer}, Int32, Ptr{Cvoid}, Ptr{Cvoid},
+                 Csize_t, Ptr{Cvoid}),
+                dt, X.D, X.N, X.buf.ptr, X.D, layers, length(layers), out.buf.ptr, ws.ptr, wsb[], C_NULL))
+    GC.@preserve keep nothing
+    g = Array(out)[:, 1] ./ X.N
+    g[1], g[2:end]
+end
+
+export HipMatrix, mvnormal_negll_trafograd
 
 end # module

@@ -211,3 +211,65 @@ def test_optimize_whitening_hj_flow_matches_manual_step(enf, gpu):
     for o in (0, 5 * D):
         th1[o:o + D] /= np.linalg.norm(th1[o:o + D])
     assert np.allclose(res.optimizer_state.theta.cpu().numpy(), th1, rtol=1e-12, atol=1e-14)
+
+
+def _dp_worker(rank, world, port, q):
+    """One rank of a data-parallel optimize_whitening on the one visible GPU (gloo moves the
+    (1 + P) gradient sums through the host; on a node the same code runs over RCCL)."""
+    import os
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "tests")]
+    from enf_pkg import load
+    from parity import colmajor_cuda, make_flow, rand_params
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    enf = load()
+    rng = np.random.default_rng(21)
+    D = 32
+    layers = []
+    for _ in range(2):
+        layers += [(5, rand_params(rng, 5, D, np.float64)), (3, rand_params(rng, 3, D, np.float64))]
+    X = rng.standard_normal((D, 3001))
+    res = enf.optimize_whitening(colmajor_cuda(X), make_flow(enf, layers), enf.ADAGrad(), nbatches=3, nepochs=2)
+    q.put((rank, res.optimizer_state.theta.cpu().numpy(), res.negll_history))
+    dist.destroy_process_group()
+
+
+def test_optimize_whitening_two_ranks_equals_one(enf, gpu):
+    """World size 2 (two processes, shares of every minibatch, summed gradients normalised by the
+    global batch) reproduces the single-process trajectory."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    rng = np.random.default_rng(21)
+    D = 32
+    layers = []
+    for _ in range(2):
+        layers += [(5, rand_params(rng, 5, D, np.float64)), (3, rand_params(rng, 3, D, np.float64))]
+    X = rng.standard_normal((D, 3001))
+    ref = enf.optimize_whitening(colmajor_cuda(X), make_flow(enf, layers), enf.ADAGrad(), nbatches=3, nepochs=2)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict((r, (th, h)) for r, th, h in (q.get(timeout=110) for _ in procs))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    th_ref = ref.optimizer_state.theta.cpu().numpy()
+    for r in (0, 1):
+        th, h = out[r]
+        assert np.allclose(th, th_ref, rtol=1e-10, atol=1e-12)
+        assert np.allclose(h, ref.negll_history, rtol=1e-10)
