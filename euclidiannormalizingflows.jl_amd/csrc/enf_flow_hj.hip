@@ -386,7 +386,9 @@ __device__ __forceinline__ void hj_pair_exact(float (&x)[U][R], float (&acc)[U],
   prm.load(r);
 }
 
-template <int D, int R, int U, int LM>
+// NP > 0: the pair loop unrolled for exactly NP pairs (no loop-carried register copies between
+// the pair loop and the tile loop); NP == 0: runtime pair count a.n.
+template <int D, int R, int U, int LM, int NP>
 struct HJBody {
   const HJArgs& a;
   const float* rec;  // this lane's record group
@@ -408,7 +410,12 @@ struct HJBody {
     prm.load(r);
     // branch-free pair loop; a tile with a product overflow (|z| large, Inf, NaN) is redone below
     float m = 0.f;
-    for (int p = 0; p < n; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ>(x, acc, r, prm));
+    if constexpr (NP > 0) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ>(x, acc, r, prm));
+    } else {
+      for (int p = 0; p < n; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ>(x, acc, r, prm));
+    }
     // column-uniform: the exact form's dot products read every lane of a column (DPP)
     m = group_max<HJLay<D, R, U>::G>(m);
     if (__builtin_expect(!(m <= FLT_MAX), 0)) {
@@ -466,7 +473,7 @@ __device__ __forceinline__ void hj_stream(const HJArgs& a, Body& body) {
   }
 }
 
-template <int D, int R, int U, int LM, int OCC, int DBG>
+template <int D, int R, int U, int LM, int OCC, int DBG, int NP>
 __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   const int n = a.n;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -476,7 +483,7 @@ __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   float* rec = reinterpret_cast<float*>(smem + kHjHeader);
   build_hj_program<D, R>(a, n, rec, scr, ctotp);
   constexpr int G = HJLay<D, R, U>::G;
-  HJBody<D, R, U, LM> body{a, rec + ((threadIdx.x & 63) % G) * 4 * R, *ctotp, stage, n};
+  HJBody<D, R, U, LM, NP> body{a, rec + ((threadIdx.x & 63) % G) * 4 * R, *ctotp, stage, n};
   hj_stream<D, R, U, LM, DBG>(a, body);
 }
 
@@ -489,14 +496,14 @@ int hj_program_pairs(const FlowArgs& a) {
   return a.nsteps / 2;
 }
 
-template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0>
+template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, int NP = 0>
 static hipError_t launch_hj(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
   const size_t lds = hj_lds_bytes(D, h.n);
-  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG>);
+  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, NP>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)HJLay<D, R, U>::TC * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG>), dim3((unsigned)blocks), dim3(256), lds, st, h);
+  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, NP>), dim3((unsigned)blocks), dim3(256), lds, st, h);
   return hipGetLastError();
 }
 
