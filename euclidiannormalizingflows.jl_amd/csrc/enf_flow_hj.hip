@@ -473,7 +473,79 @@ __device__ __forceinline__ void hj_stream(const HJArgs& a, Body& body) {
   }
 }
 
-template <int D, int R, int U, int LM, int OCC, int DBG, int NP>
+// The same loop with the next tile staged in LDS by the load-to-LDS DMA (global_load_lds_dwordx4)
+// instead of a second register tile: per wave a 64 x 16 B x U*NF image in the load order, read
+// back with one ds_read_b128 per fragment. The DMA of tile t+1 is issued after tile t has been
+// read into registers (lgkmcnt(0)), and waited for with a counted vmcnt that leaves tile t's
+// stores in flight (they are the only vector-memory operations issued after it).
+typedef __attribute__((address_space(3))) void* lds_vptr_t;
+typedef __attribute__((address_space(1))) void* gbl_vptr_t;
+// s_waitcnt immediates, gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]
+constexpr int waitcnt_vm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
+constexpr int kWaitLgkm0 = 15 | (7 << 4) | (0 << 8) | (3 << 14);
+
+template <int D, int R, int U>
+__device__ __forceinline__ void hj_glds(const HJArgs& a, int64_t col0, float* xbuf) {
+  using L = HJLay<D, R, U>;
+  const int lane = threadIdx.x & 63;
+  const float* X = (const float*)a.X;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int h = 0; h < L::NF; ++h)
+      __builtin_amdgcn_global_load_lds((gbl_vptr_t)(X + L::col(col0, u, lane) * D + L::row(h, lane)),
+                                       (lds_vptr_t)(xbuf + (u * L::NF + h) * 256), 16, 0, 0);
+}
+
+template <int D, int R, int U>
+__device__ __forceinline__ void hj_lds_tile(const float* xbuf, float (&x)[U][R]) {
+  constexpr int NF = R / 4;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int h = 0; h < NF; ++h) {
+      const u32x4 v4 = reinterpret_cast<const u32x4*>(xbuf + (u * NF + h) * 256)[lane];
+      __builtin_memcpy(&x[u][4 * h], &v4, 16);
+    }
+}
+
+template <int D, int R, int U, int LM, typename Body>
+__device__ __forceinline__ void hj_stream_lds(const HJArgs& a, Body& body, float* xbuf) {
+  using L = HJLay<D, R, U>;
+  constexpr int64_t CT = L::TC;
+  constexpr int NST = U * L::NF + (LM > 0 ? L::NLS : 0);  // vector-memory ops a tile issues after the DMA
+  const int64_t ntiles_full = a.N / CT;
+  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) +
+                          __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  float x[U][R], old[L::NLS];
+  int64_t t = wave_id;
+  if (t < ntiles_full) {
+    hj_glds<D, R, U>(a, t * CT, xbuf);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    for (;;) {
+      hj_lds_tile<D, R, U>(xbuf, x);
+      __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // the image is in registers before it is refilled
+      const int64_t tn = t + nwaves;
+      if (tn < ntiles_full) hj_glds<D, R, U>(a, tn * CT, xbuf);
+      hj_load_old<D, R, U, LM>(a, t * CT, old, false);
+      body.template tile<false, 0>(t * CT, x, old);
+      if (tn >= ntiles_full) break;
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(NST));
+      t = tn;
+    }
+  }
+  if (ntiles_full * CT < a.N && wave_id == ntiles_full % nwaves) {
+    const int64_t c0 = ntiles_full * CT;
+    hj_load<D, R, U, true, 0>(a, c0, x);
+    hj_load_old<D, R, U, LM>(a, c0, old, true);
+    body.template tile<true, 0>(c0, x, old);
+  }
+}
+
+// GLDS: stage the next tile through LDS (hj_stream_lds) instead of a second register tile.
+template <int D, int R, int U, int LM, int OCC, int DBG, int NP, int GLDS = 0>
 __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   const int n = a.n;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -484,7 +556,12 @@ __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   build_hj_program<D, R>(a, n, rec, scr, ctotp);
   constexpr int G = HJLay<D, R, U>::G;
   HJBody<D, R, U, LM, NP> body{a, rec + ((threadIdx.x & 63) % G) * 4 * R, *ctotp, stage, n};
-  hj_stream<D, R, U, LM, DBG>(a, body);
+  if constexpr (GLDS && DBG == 0) {
+    float* xbuf = rec + (size_t)(n + 1) * 4 * D + (threadIdx.x >> 6) * (U * R * 64);
+    hj_stream_lds<D, R, U, LM>(a, body, xbuf);
+  } else {
+    hj_stream<D, R, U, LM, DBG>(a, body);
+  }
 }
 
 int hj_program_pairs(const FlowArgs& a) {
@@ -496,14 +573,15 @@ int hj_program_pairs(const FlowArgs& a) {
   return a.nsteps / 2;
 }
 
-template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, int NP = 0>
+template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, int NP = 0, int GLDS = 0>
 static hipError_t launch_hj(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
-  const size_t lds = hj_lds_bytes(D, h.n);
-  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, NP>);
+  const size_t lds = hj_lds_bytes(D, h.n) + (GLDS ? (size_t)4 * U * R * 64 * sizeof(float) : 0);
+  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, NP, GLDS>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)HJLay<D, R, U>::TC * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, NP>), dim3((unsigned)blocks), dim3(256), lds, st, h);
+  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, NP, GLDS>), dim3((unsigned)blocks), dim3(256), lds, st,
+                     h);
   return hipGetLastError();
 }
 
@@ -520,6 +598,8 @@ static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, c
       if (r == 4) return u2 ? launch_hj<32, 4, 8, 1>(a, st, dev) : launch_hj<32, 4, 4, 1>(a, st, dev);
       if (r == 16) return launch_hj<32, 16, 1, 1>(a, st, dev);
       if (u2) return launch_hj<32, 8, 4, 1>(a, st, dev);
+      static const int glds = env_int("ENF_HJ_GLDS", 0);
+      if (glds) return launch_hj<32, 8, 2, 1, 1, 0, 0, 1>(a, st, dev);
     }
     return launch_hj<32, 8, 2, LM>(a, st, dev);
   }
