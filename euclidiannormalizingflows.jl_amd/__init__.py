@@ -19,6 +19,7 @@ from .trafos import (  # noqa: F401
     compose,
     inverse,
     leaves,
+    stream_with_logabsdet_jacobian,
     with_logabsdet_jacobian,
 )
 
@@ -37,6 +38,6 @@ __all__ = [
     "ADAGrad", "FlowState", "WhiteningResult", "allreduce_sum_", "minibatch_plan", "mvnormal_negll_trafo", "mvnormal_negll_trafograd",
     "optimize_whitening",
     "ScaleShiftTrafo", "CenterStretch", "CenterContract", "JohnsonTrafo", "JohnsonTrafoInv",
-    "HouseholderTrafo", "ComposedFunction", "compose", "inverse", "with_logabsdet_jacobian",
+    "HouseholderTrafo", "ComposedFunction", "compose", "inverse", "stream_with_logabsdet_jacobian", "with_logabsdet_jacobian",
     "leaves", "Trafo", "MethodError", "DimensionMismatch", "EnfError", "version",
 ]

@@ -20,7 +20,7 @@ UNIQUE_ID_BYTES = 128
 # every symbol include/enf.h declares (checked by tests/test_capi.py)
 EXPORTED = (
     "enf_version", "enf_last_error", "enf_device_count", "enf_set_device", "enf_get_device",
-    "enf_malloc", "enf_free", "enf_memcpy", "enf_stream_synchronize", "enf_flow_apply",
+    "enf_malloc", "enf_free", "enf_memcpy", "enf_stream_synchronize", "enf_flow_apply", "enf_flow_apply_host",
     "enf_flow_param_count", "enf_flow_negll_grad_workspace", "enf_flow_negll_grad",
     "enf_adagrad_step", "enf_householder_normalize", "enf_householder_normalize_strided", "enf_comm_unique_id", "enf_comm_init",
     "enf_comm_destroy", "enf_allreduce_sum",
@@ -56,6 +56,8 @@ _SIGS = {
     "enf_stream_synchronize": (ctypes.c_int, [_vp]),
     "enf_flow_apply": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i32,
                                       ctypes.POINTER(Layer), _i32, _vp]),
+    "enf_flow_apply_host": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i32,
+                                           ctypes.POINTER(Layer), _i32, _i64, _vp]),
     "enf_flow_param_count": (ctypes.c_int, [_i64, ctypes.POINTER(Layer), _i32, ctypes.POINTER(_i64)]),
     "enf_flow_negll_grad_workspace": (ctypes.c_int, [ctypes.c_int, _i64, _i64, ctypes.POINTER(Layer), _i32,
                                                      ctypes.POINTER(_sz)]),

@@ -269,6 +269,123 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
   ENF_CATCH
 }
 
+// ------------------------------------------------------------------- host-resident batches ----
+namespace {
+
+// Page-lock a host range for the duration of a call unless it already is (hipHostRegister makes
+// the async copies true DMA and lets them overlap the kernels).
+struct HostPin {
+  void* p = nullptr;
+  bool mine = false;
+  hipError_t pin(void* ptr, size_t bytes) {
+    hipPointerAttribute_t at;
+    std::memset(&at, 0, sizeof at);
+    if (hipPointerGetAttributes(&at, ptr) == hipSuccess && at.type != hipMemoryTypeUnregistered) return hipSuccess;
+    (void)hipGetLastError();  // clear the "not registered" status
+    hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
+    if (e == hipSuccess) {
+      p = ptr;
+      mine = true;
+    }
+    return e;
+  }
+  ~HostPin() {
+    if (mine) (void)hipHostUnregister(p);
+  }
+};
+
+struct Ring {
+  static constexpr int kSlots = 3;
+  void* buf[kSlots] = {};
+  hipEvent_t h2d[kSlots] = {}, comp[kSlots] = {}, d2h[kSlots] = {};
+  hipStream_t up = nullptr, down = nullptr;
+  ~Ring() {
+    for (int s = 0; s < kSlots; ++s) {
+      if (buf[s]) (void)hipFree(buf[s]);
+      if (h2d[s]) (void)hipEventDestroy(h2d[s]);
+      if (comp[s]) (void)hipEventDestroy(comp[s]);
+      if (d2h[s]) (void)hipEventDestroy(d2h[s]);
+    }
+    if (up) (void)hipStreamDestroy(up);
+    if (down) (void)hipStreamDestroy(down);
+  }
+};
+
+}  // namespace
+
+enf_status enf_flow_apply_host(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx, void* Y,
+                               int64_t ldy, void* ladj, int32_t accumulate_ladj, const enf_layer* layers,
+                               int32_t nlayers, int64_t chunk_cols, void* hip_stream) {
+  ENF_TRY
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "dtype must be ENF_F32 or ENF_F64");
+  if (D < 1 || N < 0) return fail(ENF_ERR_INVALID, "D must be >= 1 and N >= 0");
+  if (ldx < D || ldy < D) return fail(ENF_ERR_INVALID, "leading dimension < D");
+  if (chunk_cols < 0) return fail(ENF_ERR_INVALID, "chunk_cols < 0");
+  if (N == 0) return ENF_OK;
+  if (!X || !Y) return fail(ENF_ERR_INVALID, "X or Y is NULL");
+  if (X == Y && ldx != ldy) return fail(ENF_ERR_INVALID, "in-place call (X == Y) needs ldx == ldy");
+  const size_t elem = dtype == ENF_F64 ? 8 : 4;
+  int64_t C = chunk_cols > 0 ? chunk_cols : ((int64_t)256 << 20) / (int64_t)((D + 1) * elem);  // ~256 MB slots
+  if (C > N) C = N;
+  hipStream_t st = (hipStream_t)hip_stream;
+  // host ranges (the last column only spans D values)
+  const size_t xb = ((size_t)(N - 1) * ldx + D) * elem, yb = ((size_t)(N - 1) * ldy + D) * elem;
+  HostPin px, py, pl;
+  hipError_t e = px.pin(const_cast<void*>(X), xb);
+  if (e == hipSuccess && Y != X) e = py.pin(Y, yb);
+  if (e == hipSuccess && ladj) e = pl.pin(ladj, (size_t)N * elem);
+  if (e != hipSuccess) return hip_fail(e, "hipHostRegister");
+  Ring r;
+  const size_t slot_bytes = ((size_t)D * C + (size_t)C) * elem;
+  for (int s = 0; s < Ring::kSlots; ++s) {
+    if ((e = hipMalloc(&r.buf[s], slot_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc (ingest ring)");
+    if ((e = hipEventCreateWithFlags(&r.h2d[s], hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&r.comp[s], hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&r.d2h[s], hipEventDisableTiming)) != hipSuccess)
+      return hip_fail(e, "hipEventCreate");
+  }
+  if ((e = hipStreamCreateWithFlags(&r.up, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipStreamCreateWithFlags(&r.down, hipStreamNonBlocking)) != hipSuccess)
+    return hip_fail(e, "hipStreamCreate");
+  // the ring starts after everything already queued on the caller's stream
+  if ((e = hipEventRecord(r.comp[0], st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+  if ((e = hipStreamWaitEvent(r.up, r.comp[0], 0)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
+  const char* Xc = (const char*)X;
+  char* Yc = (char*)Y;
+  char* Lc = (char*)ladj;
+  int64_t i = 0;
+  for (int64_t c0 = 0; c0 < N; c0 += C, ++i) {
+    const int s = (int)(i % Ring::kSlots);
+    const int64_t cols = N - c0 < C ? N - c0 : C;
+    char* dX = (char*)r.buf[s];
+    char* dL = dX + (size_t)D * C * elem;
+    // slot reuse: wait until its previous results have left the device
+    if (i >= Ring::kSlots && (e = hipStreamWaitEvent(r.up, r.d2h[s], 0)) != hipSuccess)
+      return hip_fail(e, "hipStreamWaitEvent");
+    e = hipMemcpy2DAsync(dX, D * elem, Xc + (size_t)c0 * ldx * elem, ldx * elem, D * elem, cols,
+                         hipMemcpyHostToDevice, r.up);
+    if (e == hipSuccess && ladj && accumulate_ladj)
+      e = hipMemcpyAsync(dL, Lc + (size_t)c0 * elem, cols * elem, hipMemcpyHostToDevice, r.up);
+    if (e == hipSuccess) e = hipEventRecord(r.h2d[s], r.up);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st, r.h2d[s], 0);
+    if (e != hipSuccess) return hip_fail(e, "ingest H2D");
+    enf_status fs = enf_flow_apply(dtype, D, cols, dX, D, dX, D, ladj ? dL : nullptr, accumulate_ladj, layers,
+                                   nlayers, st);
+    if (fs != ENF_OK) return fs;
+    if ((e = hipEventRecord(r.comp[s], st)) != hipSuccess || (e = hipStreamWaitEvent(r.down, r.comp[s], 0)) != hipSuccess)
+      return hip_fail(e, "ingest compute event");
+    e = hipMemcpy2DAsync(Yc + (size_t)c0 * ldy * elem, ldy * elem, dX, D * elem, D * elem, cols,
+                         hipMemcpyDeviceToHost, r.down);
+    if (e == hipSuccess && ladj) e = hipMemcpyAsync(Lc + (size_t)c0 * elem, dL, cols * elem, hipMemcpyDeviceToHost, r.down);
+    if (e == hipSuccess) e = hipEventRecord(r.d2h[s], r.down);
+    if (e != hipSuccess) return hip_fail(e, "ingest D2H");
+  }
+  // synchronous: the results are in host memory (and the ring can be released) on return
+  if ((e = hipStreamSynchronize(r.down)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  return ENF_OK;
+  ENF_CATCH
+}
+
 enf_status enf_flow_param_count(int64_t D, const enf_layer* layers, int32_t nlayers, int64_t* count) {
   ENF_TRY
   if (!count) return fail(ENF_ERR_INVALID, "count is NULL");

@@ -469,3 +469,49 @@ def _apply(f, X, want_ladj: bool):
 def with_logabsdet_jacobian(f, X):
     """ChangesOfVariables.with_logabsdet_jacobian(f, X) -> (Y, ladj), one fused launch per dtype run."""
     return _apply(f, X, want_ladj=True)
+
+
+def stream_with_logabsdet_jacobian(f, X: np.ndarray, chunk_cols: int = 0, out=None, want_ladj: bool = True,
+                                   device=None):
+    """with_logabsdet_jacobian for a HOST-resident batch larger than (or not wanted in) device memory
+    (SURVEY.md §8(f) item 2): X is a column-major (D, N) numpy array (np.asfortranarray; sample j =
+    the contiguous column X[:, j], Julia's flatview layout); column chunks stream through the device
+    (enf_flow_apply_host: copy-in, fused flow and copy-out overlap). Returns (Y, ladj) as numpy
+    arrays (ladj shape (1, N)); ``out`` may be X itself for an in-place transform. The flow's
+    parameters must share X's dtype (no mixed-precision promotion on this path)."""
+    X = np.asarray(X)
+    if X.ndim != 2 or not X.flags.f_contiguous:
+        raise DimensionMismatch("stream_with_logabsdet_jacobian needs a column-major (D, N) array")
+    dt = torch.float64 if X.dtype == np.float64 else torch.float32 if X.dtype == np.float32 else None
+    if dt is None:
+        raise MethodError("X must be float32 or float64")
+    ts = leaves(f)
+    if want_ladj:
+        for t in ts:
+            t._check_ladj_signature(False)
+    if _promote(dt, *[_kind(p) for t in ts for p in t.params()]) != dt:
+        raise MethodError("stream_with_logabsdet_jacobian: parameters would promote X's dtype")
+    if not torch.cuda.is_available():
+        raise RuntimeError("enf needs a ROCm GPU (torch.cuda.is_available() is False); no CPU path exists")
+    D, N = X.shape
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    Y = np.empty_like(X, order="F") if out is None else out
+    if Y.shape != X.shape or Y.dtype != X.dtype or not Y.flags.f_contiguous:
+        raise DimensionMismatch("out must be a column-major array like X")
+    L = np.empty((1, N), dtype=X.dtype) if want_ladj else None
+    keep = []
+    arr = (_lib.Layer * max(1, len(ts)))()
+    for i, t in enumerate(ts):
+        ps = t._device_params(dev, dt, D)
+        keep.extend(ps)
+        arr[i].op = t.OP
+        arr[i].k = t._k()
+        for q, p in enumerate(ps):
+            arr[i].p[q] = p.data_ptr()
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(_lib.lib().enf_flow_apply_host(
+            _lib.ENF_F64 if dt == torch.float64 else _lib.ENF_F32, D, N, X.ctypes.data, D, Y.ctypes.data, D,
+            L.ctypes.data if L is not None else None, 0, arr, len(ts), int(chunk_cols), stream))
+    del keep
+    return Y, L

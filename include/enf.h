@@ -96,6 +96,19 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
                           void* Y, int64_t ldy, void* ladj, int32_t accumulate_ladj,
                           const enf_layer* layers, int32_t nlayers, void* hip_stream);
 
+/* Host-resident batch (optimize_whitening's VectorOfSimilarVectors /
+ * flatview batches, src/optimize_whitening.jl:26,38, and N beyond device memory): the same
+ * computation as enf_flow_apply with X, Y and ladj in HOST memory. Column chunks of chunk_cols
+ * samples (0: ~256 MB per chunk) stream through a 3-slot device ring: host->device copy of chunk
+ * i+1, the fused flow on chunk i (on hip_stream) and device->host copy of chunk i-1 overlap.
+ * Pageable host ranges are page-locked for the duration of the call. Layer parameters are device
+ * pointers as in enf_flow_apply. Synchronous: returns when Y and ladj are in host memory.
+ * Y may alias X exactly (ldx == ldy). */
+enf_status enf_flow_apply_host(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
+                               void* Y, int64_t ldy, void* ladj, int32_t accumulate_ladj,
+                               const enf_layer* layers, int32_t nlayers, int64_t chunk_cols,
+                               void* hip_stream);
+
 /* ---------------------------------------------------------------- training (config 5) -- */
 /* Number of gradient entries of the flow: sum over layers of D*nparams (Householder D*k).
  * The gradient buffer layout is layer by layer, parameter by parameter, each a length-D vector

@@ -339,3 +339,30 @@ def test_hj_program_exact_redo_edge_values(enf, gpu, oracle, D):
     assert ladj_err(L[finl], Lr[finl]) < 1e-5
     good = np.setdiff1d(np.arange(N), bad)
     check_vs_oracle(oracle, layers, np.asfortranarray(X[:, good]), Y[:, good], L[good], np.float32, what="redo")
+
+
+@pytest.mark.parametrize("chunk", [0, 1000, 4097, 70_001])
+def test_host_streaming_equals_device_path(enf, gpu, chunk):
+    """enf_flow_apply_host (host-resident batch, chunked through a device ring) gives exactly the
+    device path's results: the same kernels per column, any chunking; in place on the host too."""
+    rng = np.random.default_rng(31)
+    D, N = 32, 200_003
+    layers = _hj_layers(rng, D, 4)
+    X = np.asfortranarray(rng.standard_normal((D, N)).astype(np.float32))
+    f = make_flow(enf, layers)
+    Yd, Ld = enf.with_logabsdet_jacobian(f, colmajor_cuda(X))
+    Yh, Lh = enf.stream_with_logabsdet_jacobian(f, X, chunk_cols=chunk)
+    assert np.array_equal(Yh, to_np(Yd)) and np.array_equal(Lh, to_np(Ld))
+    Xi = X.copy(order="F")
+    Yi, Li = enf.stream_with_logabsdet_jacobian(f, Xi, chunk_cols=chunk, out=Xi)
+    assert Yi is Xi and np.array_equal(Xi, Yh) and np.array_equal(Li, Lh)
+
+
+def test_host_streaming_fp64_mixed_ops(enf, gpu, oracle):
+    """Host streaming on the interpreter path (fp64, every op), against the oracle."""
+    rng = np.random.default_rng(32)
+    D, N = 5, 30_011
+    layers = [(op, rand_params(rng, op, D, np.float64, K=2 if op == 5 else 1)) for op in (0, 5, 2, 3, 1, 4, 5, 3)]
+    X = np.asfortranarray(rng.standard_normal((D, N)))
+    Y, L = enf.stream_with_logabsdet_jacobian(make_flow(enf, layers), X, chunk_cols=7001)
+    check_vs_oracle(oracle, layers, X, Y, L, np.float64, what="host streaming fp64")
