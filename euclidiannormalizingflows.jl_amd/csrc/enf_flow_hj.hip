@@ -599,6 +599,7 @@ static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, c
       if (r == 16) return launch_hj<32, 16, 1, 1>(a, st, dev);
       if (u2) return launch_hj<32, 8, 4, 1>(a, st, dev);
       static const int glds = env_int("ENF_HJ_GLDS", 0);
+      if (glds == 2) return launch_hj<32, 8, 2, 1, 5, 0, 0, 1>(a, st, dev);
       if (glds) return launch_hj<32, 8, 2, 1, 1, 0, 0, 1>(a, st, dev);
     }
     return launch_hj<32, 8, 2, LM>(a, st, dev);
