@@ -16,16 +16,19 @@
 //                                                                 Q = -xi/lambda, L := x)
 // and only the last pair forms y = gamma_n + delta'_n L. Per element and pair that is one FMA for
 // the dot product, two for z, then q = 1 + z^2, sqrt, |z| + s, log2, the sign (v_bfi), and for the
-// ladj -1/2 log2 of the product of a fragment's four q (one log per 4 elements). The records are
-// derived in double in each block's prologue from the raw device parameter vectors.
+// ladj -1/2 log2 of the product of the q of a lane's 8 rows of one column (one log per 8 elements).
+// The records are derived in double in each block's prologue from the raw device parameter vectors.
 //
-// Fast-path guard: the product of a fragment's q stays finite for |z| < 2^16; a larger (or infinite)
-// |z| makes it +Inf, and then the wave redoes the layer with the elementwise exact-range form
-// (johnson_fwd_f32_slow in enf_frag.h: asinh finite up to FLT_MAX, ladj -Inf where the reference's
-// fp32 1 + z^2 overflows). NaN propagates through the fast formulas as through the reference's.
+// Fast-path guard: the product of 8 q stays finite unless |z| is large (about 2^8 on every row),
+// infinite or NaN; then the lanes of that column redo the whole program from X with the exact-range
+// elementwise form (johnson_fwd_f32_slow in enf_frag.h: asinh finite up to FLT_MAX, ladj -Inf where
+// the reference's fp32 1 + z^2 overflows).
 //
 // Loop structure: the pair loop is a runtime loop over one compact body (small code: the I-cache
-// holds it), with the next pair's four parameter vectors read from LDS while the current one runs.
+// holds it), with the next pair's parameter vectors read from LDS while the current one runs. Measured
+// alternatives that did not pay (profiles/r01_ab_*.txt): the pair loop unrolled for a compile-time
+// pair count, the next tile staged through LDS by global_load_lds (ENF_HJ_GLDS=1), 5 waves per SIMD
+// (spills), 4 or 16 rows per lane (ENF_HJ_R).
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -599,7 +602,6 @@ static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, c
       if (r == 16) return launch_hj<32, 16, 1, 1>(a, st, dev);
       if (u2) return launch_hj<32, 8, 4, 1>(a, st, dev);
       static const int glds = env_int("ENF_HJ_GLDS", 0);
-      if (glds == 2) return launch_hj<32, 8, 2, 1, 5, 0, 0, 1>(a, st, dev);
       if (glds) return launch_hj<32, 8, 2, 1, 1, 0, 0, 1>(a, st, dev);
     }
     return launch_hj<32, 8, 2, LM>(a, st, dev);
