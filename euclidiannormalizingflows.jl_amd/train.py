@@ -157,6 +157,17 @@ def _workspace(state: FlowState, N: int):
     return torch.empty(max(1, nb.value // 8), dtype=torch.float64, device=state.device)
 
 
+def _scaleshift_a_segments(state: FlowState):
+    """(segment index, trafo) of every ScaleShiftTrafo's `a` vector in theta."""
+    out, seg = [], 0
+    for t in state.trafos:
+        for name in t.FIELDS:
+            if isinstance(t, ScaleShiftTrafo) and name == "a":
+                out.append((seg, t))
+            seg += 1
+    return out
+
+
 def _scaleshift_ladj_const(state: FlowState) -> float:
     c, seg = 0.0, 0
     th = None
@@ -254,8 +265,11 @@ def allreduce_sum_(buf: torch.Tensor, world: int, group=None) -> torch.Tensor:
 
 def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None, nbatches: int = 100,
                        nepochs: int = 100, optstate: Optional[FlowState] = None,
-                       negll_history: Optional[List[float]] = None, process_group=None) -> WhiteningResult:
-    """src/optimize_whitening.jl:25-45 on the device (see module docstring)."""
+                       negll_history: Optional[List[float]] = None, process_group=None,
+                       similar_fill_quirk: bool = False) -> WhiteningResult:
+    """src/optimize_whitening.jl:25-45 on the device (see module docstring). similar_fill_quirk=True
+    records the negll the reference records under Zygote (ScaleShiftTrafo's primal ladj taken as 0,
+    src/abstract_trafo.jl:30-33: + sum log|a| per sample); the updates are the same either way."""
     import torch.distributed as dist
 
     optimizer = optimizer or ADAGrad()
@@ -280,6 +294,7 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
     hist = torch.zeros(nepochs * len(plan), dtype=torch.float64, device=M.device)
     hbatches = householder_batches(state)
     segs = trainable_runs(state)
+    ss_a = [(int(state.offsets[i]), int(state.offsets[i + 1])) for i, _ in _scaleshift_a_segments(state)]
     step = 0
     with torch.cuda.device(M.device):
         stream = torch.cuda.current_stream(M.device).cuda_stream
@@ -293,6 +308,9 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
                                                      ws.numel() * 8, stream))
                 allreduce_sum_(out, world, process_group)
                 hist[step:step + 1].copy_(out[0:1] / B)
+                if similar_fill_quirk:
+                    for s0, s1 in ss_a:
+                        hist[step:step + 1] += torch.log(state.theta[s0:s1].abs()).sum()
                 g = out[1:]
                 for s0, s1 in segs:
                     _lib.check(L.enf_adagrad_step(dt, s1 - s0, state.theta[s0:].data_ptr(), state.acc[s0:].data_ptr(),

@@ -273,3 +273,20 @@ def test_optimize_whitening_two_ranks_equals_one(enf, gpu):
         th, h = out[r]
         assert np.allclose(th, th_ref, rtol=1e-10, atol=1e-12)
         assert np.allclose(h, ref.negll_history, rtol=1e-10)
+
+
+def test_optimize_whitening_similar_fill_quirk(enf, gpu):
+    """similar_fill_quirk=True shifts every recorded negll by the ScaleShift term sum log|a| of the
+    parameters at that step (the reference's Zygote-recorded value); the trajectory is unchanged."""
+    rng = np.random.default_rng(12)
+    D = 4
+    layers = [(0, rand_params(rng, 0, D, np.float64)), (5, rand_params(rng, 5, D, np.float64)),
+              (3, rand_params(rng, 3, D, np.float64))]
+    X = rng.standard_normal((D, 900))
+    f = make_flow(enf, layers)
+    a = enf.optimize_whitening(colmajor_cuda(X), f, enf.ADAGrad(), nbatches=3, nepochs=1)
+    b = enf.optimize_whitening(colmajor_cuda(X), f, enf.ADAGrad(), nbatches=3, nepochs=1, similar_fill_quirk=True)
+    assert np.array_equal(a.optimizer_state.theta.cpu().numpy(), b.optimizer_state.theta.cpu().numpy())
+    n0, _ = enf.mvnormal_negll_trafograd(f, colmajor_cuda(X[:, :300]), similar_fill_quirk=True)
+    assert abs(b.negll_history[0] - n0) < 1e-12 * abs(n0)
+    assert abs(b.negll_history[0] - a.negll_history[0] - np.sum(np.log(np.abs(layers[0][1][0])))) < 1e-12
