@@ -489,7 +489,9 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
   int64_t blocks = (tiles + 3) / 4;
   DeviceInfo dev;
   if (current_device_info(&dev) != ENF_OK) return ENF_ERR_HIP;
-  const int64_t cap = (int64_t)dev.num_cu * 2;
+  // blocks per CU (2: what the fused kernel's LDS lets stay resident; measured best at config 5)
+  static const int per_cu = env_int("ENF_GRAD_BPC", 2);
+  const int64_t cap = (int64_t)dev.num_cu * per_cu;
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   P.blocks = (int)blocks;

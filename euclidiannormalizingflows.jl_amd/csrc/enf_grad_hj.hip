@@ -32,15 +32,14 @@ namespace enf {
 
 namespace {
 
-constexpr int kU = 2;  // fragments (columns) per lane per tile
 constexpr int kNP = 8;  // records per pair: vh, gamma, delta*ln2, 1/lambda, -xi/lambda, lambda, xi, delta
 
-template <int D>
+template <int D, int KU>
 struct GL {
   static constexpr int V = 4;
   static constexpr int G = D / V;            // lanes per column
   static constexpr int S = 64 / G;           // column slots per wave instruction
-  static constexpr int TC = S * kU;          // columns per wave tile
+  static constexpr int TC = S * KU;          // columns per wave tile
 };
 
 // cross-slot sum: lanes with equal lane % G hold the same rows
@@ -51,18 +50,18 @@ __device__ __forceinline__ float slot_sum(float v) {
   return v;
 }
 
-template <int D, bool TAIL>
+template <int D, int KU, bool TAIL>
 __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int lane, const float* __restrict__ rec,
                                           float* __restrict__ zst, float* __restrict__ dst, float* __restrict__ acc,
                                           double& lossp, int& nvalid, float ctot) {
-  using L = GL<D>;
+  using L = GL<D, KU>;
   constexpr int V = 4, G = L::G, S = L::S;
   const int grp = lane % G;
   const int n = a.n;
-  float x[kU][V];
-  float vm[kU];  // 1 for a valid column, 0 past N
+  float x[KU][V];
+  float vm[KU];  // 1 for a valid column, 0 past N
 #pragma unroll
-  for (int u = 0; u < kU; ++u) {
+  for (int u = 0; u < KU; ++u) {
     const int64_t c = col0 + (int64_t)u * S + lane / G;
     const float* src = a.X + c * D + V * grp;
     vm[u] = (!TAIL || c < a.N) ? 1.f : 0.f;
@@ -75,7 +74,7 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
     }
   }
   // ---- forward
-  float lad[kU] = {};
+  float lad[KU] = {};
   for (int p = 0; p < n; ++p) {
     const float* r = rec + (size_t)p * kNP * D + grp * kNP * V;
     float vh[V], gam[V], dl2[V], il[V], nxil[V];
@@ -84,27 +83,27 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
     lds_vec<float, V>(r + 2 * V, dl2);
     lds_vec<float, V>(r + 3 * V, il);
     lds_vec<float, V>(r + 4 * V, nxil);
-    float dot[kU];
+    float dot[KU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < KU; ++u) {
       float t = vh[0] * x[u][0];
 #pragma unroll
       for (int e = 1; e < V; ++e) t = fmaf(vh[e], x[u][e], t);
       dot[u] = group_sum<G>(t);
     }
-    float z[kU][V], q[kU][V];
+    float z[KU][V], q[KU][V];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < KU; ++u) {
 #pragma unroll
       for (int e = 0; e < V; ++e) {
         z[u][e] = fmaf(fmaf(-dot[u], vh[e], x[u][e]), il[e], nxil[e]);
         q[u][e] = fmaf(z[u][e], z[u][e], 1.f);
       }
-      dst[(p * kU + u) * 64 + lane] = dot[u];
-      *reinterpret_cast<u32x4*>(zst + ((size_t)(p * kU + u) * 64 + lane) * V) = *reinterpret_cast<const u32x4*>(&z[u][0]);
+      dst[(p * KU + u) * 64 + lane] = dot[u];
+      *reinterpret_cast<u32x4*>(zst + ((size_t)(p * KU + u) * 64 + lane) * V) = *reinterpret_cast<const u32x4*>(&z[u][0]);
     }
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < KU; ++u) {
 #pragma unroll
       for (int e = 0; e < V; ++e) {
         const float Lz = copysignf(hw_log2(fabsf(z[u][e]) + hw_sqrt(q[u][e])), z[u][e]);
@@ -115,7 +114,7 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
   }
   // ---- loss: sum_d (y^2 + log 2 pi)/2 - ladj, ladj = ctot + ln2 * lad (valid columns)
 #pragma unroll
-  for (int u = 0; u < kU; ++u) {
+  for (int u = 0; u < KU; ++u) {
     float t = 0.f;
 #pragma unroll
     for (int e = 0; e < V; ++e) t = fmaf(x[u][e], x[u][e], t);
@@ -127,9 +126,9 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
     }
   }
   // ---- backward, g = dS/dy = y
-  float g[kU][V];
+  float g[KU][V];
 #pragma unroll
-  for (int u = 0; u < kU; ++u)
+  for (int u = 0; u < KU; ++u)
 #pragma unroll
     for (int e = 0; e < V; ++e) g[u][e] = x[u][e] * vm[u];
   for (int p = n - 1; p >= 0; --p) {
@@ -141,12 +140,12 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
     lds_vec<float, V>(r + 6 * V, xi);
     lds_vec<float, V>(r + 7 * V, del);
     float aG[V] = {}, aD[V] = {}, aX[V] = {}, aL[V] = {}, aV[V] = {};
-    float gh[kU][V], u_[kU][V], dot1[kU];
+    float gh[KU][V], u_[KU][V], dot1[KU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < KU; ++u) {
       float z[V];
-      *reinterpret_cast<u32x4*>(&z[0]) = *reinterpret_cast<const u32x4*>(zst + ((size_t)(p * kU + u) * 64 + lane) * V);
-      dot1[u] = dst[(p * kU + u) * 64 + lane];
+      *reinterpret_cast<u32x4*>(&z[0]) = *reinterpret_cast<const u32x4*>(zst + ((size_t)(p * KU + u) * 64 + lane) * V);
+      dot1[u] = dst[(p * KU + u) * 64 + lane];
 #pragma unroll
       for (int e = 0; e < V; ++e) {
         const float q = fmaf(z[e], z[e], 1.f);
@@ -163,7 +162,7 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
       }
     }
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
+    for (int u = 0; u < KU; ++u) {
       float t = vh[0] * gh[u][0];
 #pragma unroll
       for (int e = 1; e < V; ++e) t = fmaf(vh[e], gh[u][e], t);
@@ -191,9 +190,11 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
   }
 }
 
-template <int D>
+// KU: fragments (columns) per lane per tile. 1 halves the LDS image of z per wave (more resident
+// blocks per CU) but doubles the per-tile flush of the gradient partials; 2 measured faster.
+template <int D, int KU>
 __global__ __launch_bounds__(256) void hj_grad_kernel(HJGradArgs a) {
-  using L = GL<D>;
+  using L = GL<D, KU>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = a.n;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -202,8 +203,8 @@ __global__ __launch_bounds__(256) void hj_grad_kernel(HJGradArgs a) {
   float* rec = reinterpret_cast<float*>(smem + 256);                  // n * kNP * D floats
   const size_t recb = (size_t)n * kNP * D * 4;
   const size_t accb = (size_t)n * 5 * D * 4;
-  const size_t zb = (size_t)n * kU * 64 * 16;
-  const size_t db = (size_t)n * kU * 64 * 4;
+  const size_t zb = (size_t)n * KU * 64 * 16;
+  const size_t db = (size_t)n * KU * 64 * 4;
   unsigned char* wbase = smem + 256 + recb + (size_t)wave * (accb + zb + db);
   float* acc = reinterpret_cast<float*>(wbase);
   float* zst = reinterpret_cast<float*>(wbase + accb);
@@ -254,8 +255,8 @@ __global__ __launch_bounds__(256) void hj_grad_kernel(HJGradArgs a) {
   const int64_t full = a.N / L::TC;
   const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wave);
   for (int64_t t = wave_id; t < ntiles; t += (int64_t)gridDim.x * 4) {
-    if (t < full) grad_tile<D, false>(a, t * L::TC, lane, rec, zst, dst, acc, lossp, nvalid, ctot);
-    else grad_tile<D, true>(a, t * L::TC, lane, rec, zst, dst, acc, lossp, nvalid, ctot);
+    if (t < full) grad_tile<D, KU, false>(a, t * L::TC, lane, rec, zst, dst, acc, lossp, nvalid, ctot);
+    else grad_tile<D, KU, true>(a, t * L::TC, lane, rec, zst, dst, acc, lossp, nvalid, ctot);
   }
   // block partial: loss, then the flow gradient (layer order, enf_flow_param_count layout)
   for (int m = 32; m >= 1; m >>= 1) {
@@ -291,9 +292,9 @@ __global__ __launch_bounds__(256) void hj_grad_kernel(HJGradArgs a) {
   }
 }
 
-template <int D>
+template <int D, int KU>
 size_t hj_grad_lds(int n) {
-  return 256 + (size_t)n * kNP * D * 4 + 4 * ((size_t)n * 5 * D * 4 + (size_t)n * kU * 64 * 16 + (size_t)n * kU * 64 * 4);
+  return 256 + (size_t)n * kNP * D * 4 + 4 * ((size_t)n * 5 * D * 4 + (size_t)n * KU * 64 * 16 + (size_t)n * KU * 64 * 4);
 }
 
 }  // namespace
@@ -333,14 +334,22 @@ hipError_t launch_hj_grad(int64_t D, int64_t N, const void* X, const enf_layer* 
     off += 4 * (int32_t)D;
   }
   if (off != nparams) return hipErrorInvalidValue;
-  const size_t lds = D == 32 ? hj_grad_lds<32>(a.n) : hj_grad_lds<64>(a.n);
-  const void* k = D == 32 ? (const void*)&hj_grad_kernel<32> : (const void*)&hj_grad_kernel<64>;
+  static const int ku = env_int("ENF_GRAD_U", 2) == 1 ? 1 : 2;  // 2: measured 72 vs 93 us at config 5
+  const size_t lds = D == 32 ? (ku == 1 ? hj_grad_lds<32, 1>(a.n) : hj_grad_lds<32, 2>(a.n))
+                             : (ku == 1 ? hj_grad_lds<64, 1>(a.n) : hj_grad_lds<64, 2>(a.n));
+  const void* k = D == 32 ? (ku == 1 ? (const void*)&hj_grad_kernel<32, 1> : (const void*)&hj_grad_kernel<32, 2>)
+                          : (ku == 1 ? (const void*)&hj_grad_kernel<64, 1> : (const void*)&hj_grad_kernel<64, 2>);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  if (D == 32) hipLaunchKernelGGL(hj_grad_kernel<32>, dim3(blocks), dim3(256), lds, st, a);
-  else hipLaunchKernelGGL(hj_grad_kernel<64>, dim3(blocks), dim3(256), lds, st, a);
+  if (D == 32) {
+    if (ku == 1) hipLaunchKernelGGL((hj_grad_kernel<32, 1>), dim3(blocks), dim3(256), lds, st, a);
+    else hipLaunchKernelGGL((hj_grad_kernel<32, 2>), dim3(blocks), dim3(256), lds, st, a);
+  } else {
+    if (ku == 1) hipLaunchKernelGGL((hj_grad_kernel<64, 1>), dim3(blocks), dim3(256), lds, st, a);
+    else hipLaunchKernelGGL((hj_grad_kernel<64, 2>), dim3(blocks), dim3(256), lds, st, a);
+  }
   return hipGetLastError();
 }
 
