@@ -208,17 +208,29 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
   if (ds != ENF_OK) return ds;
 
   // flatten into steps: one per transform, one per Householder reflection column
+  // (dense-Householder path: a chained HouseholderTrafo with k >= wy_min_k() reflections becomes
+  // OP_DENSE steps of <= D reflections each, col = first column | count << 16)
+  const bool frag = enf::frag_path(D, ldx, ldy, X, Y) && enf::frag_path(D, ldy, ldy, Y, Y);
+  bool wy = false;
+  if (enf::wy_supported(D, frag))
+    for (int32_t l = 0; l < nlayers; ++l)
+      if (layers[l].op == ENF_OP_HOUSEHOLDER && layers[l].k >= enf::wy_min_k()) wy = true;
   struct S { int32_t op, layer, col; };
   std::vector<S> steps;
   for (int32_t l = 0; l < nlayers; ++l) {
-    if (layers[l].op == ENF_OP_HOUSEHOLDER)
+    if (layers[l].op == ENF_OP_HOUSEHOLDER && wy && layers[l].k >= enf::wy_min_k()) {
+      for (int32_t c = 0; c < layers[l].k; c += (int32_t)D) {
+        const int32_t cnt = std::min<int32_t>((int32_t)D, layers[l].k - c);
+        steps.push_back({enf::OP_DENSE, l, c | (cnt << 16)});
+      }
+    } else if (layers[l].op == ENF_OP_HOUSEHOLDER) {
       for (int32_t c = 0; c < layers[l].k; ++c) steps.push_back({layers[l].op, l, c});
-    else
+    } else {
       steps.push_back({layers[l].op, l, 0});
+    }
   }
 
   // cut into launches bounded by the kernarg tables and the LDS parameter budget
-  const bool frag = enf::frag_path(D, ldx, ldy, X, Y) && enf::frag_path(D, ldy, ldy, Y, Y);
   size_t i = 0;
   bool first = true;
   while (i < steps.size()) {
@@ -227,6 +239,7 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
     a.D = (int32_t)D;
     a.N = N;
     a.frag = frag ? 1 : 0;
+    a.wy = wy ? 1 : 0;
     size_t recs = 0;
     int last_layer = -1;
     while (i < steps.size() && a.nsteps < enf::kMaxSteps) {
@@ -234,7 +247,7 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
       const size_t w = enf::record_elems(s.op, D, elem, frag) * elem;
       const bool new_layer = s.layer != last_layer;
       if (new_layer && a.nlayers >= enf::kMaxLayers) break;
-      if (recs + w > enf::kLdsParamBudget) {
+      if (recs + w > (wy ? enf::kLdsParamBudgetWY : enf::kLdsParamBudget)) {
         if (a.nsteps == 0)
           return fail(ENF_ERR_UNSUPPORTED, "D too large: one transform's parameter records exceed the LDS budget");
         break;

@@ -35,355 +35,9 @@
 #include "enf_internal.h"
 
 #include "enf_frag.h"
+#include "enf_steps.h"
 
 namespace enf {
-
-// ------------------------------------------------------------------------------------------
-// parameter records in LDS
-// ------------------------------------------------------------------------------------------
-// A step's record holds W(op) parameter values per row (enf_internal.h record_width):
-//  fp32                                              fp64
-//  HOUSEHOLDER  W=1 {v_d * sqrt(2/v'v)}              same
-//  SCALESHIFT   W=2 {a, b}                           same
-//  JOHNSON      W=4 {gamma, delta*ln2, xi, 1/lambda} {gamma, delta, xi, 1/lambda}
-//  JOHNSON_INV  W=4 {gamma, 1/delta, xi, lambda}     {gamma, 1/delta, xi, lambda}
-//  CENTER_*     W=8 {b*log2e, c, ln2/b, exp(b*a),    {a, b, c, 0, ...}
-//                    exp(2*b*a), b*a*log2e, a, b}
-// Layout: [group g][param q][element e] with RV elements per group; element (g, e) is row
-// g*RV + e (D >= RV) or e % D (D < RV). The fragment kernel uses RV = V = 16/sizeof(T), so a
-// lane reads each parameter of its V rows with ONE 16-byte LDS read; the generic kernel uses
-// RV = 1 (row-major records). Size: W * max(D, RV) values (enf_internal.h record_elems).
-template <typename T>
-__device__ __forceinline__ void param_values(int op, const LayerDesc& L, int col, int D, int row, double hscale,
-                                             T (&out)[8]) {
-  if (op == OP_HOUSEHOLDER) {
-    out[0] = (T)((double)((const T*)L.p[0])[(int64_t)col * D + row] * hscale);
-  } else if (op == OP_SCALESHIFT) {
-    out[0] = ((const T*)L.p[0])[row];
-    out[1] = ((const T*)L.p[1])[row];
-  } else if (op == OP_JOHNSON || op == OP_JOHNSON_INV) {
-    const T g = ((const T*)L.p[0])[row], de = ((const T*)L.p[1])[row];
-    const T xi = ((const T*)L.p[2])[row], la = ((const T*)L.p[3])[row];
-    out[0] = g;
-    out[2] = xi;
-    if constexpr (std::is_same_v<T, float>) {
-      if (op == OP_JOHNSON) {
-        out[1] = (float)((double)de * kLn2);
-        out[3] = (float)(1.0 / (double)la);
-      } else {
-        out[1] = (float)(1.0 / (double)de);
-        out[3] = la;
-      }
-    } else {  // reciprocals in the prologue: one multiply per element instead of a division
-      out[1] = op == OP_JOHNSON ? de : 1.0 / de;
-      out[3] = op == OP_JOHNSON ? 1.0 / la : la;
-    }
-  } else {  // CENTER_STRETCH / CENTER_CONTRACT
-    const T av = ((const T*)L.p[0])[row], bv = ((const T*)L.p[1])[row], cv = ((const T*)L.p[2])[row];
-    if constexpr (std::is_same_v<T, float>) {
-      const double b = bv, aa = av;
-      out[0] = (float)(b * kLog2e);
-      out[1] = cv;
-      out[2] = (float)(kLn2 / b);
-      out[3] = expf(bv * av);         // exp(b*a) in T, as the reference (center_stretch.jl:7)
-      out[4] = expf(2.0f * bv * av);  // exp(2*b*a)
-      out[5] = (float)(b * aa * kLog2e);
-      out[6] = av;  // raw a, b for the generic kernel
-      out[7] = bv;
-    } else {
-      out[0] = av;
-      out[1] = bv;
-      out[2] = cv;
-      for (int q = 3; q < 8; ++q) out[q] = 0.0;
-    }
-  }
-}
-
-// Block prologue: one wave per step. Pass 1 reduces over the D distinct rows (v'v for a
-// reflection; the constant ladj part sum log|delta/lambda|, sum log|a| in double); pass 2 writes
-// the records in the layout above. ctot = sum of the per-step constants (natural log).
-template <typename T, int DC, int RV>
-__device__ void build_program(const FlowArgs& a, T* __restrict__ rec, double* __restrict__ stepc,
-                              double* __restrict__ ctot) {
-  const int D = DC > 0 ? DC : a.D;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int nent = D > RV ? D : RV;  // record entries per parameter
-  for (int s = wave; s < a.nsteps; s += nw) {
-    const Step st = a.steps[s];
-    const LayerDesc& L = a.layers[st.layer];
-    const int W = record_width(st.op);
-    T* r = rec + st.off;
-    double part = 0.0;
-    for (int d = lane; d < D; d += 64) {
-      if (st.op == OP_HOUSEHOLDER) {
-        const double v = (double)((const T*)L.p[0])[(int64_t)st.col * D + d];
-        part += v * v;
-      } else if (st.op == OP_SCALESHIFT) {
-        part += log(fabs((double)((const T*)L.p[0])[d]));  // scale_shift_trafo.jl:22
-      } else if (st.op == OP_JOHNSON || st.op == OP_JOHNSON_INV) {
-        // log|delta/lambda| (johnson_trafo.jl:41,51); the inverse negates (johnson_trafo.jl:104)
-        const double c = log(fabs((double)((const T*)L.p[1])[d])) - log(fabs((double)((const T*)L.p[3])[d]));
-        part += st.op == OP_JOHNSON ? c : -c;
-      }
-    }
-    for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m);
-    // normalised reflection: H x = x - vh (vh'x), vh = v*sqrt(2/v'v) (householder_trafo.jl:9-10)
-    const double hscale = st.op == OP_HOUSEHOLDER ? sqrt(2.0 / part) : 0.0;
-    for (int i = lane; i < nent; i += 64) {
-      const int g = D >= RV ? i / RV : 0, e = i % RV;
-      const int row = D >= RV ? i : e % D;
-      T vals[8];
-      param_values<T>(st.op, L, st.col, D, row, hscale, vals);
-      for (int q = 0; q < W; ++q) r[(g * W + q) * RV + e] = vals[q];
-    }
-    if (lane == 0)
-      stepc[s] = (st.op == OP_HOUSEHOLDER || st.op == OP_CENTER_STRETCH || st.op == OP_CENTER_CONTRACT) ? 0.0 : part;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double c = 0.0;
-    for (int s = 0; s < a.nsteps; ++s) c += stepc[s];
-    *ctot = c;
-  }
-  __syncthreads();
-}
-
-
-// y = x - vh (vh'x), vh = v*sqrt(2/v'v): householder_trafo!(y, v, x) (householder_trafo.jl:8-11)
-template <typename T, int D, int U>
-__device__ __forceinline__ void step_householder(Tile<T, D, U>& x, const T* __restrict__ r) {
-  ENF_FRAG_CONSTS
-  T vh[V];
-  lds_vec<T, V>(r, vh);
-  T dot[U][CPF];
-  tile_dots<T, D, U>(x, vh, dot);
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int e = 0; e < V; ++e) x[u][e] = fma(-dot[u][e / SEG], vh[e], x[u][e]);
-}
-
-// fp32 Johnson layer from z (in x): y = gamma + delta*asinh(z), ladj += log|delta/lambda| -
-// log(1+z^2)/2 (the constant part is in ctot). zmax = max |z| over the tile.
-template <int D, int U, bool LADJ>
-__device__ __forceinline__ void johnson_from_z(Tile<float, D, U>& x, Acc<float, D, U>& acc,
-                                               const float (&pg)[4], const float (&pd)[4], float zmax) {
-  using T = float;
-  ENF_FRAG_CONSTS
-        if (__builtin_expect(!(zmax <= 32768.f), 0)) {
-#pragma unroll
-          for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int e = 0; e < V; ++e) {
-              const YL r2 = johnson_fwd_f32_slow(x[u][e], pg[e], pd[e]);
-              x[u][e] = r2.y;
-              if (LADJ) acc[u][e / SEG] += r2.l;
-            }
-        } else {
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            float prod[CPF];
-#pragma unroll
-            for (int c = 0; c < CPF; ++c) prod[c] = 1.0f;
-#pragma unroll
-            for (int e = 0; e < V; ++e) {
-              const float z = x[u][e];
-              const float q = fmaf(z, z, 1.0f);
-              const float L = hw_log2(fabsf(z) + hw_sqrt(q));
-              x[u][e] = fmaf(pd[e], copysignf(L, z), pg[e]);
-              prod[e / SEG] *= q;
-            }
-            if (LADJ)
-#pragma unroll
-              for (int c = 0; c < CPF; ++c) acc[u][c] = fmaf(-0.5f, hw_log2(prod[c]), acc[u][c]);
-          }
-        }
-}
-
-template <typename T, int D, int U, bool LADJ>
-__device__ __forceinline__ void step_johnson(Tile<T, D, U>& x, Acc<T, D, U>& acc,
-                                             const T* __restrict__ r) {
-  ENF_FRAG_CONSTS
-  T pg[V], pd[V], px[V], pl[V];
-  lds_vec<T, V>(r, pg);
-  lds_vec<T, V>(r + V, pd);
-  lds_vec<T, V>(r + 2 * V, px);
-  lds_vec<T, V>(r + 3 * V, pl);
-      if constexpr (std::is_same_v<T, float>) {
-        // y = gamma + delta*asinh(z), asinh|z| = ln2*log2(|z| + sqrt(1+z^2))  (johnson_trafo.jl:31)
-        // ladj: log|delta/lambda| - log(1+z^2)/2, one log2 of the product of the q = 1+z^2 of a
-        // fragment's rows                                                    (johnson_trafo.jl:41,51)
-        // Pass 1: z for the whole tile (in place) and its largest |z|; the product of <= 4 q stays
-        // finite for |z| <= 2^15, larger or infinite |z| take the exact elementwise path (one
-        // uniform branch per tile, so the fast path interleaves all U*V elements). NaN needs no
-        // special path: it propagates through the fast formulas as through the reference's.
-        float zmax = 0.f;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-          for (int e = 0; e < V; ++e) {
-            x[u][e] = (x[u][e] - px[e]) * pl[e];
-            zmax = fmaxf(zmax, fabsf(x[u][e]));
-          }
-        johnson_from_z<D, U, LADJ>(x, acc, pg, pd, zmax);
-      } else {
-        // y = gamma + delta*asinh(z) (ocml double asinh); ladj: -log(prod of the fragment
-        // column's 1 + z^2)/2, one log per column segment (absolute error ~1e-16)
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          double prod[CPF];
-#pragma unroll
-          for (int c = 0; c < CPF; ++c) prod[c] = 1.0;
-#pragma unroll
-          for (int e = 0; e < V; ++e) {
-            const double z = (x[u][e] - px[e]) * pl[e];
-            x[u][e] = fma(pd[e], asinh(z), pg[e]);
-            prod[e / SEG] = fma(prod[e / SEG], z * z, prod[e / SEG]);
-          }
-          if (LADJ)
-#pragma unroll
-            for (int c = 0; c < CPF; ++c) acc[u][c] -= 0.5 * log(prod[c]);
-        }
-      }
-}
-
-template <typename T, int D, int U, bool LADJ>
-__device__ __forceinline__ void step_johnson_inv(Tile<T, D, U>& x, Acc<T, D, U>& acc,
-                                                 const T* __restrict__ r) {
-  ENF_FRAG_CONSTS
-  T pg[V], pd[V], px[V], pl[V];
-  lds_vec<T, V>(r, pg);
-  lds_vec<T, V>(r + V, pd);
-  lds_vec<T, V>(r + 2 * V, px);
-  lds_vec<T, V>(r + 3 * V, pl);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-#pragma unroll
-        for (int e = 0; e < V; ++e) {
-          if constexpr (std::is_same_v<T, float>) {
-            // x = lambda*sinh((y-gamma)/delta) + xi (johnson_trafo.jl:36); ladj = -ladj_fwd(x_out)
-            // (johnson_trafo.jl:103-104) = -log|delta/lambda| + log(1 + sinh(w)^2)/2
-            const float w = (x[u][e] - pg[e]) * pd[e];
-            const float aw = fabsf(w);
-            // sinh: Taylor to w^7 below |w| = 0.5 (truncation < 1e-8 relative), else (E - 1/E)/2
-            const float E = hw_exp2(aw * (float)kLog2e);
-            const float big = 0.5f * (E - hw_rcp(E));
-            const float w2 = w * w;
-            const float sm = aw * fmaf(w2, fmaf(w2, fmaf(w2, 1.0f / 5040.0f, 1.0f / 120.0f), 1.0f / 6.0f), 1.0f);
-            const float sh = copysignf(aw < 0.5f ? sm : big, w);
-            x[u][e] = fmaf(pl[e], sh, px[e]);
-            if (LADJ) acc[u][e / SEG] = fmaf(0.5f, hw_log2(fmaf(sh, sh, 1.0f)), acc[u][e / SEG]);
-          } else {
-            // the reference's ladj is from the output, log(1 + ((x_out - xi)/lambda)^2)/2, and
-            // (x_out - xi)/lambda = sinh(w) up to the rounding of x_out
-            const double w = (x[u][e] - pg[e]) * pd[e];
-            const double sh = sinh(w);
-            x[u][e] = fma(pl[e], sh, px[e]);
-            if (LADJ) acc[u][e / SEG] += 0.5 * log1p(sh * sh);
-          }
-        }
-      }
-}
-
-template <typename T, int D, int U>
-__device__ __forceinline__ void step_scaleshift(Tile<T, D, U>& x, const T* __restrict__ r) {
-  ENF_FRAG_CONSTS
-      // y = muladd(x, a, b) (scale_shift_trafo.jl:16); ladj = sum log|a| (constant, in ctot)
-      T pa[V], pb[V];
-      lds_vec<T, V>(r, pa);
-      lds_vec<T, V>(r + V, pb);
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int e = 0; e < V; ++e) x[u][e] = fma(x[u][e], pa[e], pb[e]);
-}
-
-template <typename T, int D, int U, bool LADJ>
-__device__ __forceinline__ void step_center_stretch(Tile<T, D, U>& x, Acc<T, D, U>& acc,
-                                                    const T* __restrict__ r) {
-  ENF_FRAG_CONSTS
-      T rr[8][V];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) lds_vec<T, V>(r + q * V, rr[q]);
-#pragma unroll
-      for (int e = 0; e < V; ++e) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if constexpr (std::is_same_v<T, float>) {
-            // center_stretch.jl:4-8 with e = exp(|b x|); ladj = -contract_ladj(y) (:41-42)
-            const float bl = rr[0][e], c = rr[1][e], lnb = rr[2][e], E1 = rr[3][e], E2 = rr[4][e], bal = rr[5][e];
-            const float xv = x[u][e];
-            const float ex = hw_exp2(fabsf(xv * bl));
-            const float ome = 1.0f - ex;
-            const float A = fmaf(ome * ome, E2, 4.0f * ex);
-            const float inner = (hw_sqrt(A) - ome * E1) * 0.5f;
-            const float L = hw_log2(inner);
-            const float sg = xv > 0.f ? 1.f : (xv < 0.f ? -1.f : xv);  // Julia sign()
-            const float y = sg * L * lnb + c;
-            x[u][e] = y;
-            if (LADJ) {
-              const float yu = y - c;
-              const float e1 = hw_exp2(fmaf(-bl, yu, bal));
-              const float e2 = hw_exp2(fmaf(bl, yu, bal));
-              const float dy = hw_rcp(1.0f + e1) + hw_rcp(1.0f + e2);
-              acc[u][e / SEG] -= hw_log2(fabsf(dy));
-            }
-          } else {
-            const double av = rr[0][e], bv = rr[1][e], c = rr[2][e];
-            const double xv = x[u][e];
-            const double ex = exp(fabs(bv * xv));
-            const double ome = 1.0 - ex;
-            const double inner = (sqrt(ome * ome * exp(2.0 * bv * av) + 4.0 * ex) - ome * exp(bv * av)) / 2.0;
-            const double sg = xv > 0. ? 1. : (xv < 0. ? -1. : xv);
-            const double y = sg * log(inner) / bv + c;
-            x[u][e] = y;
-            if (LADJ) {
-              const double yu = y - c;
-              const double dy = 1.0 / (1.0 + exp(-bv * (yu - av))) + 1.0 / (1.0 + exp(bv * (yu + av)));
-              acc[u][e / SEG] -= log(fabs(dy));
-            }
-          }
-        }
-      }
-}
-
-template <typename T, int D, int U, bool LADJ>
-__device__ __forceinline__ void step_center_contract(Tile<T, D, U>& x, Acc<T, D, U>& acc,
-                                                     const T* __restrict__ r) {
-  ENF_FRAG_CONSTS
-      T rr[8][V];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) lds_vec<T, V>(r + q * V, rr[q]);
-#pragma unroll
-      for (int e = 0; e < V; ++e) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if constexpr (std::is_same_v<T, float>) {
-            // center_stretch.jl:11-15; ladj = contract_ladj(x) (:17-22, :65)
-            const float bl = rr[0][e], c = rr[1][e], lnb = rr[2][e], bal = rr[5][e];
-            const float xu = x[u][e] - c;
-            const float e1 = hw_exp2(fmaf(bl, xu, -bal));   // exp(b(xu - a))
-            const float e2 = hw_exp2(fmaf(-bl, xu, -bal));  // exp(-b(xu + a))
-            x[u][e] = (hw_log2(1.0f + e1) - hw_log2(1.0f + e2)) * lnb;
-            if (LADJ) {
-              const float e3 = hw_exp2(fmaf(-bl, xu, bal));  // exp(-b(xu - a))
-              const float e4 = hw_exp2(fmaf(bl, xu, bal));   // exp(b(xu + a))
-              const float dy = hw_rcp(1.0f + e3) + hw_rcp(1.0f + e4);
-              acc[u][e / SEG] += hw_log2(fabsf(dy));
-            }
-          } else {
-            const double av = rr[0][e], bv = rr[1][e], c = rr[2][e];
-            const double xu = x[u][e] - c;
-            x[u][e] = (log(1.0 + exp(bv * (xu - av))) - log(1.0 + exp(-bv * (xu + av)))) / bv;
-            if (LADJ) {
-              const double dy = 1.0 / (1.0 + exp(-bv * (xu - av))) + 1.0 / (1.0 + exp(bv * (xu + av)));
-              acc[u][e / SEG] += log(fabs(dy));
-            }
-          }
-        }
-      }
-}
-
 
 // Interpreter: runs the step table of the kernel arguments on one register tile, then stores it.
 template <typename T, int D, int U, int LM, bool TAIL, int DBG>
@@ -628,6 +282,7 @@ hipError_t launch_flow(const FlowArgs& a, bool f64, hipStream_t st, const Device
   const size_t elem = f64 ? 8 : 4;
   const size_t lds = program_lds_bytes(a, elem);
   const bool ladj = a.ladj != nullptr;
+  if (a.wy) return launch_wy(a, f64, st, dev);
   if (frag_supported(a, elem)) {
     const int lm = !ladj ? 0 : (a.accumulate ? 2 : 1);
     if (f64) return lm == 0 ? dispatch_D<double, 0>(a, lds, st, dev)

@@ -14,6 +14,7 @@ enum : int32_t {
   OP_JOHNSON = 3,
   OP_JOHNSON_INV = 4,
   OP_HOUSEHOLDER = 5,
+  OP_DENSE = 6,  // internal: a whole chained HouseholderTrafo as one orthogonal D x D product (MFMA)
 };
 
 constexpr int kMaxLayers = 16;  // layers per launch (kernarg table)
@@ -50,6 +51,8 @@ struct FlowArgs {
   int32_t nlayers;
   int32_t accumulate;
   int32_t frag;  // 1: fragment kernel (records laid out with RV = 16/elem), 0: generic kernel
+  int32_t wy;  // 1: run on the dense-Householder MFMA kernel (the step table has OP_DENSE steps)
+  int32_t img_off;  // dense kernel: LDS byte offset of the per-wave transpose images (set at launch)
   int32_t pad_;
   LayerDesc layers[kMaxLayers];
   Step steps[kMaxSteps];
@@ -76,6 +79,7 @@ inline bool frag_path(int64_t D, int64_t ldx, int64_t ldy, const void* X, const 
 // Values of T in one step's LDS record: W * max(D, RV) (RV = 16/elem on the fragment path, else 1),
 // rounded up to 16 bytes.
 inline size_t record_elems(int op, int64_t D, size_t elem, bool frag) {
+  if (op == OP_DENSE) return (size_t)(D * D);  // the product's MFMA A-operand image
   const int64_t rv = frag ? (int64_t)(16 / elem) : 1;
   size_t n = (size_t)record_width(op) * (size_t)(D > rv ? D : rv);
   const size_t q = 16 / elem;
@@ -88,6 +92,14 @@ int env_int(const char* name, int dflt);
 size_t program_lds_bytes(const FlowArgs& a, size_t elem);
 bool frag_supported(const FlowArgs& a, size_t elem);
 hipError_t launch_flow(const FlowArgs& a, bool f64, hipStream_t st, const DeviceInfo& dev);
+
+// Dense-Householder MFMA kernel (enf_flow_wy.hip): a chained HouseholderTrafo with k >= wy_min_k()
+// reflections runs as one D x D orthogonal product on the matrix cores, the other steps of the flow
+// elementwise in the same launch. Fragment path, D in {32, 64}, fp32 or fp64.
+bool wy_supported(int64_t D, bool frag);
+int wy_min_k();
+constexpr size_t kLdsParamBudgetWY = 64 * 1024;
+hipError_t launch_wy(const FlowArgs& a, bool f64, hipStream_t st, const DeviceInfo& dev);
 
 // Compiled (J o H)^n program (enf_flow_hj.hip): n if the fp32 step table is H, J, H, J, ... (one
 // reflection per H, Johnson forward) on the fragment path with D in {32, 64}, else 0.
