@@ -23,7 +23,7 @@ EXPORTED = (
     "enf_malloc", "enf_free", "enf_memcpy", "enf_stream_synchronize", "enf_flow_apply", "enf_flow_apply_host",
     "enf_flow_param_count", "enf_flow_negll_grad_workspace", "enf_flow_negll_grad",
     "enf_adagrad_step", "enf_householder_normalize", "enf_householder_normalize_strided", "enf_comm_unique_id", "enf_comm_init",
-    "enf_comm_destroy", "enf_allreduce_sum",
+    "enf_comm_destroy", "enf_allreduce_sum", "enf_johnsonsu_eval", "enf_johnsonsu_sample",
 )
 
 
@@ -70,6 +70,9 @@ _SIGS = {
     "enf_comm_init": (ctypes.c_int, [ctypes.POINTER(_vp), _i32, ctypes.c_char_p, _i32]),
     "enf_comm_destroy": (ctypes.c_int, [_vp]),
     "enf_allreduce_sum": (ctypes.c_int, [_vp, _vp, _i64, ctypes.c_int, _vp]),
+    "enf_johnsonsu_eval": (ctypes.c_int, [ctypes.c_int, _i32, _i64, _vp, _vp, _dbl, _dbl, _dbl, _dbl, _vp]),
+    "enf_johnsonsu_sample": (ctypes.c_int, [ctypes.c_int, _i64, _vp, _dbl, _dbl, _dbl, _dbl, ctypes.c_uint64,
+                                            ctypes.c_uint64, _vp]),
 }
 
 

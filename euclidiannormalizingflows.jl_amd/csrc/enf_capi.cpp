@@ -476,6 +476,40 @@ enf_status enf_householder_normalize_strided(enf_dtype dtype, int64_t D, int64_t
   ENF_CATCH
 }
 
+// ------------------------------------------------------------------------ JohnsonSU ----
+enf_status enf_johnsonsu_eval(enf_dtype dtype, int32_t fn, int64_t n, const void* x, void* out, double gamma,
+                              double delta, double xi, double lambda, void* hip_stream) {
+  ENF_TRY
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
+  if (fn < ENF_JSU_PDF || fn > ENF_JSU_QUANTILE) return fail(ENF_ERR_INVALID, "unknown JohnsonSU function");
+  if (n < 0) return fail(ENF_ERR_INVALID, "n must be >= 0");
+  if (n == 0) return ENF_OK;
+  if (!x || !out) return fail(ENF_ERR_INVALID, "x or out is NULL");
+  enf::DeviceInfo dev;
+  enf_status ds = device_info(&dev);
+  if (ds != ENF_OK) return ds;
+  const double prm[4] = {gamma, delta, xi, lambda};
+  hipError_t e = enf::launch_jsu_eval(dtype == ENF_F64, fn, n, x, out, prm, (hipStream_t)hip_stream, dev);
+  return e == hipSuccess ? ENF_OK : hip_fail(e, "JohnsonSU kernel launch");
+  ENF_CATCH
+}
+
+enf_status enf_johnsonsu_sample(enf_dtype dtype, int64_t n, void* out, double gamma, double delta, double xi,
+                                double lambda, uint64_t seed, uint64_t offset, void* hip_stream) {
+  ENF_TRY
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
+  if (n < 0) return fail(ENF_ERR_INVALID, "n must be >= 0");
+  if (n == 0) return ENF_OK;
+  if (!out) return fail(ENF_ERR_INVALID, "out is NULL");
+  enf::DeviceInfo dev;
+  enf_status ds = device_info(&dev);
+  if (ds != ENF_OK) return ds;
+  const double prm[4] = {gamma, delta, xi, lambda};
+  hipError_t e = enf::launch_jsu_sample(dtype == ENF_F64, n, out, prm, seed, offset, (hipStream_t)hip_stream, dev);
+  return e == hipSuccess ? ENF_OK : hip_fail(e, "JohnsonSU sampling kernel launch");
+  ENF_CATCH
+}
+
 // ---------------------------------------------------------------------------------- RCCL ----
 struct enf_comm_s {
   ncclComm_t comm;

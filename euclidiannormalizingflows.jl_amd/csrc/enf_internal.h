@@ -101,6 +101,12 @@ int wy_min_k();
 constexpr size_t kLdsParamBudgetWY = 64 * 1024;
 hipError_t launch_wy(const FlowArgs& a, bool f64, hipStream_t st, const DeviceInfo& dev);
 
+// JohnsonSU distribution (enf_johnsonsu.hip); prm = {gamma, delta, xi, lambda}
+hipError_t launch_jsu_eval(bool f64, int fn, int64_t n, const void* x, void* out, const double (&prm)[4], hipStream_t st,
+                           const DeviceInfo& dev);
+hipError_t launch_jsu_sample(bool f64, int64_t n, void* out, const double (&prm)[4], uint64_t seed, uint64_t offset,
+                             hipStream_t st, const DeviceInfo& dev);
+
 // Compiled (J o H)^n program (enf_flow_hj.hip): n if the fp32 step table is H, J, H, J, ... (one
 // reflection per H, Johnson forward) on the fragment path with D in {32, 64}, else 0.
 int hj_program_pairs(const FlowArgs& a);

@@ -142,6 +142,36 @@ enf_status enf_householder_normalize(enf_dtype dtype, int64_t D, int64_t k, void
 enf_status enf_householder_normalize_strided(enf_dtype dtype, int64_t D, int64_t k, void* V, int64_t ldv,
                                              void* hip_stream);
 
+/* ------------------------------------------------------- JohnsonSU distribution -------- */
+/* JohnsonSU(gamma, delta, xi, lambda) (src/johnson_trafo.jl:1-26) evaluated elementwise over n
+ * device values of the dtype, out[i] = fn(x[i]) (out may equal x), with the reference's formulas
+ * (src/johnson_trafo.jl:120-129):
+ *   PDF      deriv_johnsontrafo(x) * pdf(Normal(), johnsontrafo(x))          (:120)
+ *   LOGPDF   log of the same product                                         (:123)
+ *   CDF      cdf(Normal(), johnsontrafo(x))                                  (:121)
+ *   LOGCDF   logcdf(Normal(), johnsontrafo(x))                               (:124)
+ *   CCDF     1 - cdf;  LOGCCDF  log(1 - cdf)                                 (:125-126)
+ *   QUANTILE johnsontrafo_inv(quantile(Normal(), x)), x = probability       (:129)
+ * Parameters are passed as doubles and rounded to the dtype. */
+typedef enum {
+  ENF_JSU_PDF = 0,
+  ENF_JSU_LOGPDF = 1,
+  ENF_JSU_CDF = 2,
+  ENF_JSU_LOGCDF = 3,
+  ENF_JSU_CCDF = 4,
+  ENF_JSU_LOGCCDF = 5,
+  ENF_JSU_QUANTILE = 6
+} enf_jsu_fn;
+enf_status enf_johnsonsu_eval(enf_dtype dtype, int32_t fn, int64_t n, const void* x, void* out,
+                              double gamma, double delta, double xi, double lambda, void* hip_stream);
+/* rand(JohnsonSU(...), n) (Distributions' inverse-CDF fallback through quantile, exercised by
+ * test/test_johnson_trafo.jl:12-14): out[i] = quantile(u_i), u_i uniform on (0, 1) from
+ * Philox4x32-10 with key = seed and counter = offset + i/4 (fp32: the four 32-bit words of a call
+ * give samples 4c..4c+3) or offset + i/2 (fp64: two 64-bit draws per call). */
+enf_status enf_johnsonsu_sample(enf_dtype dtype, int64_t n, void* out, double gamma, double delta,
+                                double xi, double lambda, uint64_t seed, uint64_t offset,
+                                void* hip_stream);
+
 /* ---------------------------------------------------------------- RCCL ---------------- */
 /* Opaque communicator for the gradient all-reduce (one rank per GPU, one process each). */
 typedef struct enf_comm_s* enf_comm;

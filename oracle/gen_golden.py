@@ -18,6 +18,7 @@ Formulas (bat/EuclidianNormalizingFlows.jl v0.1.0):
   composition               ChangesOfVariables 0.1: ladj(f o g) = ladj(g) + ladj(f)
 
 Usage: python oracle/gen_golden.py   (writes tests/golden/*.npz and kats.json; deterministic)
+       python oracle/gen_golden.py --only johnsonsu   (tests/golden/johnsonsu.npz only)
 """
 from __future__ import annotations
 
@@ -295,7 +296,58 @@ def main():
                   (OP_JOHNSON_INV, rand_params(rng, OP_JOHNSON_INV, D, dtype))]
         X = np.asfortranarray(rng.standard_normal((D, 64)).astype(dtype))
         save_flow(f"mixed_all_ops_D4_{np.dtype(dtype).name}", layers, X, dtype)
+    # 7. the JohnsonSU distribution functions
+    gen_johnsonsu()
+
+
+def gen_johnsonsu():
+    """JohnsonSU distribution functions (src/johnson_trafo.jl:120-129) evaluated exactly:
+    pdf, logpdf, cdf, logcdf, ccdf, logccdf at x and quantile at p, for several parameter sets
+    (including the reference test's JohnsonSU(-15, 6.5, 0, 2.5), test/test_johnson_trafo.jl:12-14,
+    and the constructor defaults gamma=10, delta=3.5, xi=10, lambda=1, :9-12). Points keep the
+    standard-normal argument |y| <= 30, where the reference's own formulas do not underflow."""
+    rng = np.random.default_rng(20261016)
+    psets = [(-15.0, 6.5, 0.0, 2.5), (10.0, 3.5, 10.0, 1.0), (0.3, 1.0, -4.0, 0.5), (0.0, 1.0, 0.0, 1.0),
+             (-0.7, 2.25, 1.5, 3.0)]
+    out = {"params": np.array(psets)}
+    for i, (g, d, xi, l) in enumerate(psets):
+        # x such that y = g + d asinh((x - xi)/l) spans [-8, 8] plus the tails up to |y| = 30
+        ys = np.concatenate([np.linspace(-8, 8, 41), [-30, -20, -12, 12, 20, 30], rng.uniform(-6, 6, 13)])
+        xs = np.array([float(l * mp.sinh((M(y) - g) / d) + xi) for y in ys])
+        ps = np.concatenate([[1e-300, 1e-100, 1e-20, 1e-8, 1e-3, 0.01, 0.25, 0.5, 0.75, 0.99, 0.999],
+                             rng.uniform(0, 1, 13)])
+        G, Dl, XI, L = M(g), M(d), M(xi), M(l)
+        rows = {k: [] for k in ("pdf", "logpdf", "cdf", "logcdf", "ccdf", "logccdf")}
+        for x in xs:
+            u = (M(x) - XI) / L
+            y = G + Dl * mp.asinh(u)
+            deriv = (Dl / L) / mp.sqrt(1 + u * u)
+            pdf = deriv * mp.npdf(y)
+            cdf = mp.ncdf(y)
+            rows["pdf"].append(float(pdf))
+            rows["logpdf"].append(float(mp.log(pdf)))
+            rows["cdf"].append(float(cdf))
+            rows["logcdf"].append(float(mp.log(cdf)))
+            rows["ccdf"].append(float(1 - cdf))
+            rows["logccdf"].append(float(mp.log(1 - cdf)))
+        q = []
+        for p in ps:
+            with mp.workdps(400):  # 2p - 1 must keep p = 1e-300
+                z = mp.sqrt(2) * mp.erfinv(2 * M(p) - 1)
+            q.append(float(L * mp.sinh((z - G) / Dl) + XI))
+        out[f"x{i}"] = xs
+        out[f"p{i}"] = ps
+        out[f"quantile{i}"] = np.array(q)
+        for k, v in rows.items():
+            out[f"{k}{i}"] = np.array(v)
+    np.savez_compressed(os.path.join(OUT, "johnsonsu.npz"), **out)
+    print("wrote johnsonsu.npz")
 
 
 if __name__ == "__main__":
+    import sys
+
+    if sys.argv[1:] == ["--only", "johnsonsu"]:
+        gen_johnsonsu()
+        sys.exit(0)
     main()

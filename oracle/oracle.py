@@ -30,7 +30,7 @@ class _Layer(ctypes.Structure):
 
 def build() -> str:
     """Compile liboracle.so with gcc (oracle/Makefile) if it is missing or stale."""
-    src = [os.path.join(_HERE, f) for f in ("enf_oracle.c", "enf_oracle.h", "Makefile")]
+    src = [os.path.join(_HERE, f) for f in ("enf_oracle.c", "enf_oracle_jsu.c", "enf_oracle.h", "Makefile")]
     if not os.path.exists(_LIB) or os.path.getmtime(_LIB) < max(os.path.getmtime(s) for s in src):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB
@@ -64,7 +64,46 @@ def lib() -> ctypes.CDLL:
             f = getattr(_lib, f"or_mvnormal_negll_{S}")
             f.restype = T
             f.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
+        f = _lib.or_norminvcdf_f64
+        f.restype, f.argtypes = ctypes.c_double, [ctypes.c_double]
+        f = _lib.or_jsu_eval_vec_f64
+        f.restype = None
+        f.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_double] * 4
+        f = _lib.or_philox4x32_10
+        f.restype = None
+        f.argtypes = [ctypes.POINTER(ctypes.c_uint32 * 4), ctypes.POINTER(ctypes.c_uint32 * 2),
+                      ctypes.POINTER(ctypes.c_uint32 * 4)]
+        f = _lib.or_jsu_uniforms
+        f.restype = None
+        f.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]
     return _lib
+
+
+JSU_FNS = ("pdf", "logpdf", "cdf", "logcdf", "ccdf", "logccdf", "quantile")  # = enf_jsu_fn codes
+
+
+def jsu_eval(fn: str, x, gamma, delta, xi, lam) -> np.ndarray:
+    """JohnsonSU pdf/logpdf/cdf/logcdf/ccdf/logccdf/quantile (src/johnson_trafo.jl:120-129), in double."""
+    x = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    out = np.empty_like(x)
+    lib().or_jsu_eval_vec_f64(JSU_FNS.index(fn), x.size, x.ctypes.data, out.ctypes.data,
+                              float(gamma), float(delta), float(xi), float(lam))
+    return out
+
+
+def philox4x32_10(ctr, key):
+    c = (ctypes.c_uint32 * 4)(*ctr)
+    k = (ctypes.c_uint32 * 2)(*key)
+    o = (ctypes.c_uint32 * 4)()
+    lib().or_philox4x32_10(ctypes.byref(c), ctypes.byref(k), ctypes.byref(o))
+    return tuple(o)
+
+
+def jsu_uniforms(dtype, n: int, seed: int, offset: int = 0) -> np.ndarray:
+    """The uniforms of enf_johnsonsu_sample (Philox4x32-10 stream, include/enf.h), as float64."""
+    u = np.empty(n, dtype=np.float64)
+    lib().or_jsu_uniforms(int(np.dtype(dtype) == np.float64), n, u.ctypes.data, seed, offset)
+    return u
 
 
 def _sfx(dtype) -> str:

@@ -62,6 +62,32 @@ def test_version_and_errors(enf):
     assert L.enf_flow_apply(0, 2, 0, None, 2, None, 2, None, 0, arr, 1, None) == enf._lib.ENF_OK
 
 
+def test_johnsonsu_argument_checks(enf):
+    """enf_johnsonsu_eval / _sample reject bad arguments before any device work; n == 0 is a no-op."""
+    L = enf._lib.lib()
+    E = enf._lib.ENF_ERR_INVALID
+    assert L.enf_johnsonsu_eval(5, 0, 4, 16, 16, 0.0, 1.0, 0.0, 1.0, None) == E
+    assert L.enf_johnsonsu_eval(0, 7, 4, 16, 16, 0.0, 1.0, 0.0, 1.0, None) == E
+    assert "unknown JohnsonSU function" in L.enf_last_error().decode()
+    assert L.enf_johnsonsu_eval(0, 0, -1, 16, 16, 0.0, 1.0, 0.0, 1.0, None) == E
+    assert L.enf_johnsonsu_eval(0, 0, 4, None, 16, 0.0, 1.0, 0.0, 1.0, None) == E
+    assert L.enf_johnsonsu_eval(1, 6, 0, None, None, 0.0, 1.0, 0.0, 1.0, None) == enf._lib.ENF_OK
+    assert L.enf_johnsonsu_sample(3, 4, 16, 0.0, 1.0, 0.0, 1.0, 1, 0, None) == E
+    assert L.enf_johnsonsu_sample(0, 4, None, 0.0, 1.0, 0.0, 1.0, 1, 0, None) == E
+    assert L.enf_johnsonsu_sample(0, 0, None, 0.0, 1.0, 0.0, 1.0, 1, 0, None) == enf._lib.ENF_OK
+
+
+def test_johnsonsu_host_statistics(enf):
+    """Host-side statistics of the JohnsonSU mirror (src/johnson_trafo.jl:21-26)."""
+    import math
+
+    d = enf.JohnsonSU(-15, 6.5, 0, 2.5)
+    assert d.mean() == 0 - 2.5 * math.exp(6.5 ** -2 / 2) * math.sinh(-15 / 6.5)
+    assert d.median() == 2.5 * math.sinh(15 / 6.5)
+    assert d.location() == d.mean() and d.scale() == d.var()  # the reference's scale = var quirk
+    assert d.minimum() == -math.inf and d.maximum() == math.inf and d.partype == np.float64
+
+
 def test_param_count(enf):
     L = enf._lib.lib()
     arr = (enf._lib.Layer * 3)()
