@@ -164,6 +164,41 @@ function mvnormal_negll_trafograd(f::_Supported, X::HipMatrix{T}) where {T}
     g[1], g[2:end]
 end
 
-export HipMatrix, mvnormal_negll_trafograd
+# JohnsonSU (src/johnson_trafo.jl:120-129) over a 1 x n HipMatrix of values: pdf.(d, X) etc. on the
+# device (enf_johnsonsu_eval), rand(d, n) as quantile of a Philox4x32-10 stream (enf_johnsonsu_sample).
+using EuclidianNormalizingFlows: JohnsonSU
+import Distributions
+
+const ENF_JSU_PDF, ENF_JSU_LOGPDF, ENF_JSU_CDF, ENF_JSU_LOGCDF = Int32(0), Int32(1), Int32(2), Int32(3)
+const ENF_JSU_CCDF, ENF_JSU_LOGCCDF, ENF_JSU_QUANTILE = Int32(4), Int32(5), Int32(6)
+
+function _jsu(fn::Int32, d::JohnsonSU, X::HipMatrix{T}) where {T}
+    out = HipMatrix{T}(X.D, X.N)
+    check(ccall((:enf_johnsonsu_eval, libenf), Cint,
+                (Cint, Int32, Int64, Ptr{Cvoid}, Ptr{Cvoid}, Cdouble, Cdouble, Cdouble, Cdouble, Ptr{Cvoid}),
+                T === Float64 ? ENF_F64 : ENF_F32, fn, X.D * X.N, X.buf.ptr, out.buf.ptr,
+                d.gamma, d.delta, d.xi, d.lambda, C_NULL))
+    out
+end
+
+jsu_pdf(d::JohnsonSU, X::HipMatrix) = _jsu(ENF_JSU_PDF, d, X)
+jsu_logpdf(d::JohnsonSU, X::HipMatrix) = _jsu(ENF_JSU_LOGPDF, d, X)
+jsu_cdf(d::JohnsonSU, X::HipMatrix) = _jsu(ENF_JSU_CDF, d, X)
+jsu_logcdf(d::JohnsonSU, X::HipMatrix) = _jsu(ENF_JSU_LOGCDF, d, X)
+jsu_ccdf(d::JohnsonSU, X::HipMatrix) = _jsu(ENF_JSU_CCDF, d, X)
+jsu_logccdf(d::JohnsonSU, X::HipMatrix) = _jsu(ENF_JSU_LOGCCDF, d, X)
+jsu_quantile(d::JohnsonSU, P::HipMatrix) = _jsu(ENF_JSU_QUANTILE, d, P)
+
+function jsu_rand(d::JohnsonSU, ::Type{T}, n::Integer; seed::UInt64 = UInt64(0), offset::UInt64 = UInt64(0)) where {T}
+    out = HipMatrix{T}(1, n)
+    check(ccall((:enf_johnsonsu_sample, libenf), Cint,
+                (Cint, Int64, Ptr{Cvoid}, Cdouble, Cdouble, Cdouble, Cdouble, UInt64, UInt64, Ptr{Cvoid}),
+                T === Float64 ? ENF_F64 : ENF_F32, n, out.buf.ptr, d.gamma, d.delta, d.xi, d.lambda,
+                seed, offset, C_NULL))
+    out
+end
+
+export HipMatrix, mvnormal_negll_trafograd, jsu_pdf, jsu_logpdf, jsu_cdf, jsu_logcdf, jsu_ccdf,
+       jsu_logccdf, jsu_quantile, jsu_rand
 
 end # module
