@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--N", type=int, default=10_000_000, help="total samples (all ranks)")
     ap.add_argument("--nbatches", type=int, default=100)
     ap.add_argument("--pairs", type=int, default=4)
+    ap.add_argument("--history", default="", help="write the per-step negll to this file (JSON list)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -125,6 +126,9 @@ def main():
     wall, grad_ms_max = max_over_ranks([wall, grad_ms], dev, world)
     samples = sum(plan[(args.warmup + i) % len(plan)][0] for i in range(args.steps))
     negll = [float(h) for h in torch.cat(hist).cpu()]
+    if args.history and rank == 0:
+        with open(args.history, "w") as f:
+            json.dump(negll, f)
     if rank == 0:
         print(json.dumps({
             "metric": "optimize_whitening training steps/s (config 5)",

@@ -190,6 +190,87 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
   }
 }
 
+// Block prologue shared by both kernels: per pair v'v and the constant ladj part sum log|delta/lambda|
+// (double, scr), then the records [pair][group][param][4] in rec. Returns ctot = sum of the constants.
+template <int D>
+__device__ __forceinline__ float grad_prologue(const HJGradArgs& a, double* __restrict__ scr, float* __restrict__ rec) {
+  const int n = a.n;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int p = wave; p < n; p += 4) {
+    double vv = 0.0, cl = 0.0;
+    for (int d = lane; d < D; d += 64) {
+      const double vd = a.v[p][d];
+      vv += vd * vd;
+      cl += log(fabs((double)a.d[p][d])) - log(fabs((double)a.lam[p][d]));
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+      vv += __shfl_xor(vv, m);
+      cl += __shfl_xor(cl, m);
+    }
+    if (lane == 0) {
+      scr[2 * p] = sqrt(2.0 / vv);
+      scr[2 * p + 1] = cl;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < n * D; i += blockDim.x) {
+    const int p = i / D, d = i % D;
+    float* r = rec + (size_t)p * kNP * D + (d / 4) * kNP * 4 + (d % 4);
+    const double lam = a.lam[p][d], xi = a.xi[p][d], del = a.d[p][d];
+    r[0] = (float)((double)a.v[p][d] * scr[2 * p]);
+    r[4] = a.g[p][d];
+    r[8] = (float)(del * kLn2);
+    r[12] = (float)(1.0 / lam);
+    r[16] = (float)(-xi / lam);
+    r[20] = (float)lam;
+    r[24] = (float)xi;
+    r[28] = (float)del;
+  }
+  __syncthreads();
+  double c = 0.0;
+  for (int p = 0; p < n; ++p) c += scr[2 * p + 1];
+  return (float)c;
+}
+
+// Block epilogue shared by both kernels: loss and the flow gradient (layer order, the
+// enf_flow_param_count layout) of the block from the 4 waves' accumulators acc0 + w * wstride
+// ([pair][param 5][D] floats each), summed in a fixed order (deterministic).
+template <int D>
+__device__ __forceinline__ void grad_epilogue(const HJGradArgs& a, double* __restrict__ scr, const float* __restrict__ acc0,
+                                              size_t wstride, double lossp, int nvalid) {
+  const int n = a.n;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int m = 32; m >= 1; m >>= 1) {
+    lossp += __shfl_xor(lossp, m);
+    nvalid += __shfl_xor(nvalid, m);
+  }
+  double* wl = scr + 2 * kHJGradMaxPairs;
+  if (lane == 0) {
+    wl[2 * wave] = lossp;
+    wl[2 * wave + 1] = (double)nvalid;
+  }
+  __syncthreads();
+  double* out = a.partial + (int64_t)blockIdx.x * (1 + a.nparams);
+  const double nb = wl[1] + wl[3] + wl[5] + wl[7];
+  if (tid == 0) out[0] = ((wl[0] + wl[2]) + wl[4]) + wl[6];
+  for (int i = tid; i < n * 5 * D; i += blockDim.x) {
+    const int p = i / (5 * D), k = (i / D) % 5, d = i % D;
+    const double s = (((double)acc0[i] + (double)acc0[wstride + i]) + (double)acc0[2 * wstride + i]) +
+                     (double)acc0[3 * wstride + i];
+    const double del = a.d[p][d], lam = a.lam[p][d];
+    double gval;
+    int64_t o;
+    switch (k) {
+      case 0: gval = s; o = a.goffH[p] + d; break;                             // raw Householder sum
+      case 1: gval = s; o = a.goffJ[p] + d; break;                             // gamma
+      case 2: gval = kLn2 * s - nb / del; o = a.goffJ[p] + D + d; break;       // delta
+      case 3: gval = -s; o = a.goffJ[p] + 2 * D + d; break;                    // xi
+      default: gval = -s + nb / lam; o = a.goffJ[p] + 3 * D + d; break;        // lambda
+    }
+    out[1 + o] = gval;
+  }
+}
+
 // KU: fragments (columns) per lane per tile. 1 halves the LDS image of z per wave (more resident
 // blocks per CU) but doubles the per-tile flush of the gradient partials; 2 measured faster.
 template <int D, int KU>
@@ -210,45 +291,7 @@ __global__ __launch_bounds__(256) void hj_grad_kernel(HJGradArgs a) {
   float* zst = reinterpret_cast<float*>(wbase + accb);
   float* dst = reinterpret_cast<float*>(wbase + accb + zb);
   for (int i = lane; i < n * 5 * D; i += 64) acc[i] = 0.f;
-  // pass 1: per pair v'v and the constant ladj part sum log|delta/lambda| (double)
-  for (int p = wave; p < n; p += 4) {
-    double vv = 0.0, cl = 0.0;
-    for (int d = lane; d < D; d += 64) {
-      const double vd = a.v[p][d];
-      vv += vd * vd;
-      cl += log(fabs((double)a.d[p][d])) - log(fabs((double)a.lam[p][d]));
-    }
-    for (int m = 32; m >= 1; m >>= 1) {
-      vv += __shfl_xor(vv, m);
-      cl += __shfl_xor(cl, m);
-    }
-    if (lane == 0) {
-      scr[2 * p] = sqrt(2.0 / vv);
-      scr[2 * p + 1] = cl;
-    }
-  }
-  __syncthreads();
-  // pass 2: records [pair][group][param][4]
-  for (int i = tid; i < n * D; i += blockDim.x) {
-    const int p = i / D, d = i % D;
-    float* r = rec + (size_t)p * kNP * D + (d / 4) * kNP * 4 + (d % 4);
-    const double lam = a.lam[p][d], xi = a.xi[p][d], del = a.d[p][d];
-    r[0] = (float)((double)a.v[p][d] * scr[2 * p]);
-    r[4] = a.g[p][d];
-    r[8] = (float)(del * kLn2);
-    r[12] = (float)(1.0 / lam);
-    r[16] = (float)(-xi / lam);
-    r[20] = (float)lam;
-    r[24] = (float)xi;
-    r[28] = (float)del;
-  }
-  __syncthreads();
-  float ctot = 0.f;
-  {
-    double c = 0.0;
-    for (int p = 0; p < n; ++p) c += scr[2 * p + 1];
-    ctot = (float)c;
-  }
+  const float ctot = grad_prologue<D>(a, scr, rec);
   double lossp = 0.0;
   int nvalid = 0;
   const int64_t ntiles = (a.N + L::TC - 1) / L::TC;
@@ -258,43 +301,192 @@ __global__ __launch_bounds__(256) void hj_grad_kernel(HJGradArgs a) {
     if (t < full) grad_tile<D, KU, false>(a, t * L::TC, lane, rec, zst, dst, acc, lossp, nvalid, ctot);
     else grad_tile<D, KU, true>(a, t * L::TC, lane, rec, zst, dst, acc, lossp, nvalid, ctot);
   }
-  // block partial: loss, then the flow gradient (layer order, enf_flow_param_count layout)
-  for (int m = 32; m >= 1; m >>= 1) {
-    lossp += __shfl_xor(lossp, m);
-    nvalid += __shfl_xor(nvalid, m);
-  }
-  double* wl = scr + 2 * kHJGradMaxPairs;
-  if (lane == 0) {
-    wl[2 * wave] = lossp;
-    wl[2 * wave + 1] = (double)nvalid;
-  }
-  __syncthreads();
-  double* out = a.partial + (int64_t)blockIdx.x * (1 + a.nparams);
-  const double nb = wl[1] + wl[3] + wl[5] + wl[7];
-  if (tid == 0) out[0] = ((wl[0] + wl[2]) + wl[4]) + wl[6];
-  const size_t wstride = (accb + zb + db) / 4;  // floats between the waves' acc arrays
-  const float* acc0 = reinterpret_cast<const float*>(smem + 256 + recb);
-  for (int i = tid; i < n * 5 * D; i += blockDim.x) {
-    const int p = i / (5 * D), k = (i / D) % 5, d = i % D;
-    const double s = (((double)acc0[i] + (double)acc0[wstride + i]) + (double)acc0[2 * wstride + i]) +
-                     (double)acc0[3 * wstride + i];
-    const double del = a.d[p][d], lam = a.lam[p][d];
-    double gval;
-    int64_t o;
-    switch (k) {
-      case 0: gval = s; o = a.goffH[p] + d; break;                             // raw Householder sum
-      case 1: gval = s; o = a.goffJ[p] + d; break;                             // gamma
-      case 2: gval = kLn2 * s - nb / del; o = a.goffJ[p] + D + d; break;       // delta
-      case 3: gval = -s; o = a.goffJ[p] + 2 * D + d; break;                    // xi
-      default: gval = -s + nb / lam; o = a.goffJ[p] + 3 * D + d; break;        // lambda
+  grad_epilogue<D>(a, scr, reinterpret_cast<const float*>(smem + 256 + recb), (accb + zb + db) / 4, lossp, nvalid);
+}
+
+// ---- register variant (NP <= 4 pairs, compile time): z and the reflection dots of a tile stay in
+// registers between its forward and backward, and the per-lane gradient partials accumulate in
+// registers over all of the wave's tiles (acc[pair][param][row]); one cross-slot reduction per
+// wave at the end instead of one per tile and pair. Same arithmetic per element as grad_tile.
+template <int D, int KU, int NP, bool TAIL>
+__device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0, int lane, const float* __restrict__ rec,
+                                              float (&acc)[NP][5][4], double& lossp, int& nvalid, float ctot) {
+  using L = GL<D, KU>;
+  constexpr int V = 4, G = L::G, S = L::S;
+  const int grp = lane % G;
+  float x[KU][V];
+  float vm[KU];
+#pragma unroll
+  for (int u = 0; u < KU; ++u) {
+    const int64_t c = col0 + (int64_t)u * S + lane / G;
+    const float* src = a.X + c * D + V * grp;
+    vm[u] = (!TAIL || c < a.N) ? 1.f : 0.f;
+    if (!TAIL) {
+      const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
+      __builtin_memcpy(&x[u][0], &v4, 16);
+    } else {
+#pragma unroll
+      for (int e = 0; e < V; ++e) x[u][e] = c < a.N ? src[e] : 0.f;
     }
-    out[1 + o] = gval;
   }
+  float zs[NP][KU][V], ds[NP][KU];
+  float lad[KU] = {};
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const float* r = rec + (size_t)p * kNP * D + grp * kNP * V;
+    float vh[V], gam[V], dl2[V], il[V], nxil[V];
+    lds_vec<float, V>(r, vh);
+    lds_vec<float, V>(r + V, gam);
+    lds_vec<float, V>(r + 2 * V, dl2);
+    lds_vec<float, V>(r + 3 * V, il);
+    lds_vec<float, V>(r + 4 * V, nxil);
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      float t = vh[0] * x[u][0];
+#pragma unroll
+      for (int e = 1; e < V; ++e) t = fmaf(vh[e], x[u][e], t);
+      ds[p][u] = group_sum<G>(t);
+    }
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      float q[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        zs[p][u][e] = fmaf(fmaf(-ds[p][u], vh[e], x[u][e]), il[e], nxil[e]);
+        q[e] = fmaf(zs[p][u][e], zs[p][u][e], 1.f);
+        const float Lz = copysignf(hw_log2(fabsf(zs[p][u][e]) + hw_sqrt(q[e])), zs[p][u][e]);
+        x[u][e] = fmaf(dl2[e], Lz, gam[e]);
+      }
+      lad[u] = fmaf(-0.5f, hw_log2((q[0] * q[1]) * (q[2] * q[3])), lad[u]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < KU; ++u) {
+    float t = 0.f;
+#pragma unroll
+    for (int e = 0; e < V; ++e) t = fmaf(x[u][e], x[u][e], t);
+    const float ysq = group_sum<G>(t);
+    const float ltot = group_sum<G>(lad[u]);
+    if (grp == 0 && vm[u] != 0.f) {
+      lossp += 0.5 * (double)ysq + 0.5 * D * 1.8378770664093454836 - ((double)ctot + kLn2 * (double)ltot);
+      ++nvalid;
+    }
+  }
+  float g[KU][V];
+#pragma unroll
+  for (int u = 0; u < KU; ++u)
+#pragma unroll
+    for (int e = 0; e < V; ++e) g[u][e] = x[u][e] * vm[u];
+#pragma unroll
+  for (int p = NP - 1; p >= 0; --p) {
+    const float* r = rec + (size_t)p * kNP * D + grp * kNP * V;
+    float vh[V], il[V], lam[V], xi[V], del[V];
+    lds_vec<float, V>(r, vh);
+    lds_vec<float, V>(r + 3 * V, il);
+    lds_vec<float, V>(r + 5 * V, lam);
+    lds_vec<float, V>(r + 6 * V, xi);
+    lds_vec<float, V>(r + 7 * V, del);
+    float gh[KU][V], u_[KU][V];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float z = zs[p][u][e];
+        const float q = fmaf(z, z, 1.f);
+        const float s = hw_sqrt(q);
+        const float rs = hw_rcp(s);
+        const float Lz = copysignf(hw_log2(fabsf(z) + s), z);
+        acc[p][1][e] += g[u][e];
+        acc[p][2][e] = fmaf(g[u][e], Lz, acc[p][2][e]);
+        const float dz = fmaf(g[u][e] * del[e], rs, z * (rs * rs) * vm[u]);
+        gh[u][e] = dz * il[e];
+        acc[p][3][e] += gh[u][e];
+        acc[p][4][e] = fmaf(gh[u][e], z, acc[p][4][e]);
+        u_[u][e] = fmaf(ds[p][u], vh[e], fmaf(lam[e], z, xi[e]));  // layer input u = h + dot vh
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      float t = vh[0] * gh[u][0];
+#pragma unroll
+      for (int e = 1; e < V; ++e) t = fmaf(vh[e], gh[u][e], t);
+      const float vg = group_sum<G>(t);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        acc[p][0][e] = fmaf(gh[u][e], ds[p][u], fmaf(u_[u][e], vg, acc[p][0][e]));
+        g[u][e] = fmaf(-vg, vh[e], gh[u][e]);
+      }
+    }
+  }
+}
+
+template <int D, int KU, int NP>
+__global__ __launch_bounds__(256) void hj_grad_reg_kernel(HJGradArgs a) {
+  using L = GL<D, KU>;
+  constexpr int G = L::G;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double* scr = reinterpret_cast<double*>(smem);
+  float* rec = reinterpret_cast<float*>(smem + 256);
+  const size_t recb = (size_t)NP * kNP * D * 4;
+  float* accs = reinterpret_cast<float*>(smem + 256 + recb);  // per wave [pair][param 5][D]
+  const float ctot = grad_prologue<D>(a, scr, rec);
+  float acc[NP][5][4];
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[p][k][e] = 0.f;
+  double lossp = 0.0;
+  int nvalid = 0;
+  const int64_t ntiles = (a.N + L::TC - 1) / L::TC;
+  const int64_t full = a.N / L::TC;
+  const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wave);
+  for (int64_t t = wave_id; t < ntiles; t += (int64_t)gridDim.x * 4) {
+    if (t < full) grad_tile_reg<D, KU, NP, false>(a, t * L::TC, lane, rec, acc, lossp, nvalid, ctot);
+    else grad_tile_reg<D, KU, NP, true>(a, t * L::TC, lane, rec, acc, lossp, nvalid, ctot);
+  }
+  // one cross-slot reduction per wave; lanes 0..G-1 then hold the row sums of their 4 rows
+  float* wacc = accs + (size_t)wave * NP * 5 * D;
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float sv = slot_sum<G>(acc[p][k][e]);
+        if (lane < G) wacc[(p * 5 + k) * D + 4 * lane + e] = sv;
+      }
+  __syncthreads();
+  grad_epilogue<D>(a, scr, accs, (size_t)NP * 5 * D, lossp, nvalid);
+}
+
+template <int D, int KU, int NP>
+size_t hj_grad_reg_lds() {
+  return 256 + (size_t)NP * kNP * D * 4 + 4 * (size_t)NP * 5 * D * 4;
 }
 
 template <int D, int KU>
 size_t hj_grad_lds(int n) {
   return 256 + (size_t)n * kNP * D * 4 + 4 * ((size_t)n * 5 * D * 4 + (size_t)n * KU * 64 * 16 + (size_t)n * KU * 64 * 4);
+}
+
+template <int D, int KU, int NP>
+hipError_t launch_reg_np(const HJGradArgs& a, int blocks, hipStream_t st) {
+  const size_t lds = hj_grad_reg_lds<D, KU, NP>();
+  hipLaunchKernelGGL((hj_grad_reg_kernel<D, KU, NP>), dim3(blocks), dim3(256), lds, st, a);
+  return hipGetLastError();
+}
+
+template <int D, int KU>
+hipError_t launch_reg(const HJGradArgs& a, int blocks, hipStream_t st) {
+  switch (a.n) {
+    case 1: return launch_reg_np<D, KU, 1>(a, blocks, st);
+    case 2: return launch_reg_np<D, KU, 2>(a, blocks, st);
+    case 3: return launch_reg_np<D, KU, 3>(a, blocks, st);
+    default: return launch_reg_np<D, KU, 4>(a, blocks, st);
+  }
 }
 
 }  // namespace
@@ -334,6 +526,13 @@ hipError_t launch_hj_grad(int64_t D, int64_t N, const void* X, const enf_layer* 
     off += 4 * (int32_t)D;
   }
   if (off != nparams) return hipErrorInvalidValue;
+  // register variant for <= 4 pairs (ENF_GRAD_REG=0: the LDS variant; ENF_GRAD_RU: its KU)
+  static const int reg = env_int("ENF_GRAD_REG", 1);
+  static const int ru = env_int("ENF_GRAD_RU", 1) == 2 ? 2 : 1;  // 1: 215 VGPRs at 4 pairs (2 waves/SIMD)
+  if (reg && a.n <= 4) {
+    if (D == 32) return ru == 1 ? launch_reg<32, 1>(a, blocks, st) : launch_reg<32, 2>(a, blocks, st);
+    return ru == 1 ? launch_reg<64, 1>(a, blocks, st) : launch_reg<64, 2>(a, blocks, st);
+  }
   static const int ku = env_int("ENF_GRAD_U", 2) == 1 ? 1 : 2;  // 2: measured 72 vs 93 us at config 5
   const size_t lds = D == 32 ? (ku == 1 ? hj_grad_lds<32, 1>(a.n) : hj_grad_lds<32, 2>(a.n))
                              : (ku == 1 ? hj_grad_lds<64, 1>(a.n) : hj_grad_lds<64, 2>(a.n));
