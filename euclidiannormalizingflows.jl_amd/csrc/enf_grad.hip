@@ -375,38 +375,51 @@ struct ReduceArgs {
   int32_t D;
   int32_t nh;  // Householder columns
   void* out;
-  double* tot;  // 1 + nparams totals (workspace tail)
+  double* tot;  // kSumSlices x (1 + nparams) slice totals (workspace tail); slice 0 = the total
   // per Householder column: offset of its gradient vector and its device column pointer
   int32_t hoff[kMaxGradSteps];
   const void* hcol[kMaxGradSteps];
 };
 
-// Sum of the block partials, in block order per wave (b = w, w + 4, ...) and then over the 4 waves,
-// in double: tot[i] for the loss (i = 0) and every gradient entry. 64 entries per block.
+// Sum of the block partials in kSumSlices slices (blockIdx.y): slice s covers blocks
+// [s*bs, (s+1)*bs), summed in block order per wave (b = start + w, + 4, ...) with 8 independent
+// accumulators and then over the 4 waves, in double -> tot[s][i] for the loss (i = 0) and every
+// gradient entry. grad_finalize_kernel adds the slices in order: a fixed summation tree, so the
+// result is deterministic. 64 entries per block.
+constexpr int kSumSlices = 8;
 __global__ __launch_bounds__(256) void grad_sum_kernel(ReduceArgs r) {
   __shared__ double red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 64 + lane;
   const int64_t n = 1 + (int64_t)r.nparams;
-  // 8 independent accumulators (loads in flight together), combined in a fixed order
+  const int bs = (r.nblocks + kSumSlices - 1) / kSumSlices;
+  const int b0 = (int)blockIdx.y * bs;
+  const int b1 = b0 + bs < r.nblocks ? b0 + bs : r.nblocks;
   double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (i < n) {
-    int b = w;
-    for (; b + 28 < r.nblocks; b += 32)
+    int b = b0 + w;
+    for (; b + 28 < b1; b += 32)
 #pragma unroll
       for (int k = 0; k < 8; ++k) s8[k] += r.partial[(int64_t)(b + 4 * k) * n + i];
-    for (; b < r.nblocks; b += 4) s8[0] += r.partial[(int64_t)b * n + i];
+    for (; b < b1; b += 4) s8[0] += r.partial[(int64_t)b * n + i];
   }
   const double s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
   red[w][lane] = s;
   __syncthreads();
-  if (w == 0 && i < n) r.tot[i] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  if (w == 0 && i < n) r.tot[(int64_t)blockIdx.y * n + i] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
 // Householder direction projection and accumulation into out (one block).
 template <typename T>
 __global__ __launch_bounds__(256) void grad_finalize_kernel(ReduceArgs r) {
   double* tot = r.tot;
+  const int64_t n = 1 + (int64_t)r.nparams;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {  // the slices in order, into slice 0
+    double t = tot[i];
+    for (int s = 1; s < kSumSlices; ++s) t += tot[s * n + i];
+    tot[i] = t;
+  }
+  __syncthreads();
   // Householder: dS/dw = -sqrt2 * G;  dS/dv = (dS/dw - w (dS/dw . w)) / |v|  (householder_trafo.jl:32)
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
@@ -522,7 +535,7 @@ hipError_t launch_grad(const Plan& P, hipStream_t st) {
     default: return hipErrorInvalidValue;
   }
   if (e0 != hipSuccess) return e0;
-  hipLaunchKernelGGL(grad_sum_kernel, dim3((unsigned)((1 + P.ra.nparams + 63) / 64)), dim3(256), 0, st, P.ra);
+  hipLaunchKernelGGL(grad_sum_kernel, dim3((unsigned)((1 + P.ra.nparams + 63) / 64), kSumSlices), dim3(256), 0, st, P.ra);
   hipLaunchKernelGGL((grad_finalize_kernel<T>), dim3(1), dim3(256), 0, st, P.ra);
   return hipGetLastError();
 }
@@ -534,7 +547,7 @@ enf_status negll_grad_workspace(bool f64, int64_t D, int64_t N, const enf_layer*
   Plan P;
   enf_status s = make_plan(f64, D, N > 0 ? N : 1, layers, nlayers, P);
   if (s != ENF_OK) return s;
-  *bytes = ((size_t)P.blocks + 1) * (1 + (size_t)P.ga.nparams) * sizeof(double);
+  *bytes = ((size_t)P.blocks + kSumSlices) * (1 + (size_t)P.ga.nparams) * sizeof(double);
   return ENF_OK;
 }
 
@@ -543,7 +556,7 @@ enf_status negll_grad(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx
   Plan P;
   enf_status s = make_plan(f64, D, N, layers, nlayers, P);
   if (s != ENF_OK) return s;
-  const size_t need = ((size_t)P.blocks + 1) * (1 + (size_t)P.ga.nparams) * sizeof(double);
+  const size_t need = ((size_t)P.blocks + kSumSlices) * (1 + (size_t)P.ga.nparams) * sizeof(double);
   if (!workspace || workspace_bytes < need) return set_error(ENF_ERR_INVALID, "enf_flow_negll_grad: workspace too small");
   P.ga.X = X;
   P.ga.ldx = ldx;
@@ -556,7 +569,7 @@ enf_status negll_grad(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx
   if (!f64 && !generic && hj_grad_eligible(D, ldx, X, layers, nlayers)) {
     e = launch_hj_grad(D, N, X, layers, nlayers, P.ga.nparams, (double*)workspace, P.blocks, st);
     if (e == hipSuccess) {
-      hipLaunchKernelGGL(grad_sum_kernel, dim3((unsigned)((1 + P.ra.nparams + 63) / 64)), dim3(256), 0, st, P.ra);
+      hipLaunchKernelGGL(grad_sum_kernel, dim3((unsigned)((1 + P.ra.nparams + 63) / 64), kSumSlices), dim3(256), 0, st, P.ra);
       hipLaunchKernelGGL((grad_finalize_kernel<float>), dim3(1), dim3(256), 0, st, P.ra);
       e = hipGetLastError();
     }
