@@ -88,8 +88,23 @@ def main():
     opt = enf.ADAGrad()
     hist = []
 
+    fused = world == 1 and os.environ.get("BENCH_UNFUSED", "0") != "1"
+    runs = np.ascontiguousarray(np.array(segs, dtype=np.int64).reshape(-1))
+    hbs = np.ascontiguousarray(np.array(hbatches, dtype=np.int64).reshape(-1))
+    hdev = torch.zeros(args.warmup + args.steps, dtype=torch.float64, device=dev)
+
     def step(i, ev=None):
         B, lo, hi = plan[i % len(plan)]
+        if fused:  # enf_whitening_step: gradient, loss, ADAGrad, re-normalisation (3 launches)
+            if ev is not None:
+                ev[0].record(stream)
+            lib.check(L.enf_whitening_step(lib.ENF_F32, D, hi - lo, X[:, lo:hi].data_ptr(), ldx, state.layers(),
+                                           len(state.trafos), state.theta.data_ptr(), state.acc.data_ptr(),
+                                           runs.ctypes.data, len(segs), hbs.ctypes.data, len(hbatches), opt.eta,
+                                           opt.epsilon, hdev[i:].data_ptr(), ws.data_ptr(), ws.numel() * 8, sh))
+            if ev is not None:
+                ev[1].record(stream)
+            return hdev[i:i + 1]
         out.zero_()
         if ev is not None:
             ev[0].record(stream)
@@ -134,7 +149,10 @@ def main():
             "metric": "optimize_whitening training steps/s (config 5)",
             "value": args.steps / wall, "unit": "steps/s", "samples_per_s": samples / wall,
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
-            "grad_kernel_ms_median": grad_ms, "grad_kernel_ms_max_rank": grad_ms_max, "dtype": "f32",
+            "grad_kernel_ms_median" if not fused else "fused_step_ms_median": grad_ms,
+            "grad_kernel_ms_max_rank" if not fused else "fused_step_ms_max_rank": grad_ms_max, "dtype": "f32",
+            "step": "enf_whitening_step (fused, 1 rank)" if fused else "enf_flow_negll_grad + RCCL sum + enf_adagrad_step"
+                    " + enf_householder_normalize_strided",
             "data": "synthetic: X = f_true^-1(Z), Z ~ N(0,1) (torch Philox 0x5EED), f_true seed 7, init seed 42",
             "config": {"workload": f"optimize_whitening D={D}, N={N}, nbatches={args.nbatches} "
                                    f"(B={plan[0][0]}), {args.pairs}x(J∘H), ADAGrad(0.1)",

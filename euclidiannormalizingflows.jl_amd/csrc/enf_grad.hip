@@ -409,9 +409,10 @@ __global__ __launch_bounds__(256) void grad_sum_kernel(ReduceArgs r) {
   if (w == 0 && i < n) r.tot[(int64_t)blockIdx.y * n + i] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
-// Householder direction projection and accumulation into out (one block).
+// Slices -> total, then the Householder direction projection on tot (whole block; ends with a
+// barrier, tot[0 .. nparams] final).
 template <typename T>
-__global__ __launch_bounds__(256) void grad_finalize_kernel(ReduceArgs r) {
+__device__ __forceinline__ void finalize_totals(const ReduceArgs& r) {
   double* tot = r.tot;
   const int64_t n = 1 + (int64_t)r.nparams;
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {  // the slices in order, into slice 0
@@ -439,8 +440,45 @@ __global__ __launch_bounds__(256) void grad_finalize_kernel(ReduceArgs r) {
     }
   }
   __syncthreads();
+}
+
+// Householder direction projection and accumulation into out (one block).
+template <typename T>
+__global__ __launch_bounds__(256) void grad_finalize_kernel(ReduceArgs r) {
+  finalize_totals<T>(r);
   T* out = (T*)r.out;
-  for (int i = threadIdx.x; i < 1 + r.nparams; i += blockDim.x) out[i] += (T)tot[i];
+  for (int i = threadIdx.x; i < 1 + r.nparams; i += blockDim.x) out[i] += (T)r.tot[i];
+}
+
+// The rest of a single-rank optimize_whitening step in the same block (enf_whitening_step):
+// loss/B (as the host computes out[0] / B in T), ADAGrad over the trainable runs with
+// g = (T)total (what enf_adagrad_step reads from a zeroed out), then the Householder
+// re-normalisation of every batch -- the operations and roundings of the unfused sequence.
+struct StepArgs {
+  void* theta;
+  void* acc;
+  double* loss_out;
+  double scale, eta, eps;
+  int64_t D, nsamp;
+  int32_t nruns, nhb;
+  int64_t runs[kMaxStepRuns][2];
+  int64_t hb[kMaxStepHB][3];  // offset, k, ldv
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void whitening_tail_kernel(ReduceArgs r, StepArgs a) {
+  finalize_totals<T>(r);
+  const double* tot = r.tot;
+  T* th = (T*)a.theta;
+  T* ac = (T*)a.acc;
+  if (threadIdx.x == 0) *a.loss_out = (double)((T)tot[0] / (T)a.nsamp);
+  for (int q = 0; q < a.nruns; ++q)
+    for (int64_t i = a.runs[q][0] + threadIdx.x; i < a.runs[q][1]; i += blockDim.x)
+      adagrad_update<T>(th[i], ac[i], (T)tot[1 + i], (T)a.scale, (T)a.eta, (T)a.eps);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int q = 0; q < a.nhb; ++q)
+    for (int64_t c = w; c < a.hb[q][1]; c += 4) normalize_column<T>(th + a.hb[q][0] + c * a.hb[q][2], a.D, lane);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -534,10 +572,7 @@ hipError_t launch_grad(const Plan& P, hipStream_t st) {
 #undef ENF_G
     default: return hipErrorInvalidValue;
   }
-  if (e0 != hipSuccess) return e0;
-  hipLaunchKernelGGL(grad_sum_kernel, dim3((unsigned)((1 + P.ra.nparams + 63) / 64), kSumSlices), dim3(256), 0, st, P.ra);
-  hipLaunchKernelGGL((grad_finalize_kernel<T>), dim3(1), dim3(256), 0, st, P.ra);
-  return hipGetLastError();
+  return e0;
 }
 
 }  // namespace
@@ -551,9 +586,11 @@ enf_status negll_grad_workspace(bool f64, int64_t D, int64_t N, const enf_layer*
   return ENF_OK;
 }
 
-enf_status negll_grad(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
-                      int32_t nlayers, void* out, void* workspace, size_t workspace_bytes, hipStream_t st) {
-  Plan P;
+namespace {
+
+// The per-block partials (fused (J o H)^n kernel or the generic one) and their slice sums: tot of P.ra.
+enf_status grad_parts(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
+                      int32_t nlayers, void* workspace, size_t workspace_bytes, hipStream_t st, Plan& P) {
   enf_status s = make_plan(f64, D, N, layers, nlayers, P);
   if (s != ENF_OK) return s;
   const size_t need = ((size_t)P.blocks + kSumSlices) * (1 + (size_t)P.ga.nparams) * sizeof(double);
@@ -563,22 +600,77 @@ enf_status negll_grad(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx
   P.ga.partial = workspace;
   P.ra.partial = (const double*)workspace;
   P.ra.tot = (double*)workspace + (size_t)P.blocks * (1 + (size_t)P.ga.nparams);
-  P.ra.out = out;
   hipError_t e;
   static const int generic = env_int("ENF_GRAD_GENERIC", 0);
   if (!f64 && !generic && hj_grad_eligible(D, ldx, X, layers, nlayers)) {
     e = launch_hj_grad(D, N, X, layers, nlayers, P.ga.nparams, (double*)workspace, P.blocks, st);
-    if (e == hipSuccess) {
-      hipLaunchKernelGGL(grad_sum_kernel, dim3((unsigned)((1 + P.ra.nparams + 63) / 64), kSumSlices), dim3(256), 0, st, P.ra);
-      hipLaunchKernelGGL((grad_finalize_kernel<float>), dim3(1), dim3(256), 0, st, P.ra);
-      e = hipGetLastError();
-    }
   } else {
     if (P.lds > 160 * 1024) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: flow too large for LDS");
     e = f64 ? launch_grad<double>(P, st) : launch_grad<float>(P, st);
   }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(grad_sum_kernel, dim3((unsigned)((1 + P.ra.nparams + 63) / 64), kSumSlices), dim3(256), 0, st,
+                       P.ra);
+    e = hipGetLastError();
+  }
   if (e != hipSuccess) return set_error(ENF_ERR_HIP, hipGetErrorString(e));
   return ENF_OK;
+}
+
+}  // namespace
+
+enf_status negll_grad(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
+                      int32_t nlayers, void* out, void* workspace, size_t workspace_bytes, hipStream_t st) {
+  Plan P;
+  enf_status s = grad_parts(f64, D, N, X, ldx, layers, nlayers, workspace, workspace_bytes, st, P);
+  if (s != ENF_OK) return s;
+  P.ra.out = out;
+  if (f64) hipLaunchKernelGGL((grad_finalize_kernel<double>), dim3(1), dim3(256), 0, st, P.ra);
+  else hipLaunchKernelGGL((grad_finalize_kernel<float>), dim3(1), dim3(256), 0, st, P.ra);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? ENF_OK : set_error(ENF_ERR_HIP, hipGetErrorString(e));
+}
+
+enf_status whitening_step(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
+                          int32_t nlayers, void* theta, void* acc, const int64_t* runs, int32_t nruns,
+                          const int64_t* hb, int32_t nhb, double eta, double epsilon, double* loss_out,
+                          void* workspace, size_t workspace_bytes, hipStream_t st) {
+  if (nruns < 0 || nruns > kMaxStepRuns || nhb < 0 || nhb > kMaxStepHB)
+    return set_error(ENF_ERR_UNSUPPORTED, "enf_whitening_step: too many parameter runs or Householder batches");
+  StepArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.theta = theta;
+  a.acc = acc;
+  a.loss_out = loss_out;
+  a.scale = 1.0 / (double)N;
+  a.eta = eta;
+  a.eps = epsilon;
+  a.D = D;
+  a.nsamp = N;
+  a.nruns = nruns;
+  a.nhb = nhb;
+  for (int i = 0; i < nruns; ++i) {
+    a.runs[i][0] = runs[2 * i];
+    a.runs[i][1] = runs[2 * i + 1];
+  }
+  for (int i = 0; i < nhb; ++i)
+    for (int q = 0; q < 3; ++q) a.hb[i][q] = hb[3 * i + q];
+  Plan P;
+  enf_status s = make_plan(f64, D, N, layers, nlayers, P);
+  if (s != ENF_OK) return s;
+  for (int i = 0; i < nruns; ++i)
+    if (a.runs[i][0] < 0 || a.runs[i][1] < a.runs[i][0] || a.runs[i][1] > P.ga.nparams)
+      return set_error(ENF_ERR_INVALID, "enf_whitening_step: parameter run outside theta");
+  for (int i = 0; i < nhb; ++i)
+    if (a.hb[i][0] < 0 || a.hb[i][1] < 0 || a.hb[i][2] < D ||
+        (a.hb[i][1] > 0 && a.hb[i][0] + (a.hb[i][1] - 1) * a.hb[i][2] + D > P.ga.nparams))
+      return set_error(ENF_ERR_INVALID, "enf_whitening_step: Householder batch outside theta");
+  s = grad_parts(f64, D, N, X, ldx, layers, nlayers, workspace, workspace_bytes, st, P);
+  if (s != ENF_OK) return s;
+  if (f64) hipLaunchKernelGGL((whitening_tail_kernel<double>), dim3(1), dim3(256), 0, st, P.ra, a);
+  else hipLaunchKernelGGL((whitening_tail_kernel<float>), dim3(1), dim3(256), 0, st, P.ra, a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? ENF_OK : set_error(ENF_ERR_HIP, hipGetErrorString(e));
 }
 
 }  // namespace enf

@@ -21,4 +21,34 @@ enf_status adagrad_step(bool f64, int64_t count, void* params, void* acc, const 
                         double eta, double epsilon, hipStream_t st);
 enf_status householder_normalize(bool f64, int64_t D, int64_t k, void* V, int64_t ldv, hipStream_t st);
 
+// Fused single-rank optimize_whitening step (enf_whitening_step): runs = [start, end) ranges of
+// theta to update, hb = (offset, k, ldv) Householder column batches to re-normalise.
+constexpr int kMaxStepRuns = 64;
+constexpr int kMaxStepHB = 16;
+enf_status whitening_step(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
+                          int32_t nlayers, void* theta, void* acc, const int64_t* runs, int32_t nruns,
+                          const int64_t* hb, int32_t nhb, double eta, double epsilon, double* loss_out,
+                          void* workspace, size_t workspace_bytes, hipStream_t st);
+
+// Optimisers.jl 0.2 ADAGrad on one parameter (src/optimize_whitening.jl:40): the arithmetic shared
+// by enf_adagrad_step and the fused step, so both round identically.
+template <typename T>
+__device__ __forceinline__ void adagrad_update(T& p, T& acc, T g, T scale, T eta, T eps) {
+  const T dx = g * scale;
+  const T a = acc + dx * dx;
+  acc = a;
+  p = p - dx * eta / (sqrt(a) + eps);
+}
+
+// LinearAlgebra.normalize! of one column by one wave (src/householder_trafo.jl:135-139), the sum
+// of squares in double.
+template <typename T>
+__device__ __forceinline__ void normalize_column(T* __restrict__ v, int64_t D, int lane) {
+  double ss = 0.0;
+  for (int64_t d = lane; d < D; d += 64) ss += (double)v[d] * (double)v[d];
+  for (int m = 32; m >= 1; m >>= 1) ss += __shfl_xor(ss, m);
+  const T inv = (T)(1.0 / sqrt(ss));
+  for (int64_t d = lane; d < D; d += 64) v[d] *= inv;
+}
+
 }  // namespace enf

@@ -15,12 +15,8 @@ namespace enf {
 template <typename T>
 __global__ void adagrad_kernel(int64_t n, T* __restrict__ p, T* __restrict__ acc, const T* __restrict__ g,
                                T scale, T eta, T eps) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const T dx = g[i] * scale;
-    const T a = acc[i] + dx * dx;
-    acc[i] = a;
-    p[i] = p[i] - dx * eta / (sqrt(a) + eps);
-  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    adagrad_update<T>(p[i], acc[i], g[i], scale, eta, eps);
 }
 
 enf_status adagrad_step(bool f64, int64_t count, void* params, void* acc, const void* grad, double grad_scale,
@@ -44,12 +40,7 @@ __global__ void normalize_kernel(int64_t D, int64_t k, T* __restrict__ V, int64_
   const int lane = threadIdx.x & 63;
   const int64_t col = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (col >= k) return;  // whole wave exits together
-  T* v = V + col * ldv;
-  double ss = 0.0;
-  for (int64_t d = lane; d < D; d += 64) ss += (double)v[d] * (double)v[d];
-  for (int m = 32; m >= 1; m >>= 1) ss += __shfl_xor(ss, m);
-  const T inv = (T)(1.0 / sqrt(ss));
-  for (int64_t d = lane; d < D; d += 64) v[d] *= inv;
+  normalize_column<T>(V + col * ldv, D, lane);
 }
 
 enf_status householder_normalize(bool f64, int64_t D, int64_t k, void* V, int64_t ldv, hipStream_t st) {

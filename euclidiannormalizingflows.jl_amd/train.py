@@ -296,10 +296,29 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
     segs = trainable_runs(state)
     ss_a = [(int(state.offsets[i]), int(state.offsets[i + 1])) for i, _ in _scaleshift_a_segments(state)]
     step = 0
+    # one rank: the fused step (gradient, loss, ADAGrad and re-normalisation in three launches)
+    fused = world == 1
+    runs = np.ascontiguousarray(np.array(segs, dtype=np.int64).reshape(-1))
+    hbs = np.ascontiguousarray(np.array(hbatches, dtype=np.int64).reshape(-1))
+    if fused and (len(segs) > 64 or len(hbatches) > 16):
+        fused = False
     with torch.cuda.device(M.device):
         stream = torch.cuda.current_stream(M.device).cuda_stream
         for _ in range(nepochs):
             for B, lo, hi in plan:
+                if fused and hi > lo:
+                    q = []
+                    if similar_fill_quirk:  # with the parameters of this step's forward
+                        q = [torch.log(state.theta[s0:s1].abs()).sum() for s0, s1 in ss_a]
+                    _lib.check(L.enf_whitening_step(
+                        dt, D, hi - lo, M[:, lo:hi].data_ptr(), _ld(M), state.layers(), len(state.trafos),
+                        state.theta.data_ptr(), state.acc.data_ptr(), runs.ctypes.data, len(segs), hbs.ctypes.data,
+                        len(hbatches), optimizer.eta, optimizer.epsilon, hist[step:].data_ptr(), ws.data_ptr(),
+                        ws.numel() * 8, stream))
+                    for t in q:
+                        hist[step:step + 1] += t
+                    step += 1
+                    continue
                 out.zero_()
                 if hi > lo:
                     Xb = M[:, lo:hi]

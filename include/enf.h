@@ -133,6 +133,19 @@ enf_status enf_flow_negll_grad(enf_dtype dtype, int64_t D, int64_t N, const void
 enf_status enf_adagrad_step(enf_dtype dtype, int64_t count, void* params, void* acc,
                             const void* grad, double grad_scale, double eta, double epsilon,
                             void* hip_stream);
+/* One single-GPU optimize_whitening minibatch step, fused (src/optimize_whitening.jl:36-42):
+ * the negll and gradient of the N samples X (as enf_flow_negll_grad; the layer parameter pointers
+ * point into theta), then *loss_out = negll / N (device double), ADAGrad (eta, epsilon) with
+ * g = gradient / N on the nruns ranges [runs[2i], runs[2i+1]) of theta, and the re-normalisation
+ * of the nhb Householder column batches (hbatches[3i..3i+2] = offset in theta, column count, column
+ * stride). Identical arithmetic to enf_flow_negll_grad + enf_adagrad_step per range +
+ * enf_householder_normalize_strided per batch on one rank, in three launches instead of eight.
+ * Multi-GPU training keeps the separate calls (the all-reduce sits between gradient and update). */
+enf_status enf_whitening_step(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
+                              const enf_layer* layers, int32_t nlayers, void* theta, void* acc,
+                              const int64_t* runs, int32_t nruns, const int64_t* hbatches, int32_t nhb,
+                              double eta, double epsilon, double* loss_out, void* workspace,
+                              size_t workspace_bytes, void* hip_stream);
 /* HouseholderTrafo functor reconstruction (src/householder_trafo.jl:134-146): normalise each of
  * the k columns of the D x k device matrix V to unit 2-norm, in place. */
 enf_status enf_householder_normalize(enf_dtype dtype, int64_t D, int64_t k, void* V,

@@ -290,3 +290,63 @@ def test_optimize_whitening_similar_fill_quirk(enf, gpu):
     n0, _ = enf.mvnormal_negll_trafograd(f, colmajor_cuda(X[:, :300]), similar_fill_quirk=True)
     assert abs(b.negll_history[0] - n0) < 1e-12 * abs(n0)
     assert abs(b.negll_history[0] - a.negll_history[0] - np.sum(np.log(np.abs(layers[0][1][0])))) < 1e-12
+
+
+@pytest.mark.parametrize("kind", ["hj_f32", "mixed_f64", "mixed_f32"])
+def test_whitening_step_fused_equals_unfused(enf, gpu, kind):
+    """enf_whitening_step == enf_flow_negll_grad + enf_adagrad_step per run +
+    enf_householder_normalize_strided per batch, bit for bit in the parameters and the ADAGrad state
+    over 6 consecutive steps (the recorded loss to one rounding)."""
+    import torch
+
+    from euclidiannormalizingflows_jl_amd import _lib
+    from euclidiannormalizingflows_jl_amd.train import FlowState, _workspace, householder_batches, trainable_runs
+
+    rng = np.random.default_rng(17)
+    dtype = np.float64 if kind.endswith("f64") else np.float32
+    if kind == "hj_f32":
+        D = 32
+        layers = []
+        for _ in range(4):
+            layers += [(5, rand_params(rng, 5, D, dtype)), (3, rand_params(rng, 3, D, dtype))]
+    else:
+        D = 8
+        layers = [(0, rand_params(rng, 0, D, dtype)), (5, rand_params(rng, 5, D, dtype, K=3)),
+                  (1, rand_params(rng, 1, D, dtype)), (3, rand_params(rng, 3, D, dtype)),
+                  (2, rand_params(rng, 2, D, dtype)), (5, rand_params(rng, 5, D, dtype))]
+    X = colmajor_cuda((0.5 * rng.standard_normal((D, 30_011))).astype(dtype))
+    f = make_flow(enf, layers)
+    tdt = torch.float64 if dtype == np.float64 else torch.float32
+    L = _lib.lib()
+    dt = _lib.ENF_F64 if dtype == np.float64 else _lib.ENF_F32
+    opt = enf.ADAGrad()
+    states = [FlowState(f, D, tdt, X.device, opt) for _ in range(2)]
+    segs = trainable_runs(states[0])
+    hb = householder_batches(states[0])
+    runs = np.ascontiguousarray(np.array(segs, dtype=np.int64).reshape(-1))
+    hbs = np.ascontiguousarray(np.array(hb, dtype=np.int64).reshape(-1))
+    N = X.shape[1]
+    ws = _workspace(states[0], N)
+    out = torch.zeros(1 + states[0].nparams, dtype=tdt, device=X.device)
+    loss = torch.zeros(6, dtype=torch.float64, device=X.device)
+    for it in range(6):
+        sa, sb = states
+        _lib.check(L.enf_whitening_step(dt, D, N, X.data_ptr(), X.stride(1), sa.layers(), len(sa.trafos),
+                                        sa.theta.data_ptr(), sa.acc.data_ptr(), runs.ctypes.data, len(segs),
+                                        hbs.ctypes.data, len(hb), opt.eta, opt.epsilon, loss[it:].data_ptr(),
+                                        ws.data_ptr(), ws.numel() * 8, None))
+        out.zero_()
+        _lib.check(L.enf_flow_negll_grad(dt, D, N, X.data_ptr(), X.stride(1), sb.layers(), len(sb.trafos),
+                                         out.data_ptr(), ws.data_ptr(), ws.numel() * 8, None))
+        ref_loss = float((out[0:1] / N).double())
+        for s0, s1 in segs:
+            _lib.check(L.enf_adagrad_step(dt, s1 - s0, sb.theta[s0:].data_ptr(), sb.acc[s0:].data_ptr(),
+                                          out[1:][s0:].data_ptr(), 1.0 / N, opt.eta, opt.epsilon, None))
+        for off, k, ldv in hb:
+            _lib.check(L.enf_householder_normalize_strided(dt, D, k, sb.theta[off:].data_ptr(), ldv, None))
+        torch.cuda.synchronize()
+        # the fused step divides (negll / N, as the reference's `/`); torch's out / N multiplies by
+        # the reciprocal: equal up to one rounding of T
+        assert abs(float(loss[it]) - ref_loss) <= 2 * np.finfo(dtype).eps * abs(ref_loss), (it, float(loss[it]), ref_loss)
+        assert torch.equal(sa.theta, sb.theta), it
+        assert torch.equal(sa.acc, sb.acc), it
