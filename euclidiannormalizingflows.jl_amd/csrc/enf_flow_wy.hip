@@ -124,6 +124,14 @@ __device__ void build_dense(const FlowArgs& a, const Step& st, T* __restrict__ i
   for (int i = 0; i < NC; ++i) img[a_index<T, D>(row, c0 + i)] = (T)q[i];
 }
 
+// sum over the KH lanes of a column
+template <typename T, int KH, int COLS>
+__device__ __forceinline__ T part_sum(T v) {
+  if constexpr (KH >= 2) v += __shfl_xor(v, COLS);
+  if constexpr (KH >= 4) v += __shfl_xor(v, 2 * COLS);
+  return v;
+}
+
 // Y = Q x for the lane's rows: NB accumulators, R k-steps each, A read from LDS per V steps.
 template <typename T, int D>
 __device__ __forceinline__ void dense_apply(const T* __restrict__ img, T (&x)[WYC<T, D>::NF][1][WYC<T, D>::V]) {
@@ -143,21 +151,24 @@ __device__ __forceinline__ void dense_apply(const T* __restrict__ img, T (&x)[WY
 #pragma unroll
       for (int m = 0; m < NB; ++m) acc[m] = W::mfma(av[m][e], x[sv][0][e], acc[m]);
   }
+  // Non-finite input: reflection by reflection (the reference), an Inf makes the first dot +-Inf,
+  // its own row Inf - Inf = NaN and, from the second reflection on, every row NaN; Q x would give
+  // a mix of +-Inf and NaN. nf = sum of x*0 over the column is 0, or NaN if any input is Inf/NaN,
+  // and adding it reproduces the all-NaN column (a step holds >= 2 reflections unless it is the
+  // tail chunk of a longer chain, whose input is then already all-finite or all-NaN).
+  T nf = (T)0;
+#pragma unroll
+  for (int f = 0; f < R / V; ++f)
+#pragma unroll
+    for (int e = 0; e < V; ++e) nf = fma(x[f][0][e], (T)0, nf);
+  nf = part_sum<T, W::KH, W::COLS>(nf);
 #pragma unroll
   for (int m = 0; m < NB; ++m)
 #pragma unroll
     for (int r = 0; r < RPB; ++r) {
       const int row = m * RPB + r;
-      x[row / V][0][row % V] = acc[m][r];
+      x[row / V][0][row % V] = acc[m][r] + nf;
     }
-}
-
-// sum over the KH lanes of a column
-template <typename T, int KH, int COLS>
-__device__ __forceinline__ T part_sum(T v) {
-  if constexpr (KH >= 2) v += __shfl_xor(v, COLS);
-  if constexpr (KH >= 4) v += __shfl_xor(v, 2 * COLS);
-  return v;
 }
 
 // one reflection y = x - vh (vh'x) (householder_trafo.jl:8-11) on the lane's R rows

@@ -100,3 +100,24 @@ def test_dense_householder_orthogonality_full_size(enf, gpu):
     assert float(((ny - nx).abs() / nx).max()) < 3e-6
     X2 = enf.inverse(f)(Y)
     assert float(((X2 - X).abs().amax(dim=0) / X.abs().amax(dim=0)).max()) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_dense_householder_nonfinite_columns(enf, gpu, oracle, dtype):
+    """Columns with +-Inf / NaN entries come out as the reference's reflection chain makes them
+    (all NaN from the second reflection on); the other columns of the tile are unaffected."""
+    rng = np.random.default_rng(23)
+    D = 32
+    layers = [(5, rand_params(rng, 5, D, dtype, K=12)), (3, rand_params(rng, 3, D, dtype))]
+    X = np.asfortranarray(rng.standard_normal((D, 300)).astype(dtype))
+    X[3, 5] = np.inf
+    X[0, 40] = -np.inf
+    X[31, 41] = np.nan
+    X[7, 299] = np.inf
+    Y, L = enf.with_logabsdet_jacobian(make_flow(enf, layers), colmajor_cuda(X))
+    Y, L = to_np(Y), to_np(L)
+    Yr, Lr = oracle.flow_apply(layers, X)
+    for c in (5, 40, 41, 299):
+        assert np.isnan(Yr[:, c]).all() and np.isnan(Y[:, c]).all(), c
+    assert np.array_equal(np.isnan(L), np.isnan(Lr.reshape(L.shape)))
+    check_vs_oracle(oracle, layers, X, Y, L, dtype, what="non-finite columns")
