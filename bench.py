@@ -166,6 +166,7 @@ def main():
     bytes_per_launch = N * (2 * D + 1) * esz  # read X, write Y, write ladj
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic, valu = pmc_evidence(D, N, args, kern_ms)
+    copy_gbs = copy_ceiling(X, Y, stream)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(layers, D, np_dtype, args.cpu_samples)
@@ -190,13 +191,30 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": kern_ms, "kernel_ms_max_rank": kern_ms_max,
-                         "algorithmic_bytes_per_launch": bytes_per_launch},
+                         "algorithmic_bytes_per_launch": bytes_per_launch,
+                         "copy_ceiling_GBps": copy_gbs, "frac_of_copy_ceiling": achieved / copy_gbs},
             "valu": valu,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def copy_ceiling(X, Y, stream, reps=10):
+    """Practical streaming ceiling of this GPU for the same bytes (confirm the HBM
+    peak with a copy): torch's device copy of X into Y (N*D values read and written), timed with HIP
+    events on the launch stream. Y is overwritten (after the timed steps)."""
+    Y.copy_(X)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        Y.copy_(X)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return 2 * X.numel() * X.element_size() / (ms * 1e-3) / 1e9
 
 
 def cpu_baseline(layers, D, np_dtype, nsamp):
