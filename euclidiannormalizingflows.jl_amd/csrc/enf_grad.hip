@@ -415,29 +415,39 @@ template <typename T>
 __device__ __forceinline__ void finalize_totals(const ReduceArgs& r) {
   double* tot = r.tot;
   const int64_t n = 1 + (int64_t)r.nparams;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // Householder columns h = w, w + 4, ... of this wave: their entries (D <= 64: one per lane) and
+  // norms, loaded while the slices are summed (they do not depend on the totals)
+  constexpr int kPerWave = (kMaxGradSteps + 3) / 4;
+  double vh[kPerWave], nrm[kPerWave];
+#pragma unroll
+  for (int j = 0; j < kPerWave; ++j) {
+    const int h = w + 4 * j;
+    vh[j] = (h < r.nh && lane < r.D) ? (double)((const T*)r.hcol[h])[lane] : 0.0;
+  }
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {  // the slices in order, into slice 0
     double t = tot[i];
     for (int s = 1; s < kSumSlices; ++s) t += tot[s * n + i];
     tot[i] = t;
   }
+#pragma unroll
+  for (int j = 0; j < kPerWave; ++j) {
+    double vv = vh[j] * vh[j];
+    for (int m = 32; m >= 1; m >>= 1) vv += __shfl_xor(vv, m);
+    nrm[j] = sqrt(vv);
+  }
   __syncthreads();
   // Householder: dS/dw = -sqrt2 * G;  dS/dv = (dS/dw - w (dS/dw . w)) / |v|  (householder_trafo.jl:32)
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    for (int h = 0; h < r.nh; ++h) {
-      const T* v = (const T*)r.hcol[h];
-      double* gw = tot + 1 + r.hoff[h];
-      double vv = 0.0, wd = 0.0;
-      for (int d = lane; d < r.D; d += 64) vv += (double)v[d] * (double)v[d];
-      for (int m = 32; m >= 1; m >>= 1) vv += __shfl_xor(vv, m);
-      const double nrm = sqrt(vv);
-      for (int d = lane; d < r.D; d += 64) wd += -1.4142135623730951 * gw[d] * ((double)v[d] / nrm);
-      for (int m = 32; m >= 1; m >>= 1) wd += __shfl_xor(wd, m);
-      for (int d = lane; d < r.D; d += 64) {
-        const double dw = -1.4142135623730951 * gw[d];
-        gw[d] = (dw - ((double)v[d] / nrm) * wd) / nrm;
-      }
-    }
+#pragma unroll
+  for (int j = 0; j < kPerWave; ++j) {
+    const int h = w + 4 * j;
+    if (h >= r.nh) break;  // wave-uniform
+    double* gw = tot + 1 + r.hoff[h];
+    const double g = lane < r.D ? gw[lane] : 0.0;
+    const double wv = vh[j] / nrm[j];
+    double wd = -1.4142135623730951 * g * wv;
+    for (int m = 32; m >= 1; m >>= 1) wd += __shfl_xor(wd, m);
+    if (lane < r.D) gw[lane] = (-1.4142135623730951 * g - wv * wd) / nrm[j];
   }
   __syncthreads();
 }

@@ -330,6 +330,7 @@ __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0,
     }
   }
   float zs[NP][KU][V], ds[NP][KU];
+  float ss[NP][KU][V], ls[NP][KU][V];  // sqrt(1 + z^2) and asinh(z)/ln2 of the forward, for the backward
   float lad[KU] = {};
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
@@ -354,8 +355,9 @@ __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0,
       for (int e = 0; e < V; ++e) {
         zs[p][u][e] = fmaf(fmaf(-ds[p][u], vh[e], x[u][e]), il[e], nxil[e]);
         q[e] = fmaf(zs[p][u][e], zs[p][u][e], 1.f);
-        const float Lz = copysignf(hw_log2(fabsf(zs[p][u][e]) + hw_sqrt(q[e])), zs[p][u][e]);
-        x[u][e] = fmaf(dl2[e], Lz, gam[e]);
+        ss[p][u][e] = hw_sqrt(q[e]);
+        ls[p][u][e] = copysignf(hw_log2(fabsf(zs[p][u][e]) + ss[p][u][e]), zs[p][u][e]);
+        x[u][e] = fmaf(dl2[e], ls[p][u][e], gam[e]);
       }
       lad[u] = fmaf(-0.5f, hw_log2((q[0] * q[1]) * (q[2] * q[3])), lad[u]);
     }
@@ -392,10 +394,8 @@ __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0,
 #pragma unroll
       for (int e = 0; e < V; ++e) {
         const float z = zs[p][u][e];
-        const float q = fmaf(z, z, 1.f);
-        const float s = hw_sqrt(q);
-        const float rs = hw_rcp(s);
-        const float Lz = copysignf(hw_log2(fabsf(z) + s), z);
+        const float rs = hw_rcp(ss[p][u][e]);
+        const float Lz = ls[p][u][e];
         acc[p][1][e] += g[u][e];
         acc[p][2][e] = fmaf(g[u][e], Lz, acc[p][2][e]);
         const float dz = fmaf(g[u][e] * del[e], rs, z * (rs * rs) * vm[u]);
