@@ -308,9 +308,28 @@ __global__ __launch_bounds__(256) void hj_grad_kernel(HJGradArgs a) {
 // registers between its forward and backward, and the per-lane gradient partials accumulate in
 // registers over all of the wave's tiles (acc[pair][param][row]); one cross-slot reduction per
 // wave at the end instead of one per tile and pair. Same arithmetic per element as grad_tile.
+// the lane's fragments of a tile (zeros past N)
+template <int D, int KU>
+__device__ __forceinline__ void grad_load_reg(const HJGradArgs& a, int64_t col0, int lane, float (&x)[KU][4]) {
+  using L = GL<D, KU>;
+  constexpr int G = L::G, S = L::S;
+#pragma unroll
+  for (int u = 0; u < KU; ++u) {
+    const int64_t c = col0 + (int64_t)u * S + lane / G;
+    if (c < a.N) {
+      const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.X + c * D + 4 * (lane % G)));
+      __builtin_memcpy(&x[u][0], &v4, 16);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[u][e] = 0.f;
+    }
+  }
+}
+
 template <int D, int KU, int NP, bool TAIL>
 __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0, int lane, const float* __restrict__ rec,
-                                              float (&acc)[NP][5][4], double& lossp, int& nvalid, float ctot) {
+                                              const float (&xin)[KU][4], float (&acc)[NP][5][4], double& lossp,
+                                              int& nvalid, float ctot) {
   using L = GL<D, KU>;
   constexpr int V = 4, G = L::G, S = L::S;
   const int grp = lane % G;
@@ -318,16 +337,9 @@ __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0,
   float vm[KU];
 #pragma unroll
   for (int u = 0; u < KU; ++u) {
-    const int64_t c = col0 + (int64_t)u * S + lane / G;
-    const float* src = a.X + c * D + V * grp;
-    vm[u] = (!TAIL || c < a.N) ? 1.f : 0.f;
-    if (!TAIL) {
-      const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
-      __builtin_memcpy(&x[u][0], &v4, 16);
-    } else {
+    vm[u] = (!TAIL || col0 + (int64_t)u * S + lane / G < a.N) ? 1.f : 0.f;
 #pragma unroll
-      for (int e = 0; e < V; ++e) x[u][e] = c < a.N ? src[e] : 0.f;
-    }
+    for (int e = 0; e < V; ++e) x[u][e] = xin[u][e];
   }
   float zs[NP][KU][V], ds[NP][KU];
   float ss[NP][KU][V], ls[NP][KU][V];  // sqrt(1 + z^2) and asinh(z)/ln2 of the forward, for the backward
@@ -443,9 +455,18 @@ __global__ __launch_bounds__(256) void hj_grad_reg_kernel(HJGradArgs a) {
   const int64_t ntiles = (a.N + L::TC - 1) / L::TC;
   const int64_t full = a.N / L::TC;
   const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wave);
-  for (int64_t t = wave_id; t < ntiles; t += (int64_t)gridDim.x * 4) {
-    if (t < full) grad_tile_reg<D, KU, NP, false>(a, t * L::TC, lane, rec, acc, lossp, nvalid, ctot);
-    else grad_tile_reg<D, KU, NP, true>(a, t * L::TC, lane, rec, acc, lossp, nvalid, ctot);
+  // the next tile's columns are loaded while the current one is processed
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  float xc[KU][4], xn[KU][4];
+  if (wave_id < ntiles) grad_load_reg<D, KU>(a, wave_id * L::TC, lane, xc);
+  for (int64_t t = wave_id; t < ntiles; t += stride) {
+    if (t + stride < ntiles) grad_load_reg<D, KU>(a, (t + stride) * L::TC, lane, xn);
+    if (t < full) grad_tile_reg<D, KU, NP, false>(a, t * L::TC, lane, rec, xc, acc, lossp, nvalid, ctot);
+    else grad_tile_reg<D, KU, NP, true>(a, t * L::TC, lane, rec, xc, acc, lossp, nvalid, ctot);
+#pragma unroll
+    for (int u = 0; u < KU; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xc[u][e] = xn[u][e];
   }
   // one cross-slot reduction per wave; lanes 0..G-1 then hold the row sums of their 4 rows
   float* wacc = accs + (size_t)wave * NP * 5 * D;
