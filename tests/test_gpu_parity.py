@@ -366,3 +366,33 @@ def test_host_streaming_fp64_mixed_ops(enf, gpu, oracle):
     X = np.asfortranarray(rng.standard_normal((D, N)))
     Y, L = enf.stream_with_logabsdet_jacobian(make_flow(enf, layers), X, chunk_cols=7001)
     check_vs_oracle(oracle, layers, X, Y, L, np.float64, what="host streaming fp64")
+
+
+@pytest.mark.parametrize("D", [2, 32])
+def test_fp64_asinh_wide_range(enf, gpu, oracle, D):
+    """The fp64 Johnson layer y = gamma + delta*asinh(z) (johnson_trafo.jl:31) with gamma = 0,
+    delta = 1 against libm elementwise, 1e-12 relative, over 1e-320 .. 1e308, signed zeros (0 + -0
+    is +0, as in the reference), Inf and NaN."""
+    rng = np.random.default_rng(5)
+    v = np.concatenate([np.logspace(-320, 308, 3000), rng.uniform(0.2, 0.3, 500), rng.uniform(9e3, 1.1e4, 500),
+                        rng.standard_normal(1000) * 10, [0.0, 5e-324, 1e-300, 0.25, 0.2526, 1e4, 1.0000001e4,
+                                                          1.7e308, np.inf, np.nan]])
+    v = np.concatenate([v, -v])
+    n = (v.size + D - 1) // D * D
+    x = np.zeros(n)
+    x[:v.size] = v
+    X = np.asfortranarray(x.reshape(-1, D).T)
+    one = np.ones(D)
+    layers = [(3, [np.zeros(D), one, np.zeros(D), one])]  # y = asinh(x)
+    Y, L = enf.with_logabsdet_jacobian(make_flow(enf, layers), colmajor_cuda(X))
+    Y = to_np(Y)
+    ref = 0.0 + 1.0 * np.arcsinh(X)
+    fin = np.isfinite(ref) & (ref != 0)
+    assert np.all(np.abs(Y[fin] - ref[fin]) <= 1e-12 * np.abs(ref[fin]))
+    assert np.array_equal(np.isnan(Y), np.isnan(ref))
+    inf = np.isinf(ref)
+    assert np.array_equal(Y[inf], ref[inf])
+    zero = ref == 0
+    assert np.array_equal(np.signbit(Y[zero]), np.signbit(ref[zero]))
+    Yr, Lr = oracle.flow_apply(layers, X)
+    assert np.array_equal(np.isnan(to_np(L)).reshape(-1), np.isnan(Lr).reshape(-1))
