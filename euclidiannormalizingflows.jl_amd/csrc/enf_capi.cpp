@@ -210,7 +210,7 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
   // flatten into steps: one per transform, one per Householder reflection column
   // (dense-Householder path: a chained HouseholderTrafo with k >= wy_min_k() reflections becomes
   // OP_DENSE steps of <= D reflections each, col = first column | count << 16)
-  const bool frag = enf::frag_path(D, ldx, ldy, X, Y) && enf::frag_path(D, ldy, ldy, Y, Y);
+  const bool frag = enf::frag_path(D, ldx, ldy, X, Y, elem) && enf::frag_path(D, ldy, ldy, Y, Y, elem);
   bool wy = false;
   if (enf::wy_supported(D, frag))
     for (int32_t l = 0; l < nlayers; ++l)

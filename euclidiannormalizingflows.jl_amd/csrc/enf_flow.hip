@@ -268,6 +268,12 @@ static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, cons
     case 64:
       if constexpr (std::is_same_v<T, float>) return launch_frag<T, 64, 4, LADJ>(a, lds, st, dev);
       else return launch_frag<T, 64, 2, LADJ>(a, lds, st, dev);
+    case 128:
+      if constexpr (std::is_same_v<T, float>) return launch_frag<T, 128, 4, LADJ>(a, lds, st, dev);
+      else return launch_frag<T, 128, 2, LADJ>(a, lds, st, dev);
+    case 256:
+      if constexpr (std::is_same_v<T, float>) return launch_frag<T, 256, 4, LADJ>(a, lds, st, dev);
+      break;
     default: break;
   }
   return hipErrorInvalidValue;

@@ -69,10 +69,12 @@ __host__ __device__ constexpr int record_width(int op) {
 }
 inline int record_width_host(int op) { return record_width(op); }
 
-// The fragment (fast) kernel handles D in {1,2,4,...,64}, contiguous columns (ld == D) and
-// 16-byte aligned X / Y; everything else runs on the generic kernel.
-inline bool frag_path(int64_t D, int64_t ldx, int64_t ldy, const void* X, const void* Y) {
-  const bool pow2 = D >= 1 && D <= 64 && (D & (D - 1)) == 0;
+// The fragment (fast) kernel handles power-of-two D up to 256 (fp32) / 128 (fp64: at most 64 lanes
+// per column), contiguous columns (ld == D) and 16-byte aligned X / Y; everything else runs on the
+// generic kernel.
+inline bool frag_path(int64_t D, int64_t ldx, int64_t ldy, const void* X, const void* Y, size_t elem) {
+  const int64_t dmax = elem == 4 ? 256 : 128;
+  const bool pow2 = D >= 1 && D <= dmax && (D & (D - 1)) == 0;
   return pow2 && ldx == D && ldy == D && ((((uintptr_t)X) | ((uintptr_t)Y)) & 15) == 0;
 }
 

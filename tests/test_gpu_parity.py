@@ -27,7 +27,7 @@ def test_golden_flow(enf, gpu, oracle, name):
     assert_as_accurate(to_np(Y), to_np(L), Yt, Lt, Yx, Lx, X.dtype, what=name)
 
 
-DS = [1, 2, 3, 4, 5, 8, 16, 32, 64, 100]
+DS = [1, 2, 3, 4, 5, 8, 16, 32, 64, 100, 128, 256]
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
@@ -50,7 +50,7 @@ def test_single_op_vs_oracle(enf, gpu, oracle, dtype, op, D):
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-@pytest.mark.parametrize("D", [2, 32, 64])
+@pytest.mark.parametrize("D", [2, 32, 64, 128, 256])
 def test_config3_pattern_vs_oracle(enf, gpu, oracle, dtype, D):
     """J4∘H4∘…∘J1∘H1 (SURVEY.md §8(d) config 3 pattern) on 200k samples."""
     rng = np.random.default_rng(7 + D)
