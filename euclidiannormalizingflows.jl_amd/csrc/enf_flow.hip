@@ -107,6 +107,77 @@ __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
 // generic kernel: any D, any leading dimensions, any alignment. One column per lane; the
 // column lives in Y (copied from X first), every step re-reads it from global memory.
 // ------------------------------------------------------------------------------------------
+// The whole step program on one column y[0 .. D-1] (global memory or an LDS image), in the
+// reference's elementwise order; returns the column's ladj in natural-log units (without the
+// constant part ctot).
+template <typename T>
+__device__ __forceinline__ double generic_column(const FlowArgs& a, const T* __restrict__ rec, T* y, int D) {
+  double acc = 0.0;  // natural-log units
+  for (int s = 0; s < a.nsteps; ++s) {
+    const int op = a.steps[s].op;
+    const T* r = rec + a.steps[s].off;
+    if (op == OP_HOUSEHOLDER) {
+      T dot = 0;
+      for (int d = 0; d < D; ++d) dot = fma(r[d], y[d], dot);
+      for (int d = 0; d < D; ++d) y[d] = fma(-dot, r[d], y[d]);
+    } else if (op == OP_SCALESHIFT) {
+      for (int d = 0; d < D; ++d) y[d] = fma(y[d], r[2 * d], r[2 * d + 1]);
+    } else if (op == OP_JOHNSON) {
+      for (int d = 0; d < D; ++d) {
+        if constexpr (std::is_same_v<T, float>) {
+          const YL r2 = johnson_fwd_f32_slow((y[d] - r[4 * d + 2]) * r[4 * d + 3], r[4 * d], r[4 * d + 1]);
+          y[d] = r2.y;
+          acc += (double)r2.l * kLn2;
+        } else {
+          const double z = (y[d] - r[4 * d + 2]) * r[4 * d + 3];
+          y[d] = fma(r[4 * d + 1], asinh(z), r[4 * d]);
+          acc -= 0.5 * log1p(z * z);
+        }
+      }
+    } else if (op == OP_JOHNSON_INV) {
+      for (int d = 0; d < D; ++d) {
+        if constexpr (std::is_same_v<T, float>) {
+          const float w = (y[d] - r[4 * d]) * r[4 * d + 1];
+          const float sh = sinhf(w);
+          y[d] = fmaf(r[4 * d + 3], sh, r[4 * d + 2]);
+          acc += 0.5 * log1p((double)sh * sh);
+        } else {
+          const double w = (y[d] - r[4 * d]) * r[4 * d + 1];
+          const double sh = sinh(w);
+          y[d] = fma(r[4 * d + 3], sh, r[4 * d + 2]);
+          acc += 0.5 * log1p(sh * sh);
+        }
+      }
+    } else if (op == OP_CENTER_STRETCH || op == OP_CENTER_CONTRACT) {
+      for (int d = 0; d < D; ++d) {
+        const T* rr = r + 8 * d;
+        double av, bv, c;
+        if constexpr (std::is_same_v<T, float>) {
+          av = rr[6]; bv = rr[7]; c = rr[1];
+        } else {
+          av = rr[0]; bv = rr[1]; c = rr[2];
+        }
+        const T xv = y[d];
+        if (op == OP_CENTER_STRETCH) {
+          const T ex = (T)exp(fabs((T)bv * xv));
+          const T ome = (T)1 - ex;
+          const T inner = ((T)sqrt(ome * ome * (T)exp(2.0 * bv * av) + (T)4 * ex) - ome * (T)exp(bv * av)) / (T)2;
+          const T sg = xv > (T)0 ? (T)1 : (xv < (T)0 ? (T)-1 : xv);
+          const T yv = sg * (T)log(inner) / (T)bv + (T)c;
+          y[d] = yv;
+          const double yu = (double)yv - c;
+          acc -= log(fabs(1.0 / (1.0 + exp(-bv * (yu - av))) + 1.0 / (1.0 + exp(bv * (yu + av)))));
+        } else {
+          const double xu = (double)xv - c;
+          y[d] = (T)((log(1.0 + exp(bv * (xu - av))) - log(1.0 + exp(-bv * (xu + av)))) / bv);
+          acc += log(fabs(1.0 / (1.0 + exp(-bv * (xu - av))) + 1.0 / (1.0 + exp(bv * (xu + av)))));
+        }
+      }
+    }
+  }
+  return acc;
+}
+
 template <typename T, bool LADJ>
 __global__ __launch_bounds__(256) void flow_generic_kernel(FlowArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -124,74 +195,71 @@ __global__ __launch_bounds__(256) void flow_generic_kernel(FlowArgs a) {
     T* y = Y + j * a.ldy;
     if (x != y)
       for (int d = 0; d < D; ++d) y[d] = x[d];
-    double acc = 0.0;  // natural-log units
-    for (int s = 0; s < a.nsteps; ++s) {
-      const int op = a.steps[s].op;
-      const T* r = rec + a.steps[s].off;
-      if (op == OP_HOUSEHOLDER) {
-        T dot = 0;
-        for (int d = 0; d < D; ++d) dot = fma(r[d], y[d], dot);
-        for (int d = 0; d < D; ++d) y[d] = fma(-dot, r[d], y[d]);
-      } else if (op == OP_SCALESHIFT) {
-        for (int d = 0; d < D; ++d) y[d] = fma(y[d], r[2 * d], r[2 * d + 1]);
-      } else if (op == OP_JOHNSON) {
-        for (int d = 0; d < D; ++d) {
-          if constexpr (std::is_same_v<T, float>) {
-            const YL r2 = johnson_fwd_f32_slow((y[d] - r[4 * d + 2]) * r[4 * d + 3], r[4 * d], r[4 * d + 1]);
-            y[d] = r2.y;
-            acc += (double)r2.l * kLn2;
-          } else {
-            const double z = (y[d] - r[4 * d + 2]) * r[4 * d + 3];
-            y[d] = fma(r[4 * d + 1], asinh(z), r[4 * d]);
-            acc -= 0.5 * log1p(z * z);
-          }
-        }
-      } else if (op == OP_JOHNSON_INV) {
-        for (int d = 0; d < D; ++d) {
-          if constexpr (std::is_same_v<T, float>) {
-            const float w = (y[d] - r[4 * d]) * r[4 * d + 1];
-            const float sh = sinhf(w);
-            y[d] = fmaf(r[4 * d + 3], sh, r[4 * d + 2]);
-            acc += 0.5 * log1p((double)sh * sh);
-          } else {
-            const double w = (y[d] - r[4 * d]) * r[4 * d + 1];
-            const double sh = sinh(w);
-            y[d] = fma(r[4 * d + 3], sh, r[4 * d + 2]);
-            acc += 0.5 * log1p(sh * sh);
-          }
-        }
-      } else if (op == OP_CENTER_STRETCH || op == OP_CENTER_CONTRACT) {
-        for (int d = 0; d < D; ++d) {
-          const T* rr = r + 8 * d;
-          double av, bv, c;
-          if constexpr (std::is_same_v<T, float>) {
-            av = rr[6]; bv = rr[7]; c = rr[1];
-          } else {
-            av = rr[0]; bv = rr[1]; c = rr[2];
-          }
-          const T xv = y[d];
-          if (op == OP_CENTER_STRETCH) {
-            const T ex = (T)exp(fabs((T)bv * xv));
-            const T ome = (T)1 - ex;
-            const T inner = ((T)sqrt(ome * ome * (T)exp(2.0 * bv * av) + (T)4 * ex) - ome * (T)exp(bv * av)) / (T)2;
-            const T sg = xv > (T)0 ? (T)1 : (xv < (T)0 ? (T)-1 : xv);
-            const T yv = sg * (T)log(inner) / (T)bv + (T)c;
-            y[d] = yv;
-            const double yu = (double)yv - c;
-            acc -= log(fabs(1.0 / (1.0 + exp(-bv * (yu - av))) + 1.0 / (1.0 + exp(bv * (yu + av)))));
-          } else {
-            const double xu = (double)xv - c;
-            y[d] = (T)((log(1.0 + exp(bv * (xu - av))) - log(1.0 + exp(-bv * (xu + av)))) / bv);
-            acc += log(fabs(1.0 / (1.0 + exp(-bv * (xu - av))) + 1.0 / (1.0 + exp(bv * (xu + av)))));
-          }
-        }
-      }
-    }
+    const double acc = generic_column<T>(a, rec, y, D);
     if (LADJ) {
       T* ladj = (T*)a.ladj;
       const T v = (T)(ctot + acc);
       ladj[j] = a.accumulate ? ladj[j] + v : v;
     }
+  }
+}
+
+// LDS-staged generic kernel (any D whose tile image fits, any leading dimensions and alignment):
+// a wave moves a tile of CT columns between HBM and its LDS image with coalesced accesses
+// (consecutive lanes on consecutive elements: element-linear over the whole tile when the columns
+// are contiguous, column by column otherwise), lane c runs the program on column c of the image
+// (row stride DP = D rounded up to odd: conflict-free banks), and the tile goes back the same way.
+// magic = ceil(2^32 / D): c = umulhi(i, magic) = i / D exactly for i < CT * D (CT * D <= 2^14).
+template <typename T, bool LADJ>
+__global__ __launch_bounds__(256) void flow_lds_kernel(FlowArgs a, int ct, int dp, uint32_t magic) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* stepc = reinterpret_cast<double*>(smem);
+  double* ctotp = stepc + kMaxSteps;
+  T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
+  build_program<T, 0, 1>(a, rec, stepc, ctotp);
+  const double ctot = *ctotp;
+  const int D = a.D;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  T* img = reinterpret_cast<T*>(smem + a.img_off) + (size_t)wave * ct * dp;
+  const T* __restrict__ X = (const T*)a.X;
+  T* __restrict__ Y = (T*)a.Y;
+  const int64_t ntiles = (a.N + ct - 1) / ct;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < ntiles; t += (int64_t)gridDim.x * 4) {
+    const int64_t c0 = t * ct;
+    const int nc = (int)(a.N - c0 < ct ? a.N - c0 : ct);
+    if (a.ldx == D) {
+      const T* x = X + c0 * D;
+      for (int i = lane; i < nc * D; i += 64) {
+        const int c = (int)__umulhi((uint32_t)i, magic);
+        img[c * dp + (i - c * D)] = x[i];
+      }
+    } else {
+      for (int c = 0; c < nc; ++c)
+        for (int r = lane; r < D; r += 64) img[c * dp + r] = X[(c0 + c) * a.ldx + r];
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    double acc = 0.0;
+    if (lane < nc) acc = generic_column<T>(a, rec, img + lane * dp, D);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (a.ldy == D) {
+      T* y = Y + c0 * D;
+      for (int i = lane; i < nc * D; i += 64) {
+        const int c = (int)__umulhi((uint32_t)i, magic);
+        y[i] = img[c * dp + (i - c * D)];
+      }
+    } else {
+      for (int c = 0; c < nc; ++c)
+        for (int r = lane; r < D; r += 64) Y[(c0 + c) * a.ldy + r] = img[c * dp + r];
+    }
+    if (LADJ && lane < nc) {
+      T* ladj = (T*)a.ladj;
+      const T v = (T)(ctot + acc);
+      ladj[c0 + lane] = a.accumulate ? ladj[c0 + lane] + v : v;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
   }
 }
 
@@ -295,6 +363,36 @@ hipError_t launch_flow(const FlowArgs& a, bool f64, hipStream_t st, const Device
                   : lm == 1 ? dispatch_D<double, 1>(a, lds, st, dev) : dispatch_D<double, 2>(a, lds, st, dev);
     return lm == 0 ? dispatch_D<float, 0>(a, lds, st, dev)
          : lm == 1 ? dispatch_D<float, 1>(a, lds, st, dev) : dispatch_D<float, 2>(a, lds, st, dev);
+  }
+  // LDS-staged generic kernel when a tile of >= 16 columns fits 16 KB per wave (ENF_NO_LDS_GENERIC=1:
+  // the one-column-per-lane kernel)
+  static const int no_lds = env_int("ENF_NO_LDS_GENERIC", 0);
+  static const size_t wave_kb = (size_t)env_int("ENF_LDS_GENERIC_KB", 16) * 1024;  // image bytes per wave
+  const int dp = (a.D | 1);
+  int ct = 64;
+  while (ct > 8 && (size_t)ct * dp * elem > wave_kb) ct >>= 1;
+  if (!no_lds && a.D >= 1 && (size_t)ct * dp * elem <= wave_kb && ct >= 16 && (int64_t)ct * a.D <= (1 << 14)) {
+    FlowArgs b = a;
+    b.img_off = (int32_t)((lds + 15) / 16 * 16);
+    const size_t ldsb = (size_t)b.img_off + 4 * (size_t)ct * dp * elem;
+    const uint32_t magic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)a.D - 1) / (uint64_t)a.D);
+    const void* k = f64 ? (ladj ? (const void*)&flow_lds_kernel<double, true> : (const void*)&flow_lds_kernel<double, false>)
+                        : (ladj ? (const void*)&flow_lds_kernel<float, true> : (const void*)&flow_lds_kernel<float, false>);
+    if (ldsb > 64 * 1024) {
+      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsb);
+      if (e != hipSuccess) return e;
+    }
+    int64_t nb = 0;
+    hipError_t e = frag_grid(k, a.N, (int64_t)ct * 4, ldsb, dev, &nb);
+    if (e != hipSuccess) return e;
+    if (f64) {
+      if (ladj) hipLaunchKernelGGL((flow_lds_kernel<double, true>), dim3((unsigned)nb), dim3(256), ldsb, st, b, ct, dp, magic);
+      else hipLaunchKernelGGL((flow_lds_kernel<double, false>), dim3((unsigned)nb), dim3(256), ldsb, st, b, ct, dp, magic);
+    } else {
+      if (ladj) hipLaunchKernelGGL((flow_lds_kernel<float, true>), dim3((unsigned)nb), dim3(256), ldsb, st, b, ct, dp, magic);
+      else hipLaunchKernelGGL((flow_lds_kernel<float, false>), dim3((unsigned)nb), dim3(256), ldsb, st, b, ct, dp, magic);
+    }
+    return hipGetLastError();
   }
   int64_t blocks = (a.N + 255) / 256;
   const int64_t cap = (int64_t)dev.num_cu * 8;
