@@ -37,7 +37,8 @@ struct GradArgs {
   const void* X;
   int64_t N;
   int64_t ldx;
-  int32_t D;
+  int32_t D;        // rows of the flow
+  int32_t Dp;       // kernel rows: D rounded up to a power of two (padded rows are inert)
   int32_t nsteps;
   int32_t nlayers;
   int32_t nparams;  // gradient entries of this flow
@@ -83,12 +84,12 @@ __device__ __forceinline__ T gsum(T x) {
 // per row does a plain (non-atomic) read-modify-write -- every address has exactly one writer.
 // D >= V (CPF == 1): lanes with equal lane % G share rows; D < V: every lane holds all D rows.
 template <int G, int CPF, int SEG, typename T>
-__device__ __forceinline__ void wave_accumulate(double* __restrict__ acc, int row, T v, int lane) {
+__device__ __forceinline__ void wave_accumulate(double* __restrict__ acc, int row, T v, int lane, int nrows) {
   (void)CPF;
   (void)SEG;
 #pragma unroll
   for (int m = G; m < 64; m <<= 1) v += __shfl_xor(v, m);
-  if (lane < G) acc[row] += (double)v;
+  if (lane < G && row < nrows) acc[row] += (double)v;  // padded rows (row >= D) have no parameter
 }
 
 template <typename T>
@@ -233,11 +234,20 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
       const int row = D >= V ? i : e % D;
       for (int q = 0; q < np; ++q) {
         T v;
-        if (a.op[s] == OP_HOUSEHOLDER) {
+        if (row >= a.D) {
+          // padded row (D not a power of two): parameters that map 0 to 0 with ladj 0 (ScaleShift
+          // a = 1, b = 0; Johnson gamma = xi = 0, delta = lambda = 1; Center a = c = 0, b = 1;
+          // reflection 0), so padded rows stay 0 and add nothing to the loss or the gradients
+          const int op = a.op[s];
+          v = op == OP_HOUSEHOLDER ? (T)0
+              : op == OP_SCALESHIFT ? (q == 0 ? (T)1 : (T)0)
+              : (op == OP_JOHNSON || op == OP_JOHNSON_INV) ? ((q == 1 || q == 3) ? (T)1 : (T)0)
+              : (q == 1 ? (T)1 : (T)0);
+        } else if (a.op[s] == OP_HOUSEHOLDER) {
           // normalised reflection vector vh = v*sqrt(2/v'v) (computed per block, sum in double)
-          const T* vc = (const T*)L.p[0] + (int64_t)a.col[s] * D;
+          const T* vc = (const T*)L.p[0] + (int64_t)a.col[s] * a.D;
           double vv = 0.0;
-          for (int d = 0; d < D; ++d) vv += (double)vc[d] * (double)vc[d];
+          for (int d = 0; d < a.D; ++d) vv += (double)vc[d] * (double)vc[d];
           v = (T)((double)vc[row] * sqrt(2.0 / vv));
         } else {
           v = ((const T*)L.p[q])[row];
@@ -260,7 +270,7 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
     for (int e = 0; e < V; ++e) {
       const int64_t c = c0 + e / SEG;
       valid[e] = c < a.N;
-      x[e] = valid[e] ? ((const T*)a.X)[c * a.ldx + r0 + e % SEG] : (T)0;
+      x[e] = (valid[e] && r0 + e % SEG < a.D) ? ((const T*)a.X)[c * a.ldx + r0 + e % SEG] : (T)0;
     }
     // ---- forward, storing each step's input
     T lad[CPF];
@@ -299,7 +309,7 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
       T part = 0;
 #pragma unroll
       for (int e = 0; e < V; ++e)
-        if (valid[e]) part += (x[e] * x[e] + (T)1.8378770664093454836) / (T)2;
+        if (valid[e] && r0 + e % SEG < a.D) part += (x[e] * x[e] + (T)1.8378770664093454836) / (T)2;
 #pragma unroll
       for (int c = 0; c < CPF; ++c) {
         const T tot = gsum<G>(lad[c]);  // all lanes active (DPP)
@@ -336,7 +346,7 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
 #pragma unroll
           for (int e = 0; e < SEG; ++e) {
             const T contrib = valid[c * SEG + e] ? g[c * SEG + e] * vx + xin[c * SEG + e] * vg : (T)0;
-            wave_accumulate<G, CPF, SEG>(gacc + a.goff[s], r0 + e, contrib, lane);
+            wave_accumulate<G, CPF, SEG>(gacc + a.goff[s], r0 + e, contrib, lane, a.D);
             g[c * SEG + e] = fma(-vg, r[c * SEG + e], g[c * SEG + e]);
           }
         }
@@ -348,7 +358,7 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
           const T gx = bwd_elem<T>(op, xin[e], g[e], p, dp);
           const int row = r0 + e % SEG;
           for (int q = 0; q < np; ++q)
-            wave_accumulate<G, CPF, SEG>(gacc + a.goff[s] + q * D, row, valid[e] ? dp[q] : (T)0, lane);
+            wave_accumulate<G, CPF, SEG>(gacc + a.goff[s] + q * a.D, row, valid[e] ? dp[q] : (T)0, lane, a.D);
           g[e] = valid[e] ? gx : (T)0;
         }
       }
@@ -503,15 +513,23 @@ struct Plan {
   int blocks = 0;
 };
 
-bool grad_D_supported(int64_t D) { return D >= 1 && D <= 64 && (D & (D - 1)) == 0; }
+bool grad_D_supported(int64_t D) { return D >= 1 && D <= 64; }
+
+// kernel rows: D rounded up to a power of two
+int64_t grad_Dp(int64_t D) {
+  int64_t p = 1;
+  while (p < D) p <<= 1;
+  return p;
+}
 
 enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, int32_t nlayers, Plan& P) {
   std::memset(&P.ga, 0, sizeof P.ga);
   std::memset(&P.ra, 0, sizeof P.ra);
-  if (!grad_D_supported(D)) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: D must be a power of two <= 64");
+  if (!grad_D_supported(D)) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: D must be <= 64");
   if (nlayers > kMaxGradLayers) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: more than 16 layers");
   const int V = f64 ? 2 : 4;
-  const int nent = (int)(D > V ? D : V);
+  const int64_t Dp = grad_Dp(D);
+  const int nent = (int)(Dp > V ? Dp : V);
   int s = 0, goff = 0, roff = 0;
   for (int l = 0; l < nlayers; ++l) {
     P.ga.layers[l].op = layers[l].op;
@@ -536,6 +554,7 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
     goff += (int)D * (layers[l].op == OP_HOUSEHOLDER ? layers[l].k : grad_nparams(layers[l].op));
   }
   P.ga.D = (int32_t)D;
+  P.ga.Dp = (int32_t)Dp;
   P.ga.N = N;
   P.ga.nsteps = s;
   P.ga.nlayers = nlayers;
@@ -545,7 +564,7 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
   const size_t rbytes = ((size_t)(roff + 3) / 4) * 4 * esz;
   const size_t abytes = (size_t)4 * s * 64 * V * esz;
   P.lds = 4 * gbytes + 64 + rbytes + abytes;  // generic kernel; checked where it is launched
-  const int cols = (int)(64 / (D >= V ? D / V : 1) * (D >= V ? 1 : V / D));
+  const int cols = (int)(64 / (Dp >= V ? Dp / V : 1) * (Dp >= V ? 1 : V / Dp));
   const int64_t tiles = (N + cols - 1) / cols;
   int64_t blocks = (tiles + 3) / 4;
   DeviceInfo dev;
@@ -576,7 +595,7 @@ hipError_t launch_grad_D(const Plan& P, hipStream_t st) {
 template <typename T>
 hipError_t launch_grad(const Plan& P, hipStream_t st) {
   hipError_t e0 = hipSuccess;
-  switch (P.ga.D) {
+  switch (P.ga.Dp) {
 #define ENF_G(DD) case DD: e0 = launch_grad_D<T, DD>(P, st); break;
     ENF_G(1) ENF_G(2) ENF_G(4) ENF_G(8) ENF_G(16) ENF_G(32) ENF_G(64)
 #undef ENF_G

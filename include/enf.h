@@ -121,7 +121,7 @@ enf_status enf_flow_param_count(int64_t D, const enf_layer* layers, int32_t nlay
  * out has 1 + param_count entries and is ACCUMULATED into (zero it first). Divide by the
  * global batch size after the cross-GPU sum to obtain negll and its gradient.
  * workspace: device scratch of enf_flow_negll_grad_workspace() bytes.
- * Limits: D a power of two <= 64, at most 16 layers / 32 steps (ENF_ERR_UNSUPPORTED otherwise). */
+ * Limits: D <= 64, at most 16 layers / 32 steps (ENF_ERR_UNSUPPORTED otherwise). */
 enf_status enf_flow_negll_grad_workspace(enf_dtype dtype, int64_t D, int64_t N,
                                          const enf_layer* layers, int32_t nlayers,
                                          size_t* bytes);

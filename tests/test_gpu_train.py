@@ -45,8 +45,9 @@ def mixed_layers(rng, D, dtype):
     return [(op, rand_params(rng, op, D, dtype, K=2 if op == 5 else 1)) for op in ops]
 
 
-@pytest.mark.parametrize("D", [1, 2, 4, 8])
+@pytest.mark.parametrize("D", [1, 2, 3, 4, 5, 8, 12])
 def test_negll_grad_finite_differences(enf, gpu, oracle, D):
+    """Any D <= 64: non-powers of two run on padded kernel rows that stay inert."""
     rng = np.random.default_rng(17 + D)
     layers = mixed_layers(rng, D, np.float64)
     X = np.asfortranarray(0.8 * rng.standard_normal((D, 257)))
@@ -67,6 +68,24 @@ def test_negll_grad_finite_differences(enf, gpu, oracle, D):
     # kernel -- keep the exact derivative: compare on the scale of the whole gradient
     err = np.abs(g - fd) / (np.abs(fd) + 1e-3 * np.abs(fd).max())
     assert err.max() < 1e-5, (err.argmax(), g[err.argmax()], fd[err.argmax()])
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_optimize_whitening_odd_dimension(enf, gpu, oracle, dtype):
+    """optimize_whitening at D = 3 and 48 (padded kernel rows): the recorded negll equals the
+    oracle's loss of the parameters each step started from, and decreases."""
+    import torch
+
+    for D in (3, 48):
+        rng = np.random.default_rng(D)
+        layers = [(5, rand_params(rng, 5, D, dtype)), (3, rand_params(rng, 3, D, dtype))]
+        X = (rng.standard_normal((D, 4000)) * rng.uniform(0.5, 2, (D, 1))).astype(dtype)
+        f = make_flow(enf, layers)
+        res = enf.optimize_whitening(colmajor_cuda(X), f, enf.ADAGrad(), nbatches=1, nepochs=30)
+        ref0 = oracle_negll(oracle, layers, np.asfortranarray(X.astype(np.float64)))
+        assert abs(res.negll_history[0] - ref0) <= (1e-4 if dtype == np.float32 else 1e-10) * (abs(ref0) + 1)
+        assert res.negll_history[-1] < res.negll_history[0]
+        assert np.all(np.isfinite(res.negll_history))
 
 
 def test_negll_grad_config5_fp32_vs_fp64(enf, gpu):
