@@ -192,7 +192,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": kern_ms, "kernel_ms_max_rank": kern_ms_max,
                          "algorithmic_bytes_per_launch": bytes_per_launch,
-                         "copy_ceiling_GBps": copy_gbs, "frac_of_copy_ceiling": achieved / copy_gbs},
+                         "torch_copy_GBps": copy_gbs, "frac_of_torch_copy": achieved / copy_gbs},
             "valu": valu,
             "cpu_baseline": cpu,
         }
