@@ -130,7 +130,7 @@ __device__ __forceinline__ double generic_column(const FlowArgs& a, const T* __r
           acc += (double)r2.l * kLn2;
         } else {
           const double z = (y[d] - r[4 * d + 2]) * r[4 * d + 3];
-          y[d] = fma(r[4 * d + 1], asinh(z), r[4 * d]);
+          y[d] = fma(r[4 * d + 1], asinh64(z), r[4 * d]);
           acc -= 0.5 * log1p(z * z);
         }
       }

@@ -1,0 +1,94 @@
+// enf_math64.h -- fp64 asinh and log for the Johnson layer (johnson_trafo.jl:31,41-57) on the
+// hardware reciprocal / reciprocal-square-root seeds, branch-free.
+//
+// Why: ocml's double asinh carries its argument in double-double through an extended-precision log
+// (~193 VALU instructions per element, PMC ~255 per element and layer at config 2), which makes the
+// fp64 flows fp64-VALU bound. The reference evaluates Julia's Base.Math asinh (the FreeBSD msun
+// algorithm, ~1 ulp) and Base log; these restate the same algorithms at ~1 ulp with three
+// hardware seeds (v_rsq_f64, v_rcp_f64) refined by Newton steps instead of IEEE division / sqrt:
+//
+//   asinh |x| = log1p(a + a^2/(1 + sqrt(1 + a^2)))    a <= 2      (msun s_asinh.c, case 4)
+//             = log(a + sqrt(1 + a^2))                2 < a < 2^28 (case 3; sqrt within 1 ulp, so
+//                                                      the sum is within ~1 ulp and its log within
+//                                                      1 ulp of a value >= log 4)
+//             = log(a) + ln 2                         a >= 2^28   (case 2)
+//   (a < 2^-28 comes out as x itself: u = 1 and the carried rounding c = a.)
+//
+// log1p(f) = log(u) + c/u with u = 1 + f rounded and c its exact rounding error (TwoSum), the same
+// correction msun's log1p applies. log(u), u >= 1 finite, is msun's e_log.c reduction: u = 2^k m,
+// m in [sqrt(1/2), sqrt(2)), f = m - 1, s = f/(2 + f), log m = f - (f^2/2 - s (f^2/2 + R(s^2)))
+// with its degree-14 minimax R (coefficients Lg1..Lg7, a published constant set).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace enf {
+
+// n / d for d > 0 normal: v_rcp_f64 seed (relative error < 2^-22), one Newton step, and one
+// residual correction of the quotient (error ~ 0.5 ulp + 2^-90 relative)
+__device__ __forceinline__ double div64(double n, double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  const double q = n * r;
+  return fma(fma(-d, q, n), r, q);
+}
+
+// sqrt(q) for 1 <= q < 2^1000: v_rsq_f64 seed, one Goldschmidt step on (g, h) = (sqrt, 1/(2 sqrt)),
+// one residual correction of g (within 1 ulp)
+__device__ __forceinline__ double sqrt64_ge1(double q) {
+  const double y = __builtin_amdgcn_rsq(q);
+  double g = q * y, h = 0.5 * y;
+  const double r = fma(-g, h, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  return fma(fma(-g, g, q), h, g);
+}
+
+// log(u) for u >= 1 finite (msun e_log.c restated); u = +Inf gives +Inf, NaN gives NaN
+__device__ __forceinline__ double log64_ge1(double u) {
+  constexpr double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+                   Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+                   Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+                   Lg7 = 1.479819860511658591e-01;
+  constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  double m = __builtin_amdgcn_frexp_mant(u);  // [0.5, 1)
+  int k = __builtin_amdgcn_frexp_exp(u);
+  const bool lo = m < 0.70710678118654752440;
+  m = lo ? m + m : m;
+  k = lo ? k - 1 : k;
+  const double f = m - 1.0;
+  const double s = div64(f, 2.0 + f);
+  const double z = s * s, w = z * z;
+  const double t1 = w * fma(w, fma(w, Lg6, Lg4), Lg2);
+  const double t2 = z * fma(w, fma(w, fma(w, Lg7, Lg5), Lg3), Lg1);
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double dk = (double)k;
+  const double r = fma(dk, ln2_hi, -((hfsq - fma(s, hfsq + R, dk * ln2_lo)) - f));
+  return u < __builtin_huge_val() ? r : u;
+}
+
+// asinh(x) over the whole double range, odd (asinh(-0) = -0), +-Inf -> +-Inf, NaN -> NaN
+__device__ __forceinline__ double asinh64(double x) {
+  const double a = __builtin_fabs(x);
+  const bool huge = a >= 268435456.0;  // 2^28
+  const bool small = a <= 2.0;
+  const double s = sqrt64_ge1(fma(a, a, 1.0));  // unused when huge (may be Inf there)
+  // small: f = a + a^2/(1+s); u = 1 + f. Mid: u = a + s. Both with their TwoSum error c.
+  const double t = div64(a * a, 1.0 + s);
+  const double f = a + t;
+  const double p = small ? 1.0 : a;
+  const double qv = small ? f : s;
+  const double u0 = p + qv;
+  const double bv = u0 - p;
+  const double c0 = (p - (u0 - bv)) + (qv - bv);
+  const double u = huge ? a : u0;
+  const double c = huge ? 0.0 : c0;
+  double r = log64_ge1(u) + c * __builtin_amdgcn_rcp(u);
+  r = huge ? r + 6.93147180559945309417e-01 : r;
+  r = a < __builtin_huge_val() ? r : a;  // Inf stays Inf, NaN stays NaN
+  return __builtin_copysign(r, x);
+}
+
+}  // namespace enf

@@ -10,6 +10,7 @@
 #include <type_traits>
 
 #include "enf_frag.h"
+#include "enf_math64.h"
 #include "enf_internal.h"
 
 namespace enf {
@@ -207,22 +208,36 @@ __device__ __forceinline__ void step_johnson(Tile<T, D, U>& x, Acc<T, D, U>& acc
           }
         johnson_from_z<D, U, LADJ>(x, acc, pg, pd, zmax);
       } else {
-        // y = gamma + delta*asinh(z) (ocml double asinh); ladj: -log(prod of the fragment
-        // column's 1 + z^2)/2, one log per column segment (absolute error ~1e-16)
+        // y = gamma + delta*asinh(z) (asinh64: msun's algorithm on hardware seeds, enf_math64.h);
+        // ladj: -log(prod of the fragment column's q = 1 + z^2)/2, one log per column segment
+        // (absolute error ~1e-16). A product that overflows while its factors do not (|z| ~ 1e77
+        // and up) is summed as logs instead; an infinite q gives -Inf as the reference's
+        // log(1/sqrt(Inf)) does.
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          double prod[CPF];
+          double prod[CPF], q[V];
 #pragma unroll
           for (int c = 0; c < CPF; ++c) prod[c] = 1.0;
 #pragma unroll
           for (int e = 0; e < V; ++e) {
             const double z = (x[u][e] - px[e]) * pl[e];
-            x[u][e] = fma(pd[e], asinh(z), pg[e]);
-            prod[e / SEG] = fma(prod[e / SEG], z * z, prod[e / SEG]);
+            x[u][e] = fma(pd[e], asinh64(z), pg[e]);
+            q[e] = fma(z, z, 1.0);
+            prod[e / SEG] *= q[e];
           }
           if (LADJ)
 #pragma unroll
-            for (int c = 0; c < CPF; ++c) acc[u][c] -= 0.5 * log(prod[c]);
+            for (int c = 0; c < CPF; ++c) {
+              double l;
+              if (__builtin_expect(prod[c] == __builtin_huge_val(), 0)) {
+                l = 0.0;
+#pragma unroll
+                for (int e = c * SEG; e < (c + 1) * SEG; ++e) l += log64_ge1(q[e]);
+              } else {
+                l = log64_ge1(prod[c]);
+              }
+              acc[u][c] -= 0.5 * l;
+            }
         }
       }
 }
