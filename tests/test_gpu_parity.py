@@ -396,3 +396,29 @@ def test_fp64_asinh_wide_range(enf, gpu, oracle, D):
     assert np.array_equal(np.signbit(Y[zero]), np.signbit(ref[zero]))
     Yr, Lr = oracle.flow_apply(layers, X)
     assert np.array_equal(np.isnan(to_np(L)).reshape(-1), np.isnan(Lr).reshape(-1))
+
+
+@pytest.mark.parametrize("D", [2, 32])
+def test_fp64_johnson_ulp_and_large_z_ladj(enf, gpu, oracle, D):
+    """asinh64 (enf_math64.h) within 3 ulp of the correctly rounded asinh (x87 extended precision
+    of the oracle's flow_apply_hi as the stand-in), and the ladj of columns whose 1 + z^2 product
+    overflows double while each factor does not (|z| ~ 1e100: the kernel's per-segment product
+    falls back to a sum of logs) equal to the reference's per-element sum; factors that overflow
+    themselves (|z| > 1.4e154) give -Inf as the reference's log(1/sqrt(Inf)) does."""
+    rng = np.random.default_rng(11)
+    N = 4096
+    X = rng.standard_normal((D, N)) * np.exp(rng.uniform(-30, 30, (D, N)))
+    X[:, :64] = rng.uniform(0.5, 2.0, (D, 64)) * 1e100 * rng.choice([-1, 1], (D, 64))
+    X[:, 64:80] = 1e200
+    X = np.asfortranarray(X)
+    one = np.ones(D)
+    layers = [(3, [np.zeros(D), one, np.zeros(D), one])]  # y = asinh(x), ladj = -sum log(1+x^2)/2
+    Y, L = enf.with_logabsdet_jacobian(make_flow(enf, layers), colmajor_cuda(X))
+    Y, L = to_np(Y), to_np(L).reshape(-1)
+    Yh, Lh = oracle.flow_apply_hi(layers, X)
+    assert np.all(np.abs(Y - Yh) <= 3 * np.spacing(np.abs(Yh)))
+    Yr, Lr = oracle.flow_apply(layers, X)
+    assert np.all(np.isneginf(Lr[64:80])) and np.array_equal(L[64:80], Lr[64:80])
+    fin = np.isfinite(Lr)
+    assert fin[:64].all()
+    assert np.all(np.abs(L[fin] - Lr[fin]) <= 1e-12 * (np.abs(Lr[fin]) + 1))
