@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--nbatches", type=int, default=100)
     ap.add_argument("--pairs", type=int, default=4)
     ap.add_argument("--history", default="", help="write the per-step negll to this file (JSON list)")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1 rank: capture the timed steps once into a HIP graph and replay it (0: eager launches)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -93,7 +95,7 @@ def main():
     hbs = np.ascontiguousarray(np.array(hbatches, dtype=np.int64).reshape(-1))
     hdev = torch.zeros(args.warmup + args.steps, dtype=torch.float64, device=dev)
 
-    def step(i, ev=None):
+    def step(i, ev=None, sh=sh):
         B, lo, hi = plan[i % len(plan)]
         if fused:  # enf_whitening_step: gradient, loss, ADAGrad, re-normalisation (3 launches)
             if ev is not None:
@@ -128,16 +130,36 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    graph = bool(args.graph) and fused
+    if graph:
+        # the timed steps as one HIP graph: captured (nothing runs), replayed once untimed (this
+        # advances the optimizer by args.steps more steps), then replayed once timed
+        cg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(cg):
+            cs = torch.cuda.current_stream().cuda_stream
+            for i in range(args.steps):
+                step(args.warmup + i, None, cs)
+        cg.replay()
+        torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        hist.append(step(args.warmup + i, evs[i]))
+    if graph:
+        evs = evs[:1]
+        evs[0][0].record(stream)
+        cg.replay()
+        evs[0][1].record(stream)
+        hist.append(hdev[args.warmup:args.warmup + args.steps])
+    else:
+        for i in range(args.steps):
+            hist.append(step(args.warmup + i, evs[i]))
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     grad_ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+    if graph:
+        grad_ms /= args.steps  # the replay's event pair brackets all steps
     wall, grad_ms_max = max_over_ranks([wall, grad_ms], dev, world)
     samples = sum(plan[(args.warmup + i) % len(plan)][0] for i in range(args.steps))
     negll = [float(h) for h in torch.cat(hist).cpu()]
@@ -151,6 +173,7 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
             "grad_kernel_ms_median" if not fused else "fused_step_ms_median": grad_ms,
             "grad_kernel_ms_max_rank" if not fused else "fused_step_ms_max_rank": grad_ms_max, "dtype": "f32",
+            "launch": "HIP graph of the timed steps (torch.cuda.CUDAGraph), replayed" if graph else "eager",
             "step": "enf_whitening_step (fused, 1 rank)" if fused else "enf_flow_negll_grad + RCCL sum + enf_adagrad_step"
                     " + enf_householder_normalize_strided",
             "data": "synthetic: X = f_true^-1(Z), Z ~ N(0,1) (torch Philox 0x5EED), f_true seed 7, init seed 42",

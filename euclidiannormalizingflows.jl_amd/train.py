@@ -266,10 +266,15 @@ def allreduce_sum_(buf: torch.Tensor, world: int, group=None) -> torch.Tensor:
 def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None, nbatches: int = 100,
                        nepochs: int = 100, optstate: Optional[FlowState] = None,
                        negll_history: Optional[List[float]] = None, process_group=None,
-                       similar_fill_quirk: bool = False) -> WhiteningResult:
+                       similar_fill_quirk: bool = False, graph: bool = False) -> WhiteningResult:
     """src/optimize_whitening.jl:25-45 on the device (see module docstring). similar_fill_quirk=True
     records the negll the reference records under Zygote (ScaleShiftTrafo's primal ladj taken as 0,
-    src/abstract_trafo.jl:30-33: + sum log|a| per sample); the updates are the same either way."""
+    src/abstract_trafo.jl:30-33: + sum log|a| per sample); the updates are the same either way.
+
+    graph=True (one rank): the launches of one epoch are captured once into a HIP graph
+    (torch.cuda.CUDAGraph) and the graph is replayed per epoch, which removes the host launch gaps
+    between the ~3 launches of each minibatch step; the parameters, optimizer state and history are
+    bit-identical to the eager loop (same kernels in the same order). Multi-rank runs stay eager."""
     import torch.distributed as dist
 
     optimizer = optimizer or ADAGrad()
@@ -295,50 +300,64 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
     hbatches = householder_batches(state)
     segs = trainable_runs(state)
     ss_a = [(int(state.offsets[i]), int(state.offsets[i + 1])) for i, _ in _scaleshift_a_segments(state)]
-    step = 0
     # one rank: the fused step (gradient, loss, ADAGrad and re-normalisation in three launches)
     fused = world == 1
     runs = np.ascontiguousarray(np.array(segs, dtype=np.int64).reshape(-1))
     hbs = np.ascontiguousarray(np.array(hbatches, dtype=np.int64).reshape(-1))
     if fused and (len(segs) > 64 or len(hbatches) > 16):
         fused = False
+    def one_epoch(hbuf: torch.Tensor, stream: int) -> None:
+        """Enqueue the steps of one epoch on `stream`; the loss of step j goes to hbuf[j]."""
+        for j, (B, lo, hi) in enumerate(plan):
+            if fused and hi > lo:
+                q = []
+                if similar_fill_quirk:  # with the parameters of this step's forward
+                    q = [torch.log(state.theta[s0:s1].abs()).sum() for s0, s1 in ss_a]
+                _lib.check(L.enf_whitening_step(
+                    dt, D, hi - lo, M[:, lo:hi].data_ptr(), _ld(M), state.layers(), len(state.trafos),
+                    state.theta.data_ptr(), state.acc.data_ptr(), runs.ctypes.data, len(segs), hbs.ctypes.data,
+                    len(hbatches), optimizer.eta, optimizer.epsilon, hbuf[j:].data_ptr(), ws.data_ptr(),
+                    ws.numel() * 8, stream))
+                for t in q:
+                    hbuf[j:j + 1] += t
+                continue
+            out.zero_()
+            if hi > lo:
+                Xb = M[:, lo:hi]
+                _lib.check(L.enf_flow_negll_grad(dt, D, hi - lo, Xb.data_ptr(), _ld(M), state.layers(),
+                                                 len(state.trafos), out.data_ptr(), ws.data_ptr(),
+                                                 ws.numel() * 8, stream))
+            allreduce_sum_(out, world, process_group)
+            hbuf[j:j + 1].copy_(out[0:1] / B)
+            if similar_fill_quirk:
+                for s0, s1 in ss_a:
+                    hbuf[j:j + 1] += torch.log(state.theta[s0:s1].abs()).sum()
+            g = out[1:]
+            for s0, s1 in segs:
+                _lib.check(L.enf_adagrad_step(dt, s1 - s0, state.theta[s0:].data_ptr(), state.acc[s0:].data_ptr(),
+                                              g[s0:].data_ptr(), 1.0 / B, optimizer.eta, optimizer.epsilon,
+                                              stream))
+            for off, k, ldv in hbatches:
+                _lib.check(L.enf_householder_normalize_strided(dt, D, k, state.theta[off:].data_ptr(), ldv,
+                                                               stream))
+
+    P = len(plan)
     with torch.cuda.device(M.device):
-        stream = torch.cuda.current_stream(M.device).cuda_stream
-        for _ in range(nepochs):
-            for B, lo, hi in plan:
-                if fused and hi > lo:
-                    q = []
-                    if similar_fill_quirk:  # with the parameters of this step's forward
-                        q = [torch.log(state.theta[s0:s1].abs()).sum() for s0, s1 in ss_a]
-                    _lib.check(L.enf_whitening_step(
-                        dt, D, hi - lo, M[:, lo:hi].data_ptr(), _ld(M), state.layers(), len(state.trafos),
-                        state.theta.data_ptr(), state.acc.data_ptr(), runs.ctypes.data, len(segs), hbs.ctypes.data,
-                        len(hbatches), optimizer.eta, optimizer.epsilon, hist[step:].data_ptr(), ws.data_ptr(),
-                        ws.numel() * 8, stream))
-                    for t in q:
-                        hist[step:step + 1] += t
-                    step += 1
-                    continue
-                out.zero_()
-                if hi > lo:
-                    Xb = M[:, lo:hi]
-                    _lib.check(L.enf_flow_negll_grad(dt, D, hi - lo, Xb.data_ptr(), _ld(M), state.layers(),
-                                                     len(state.trafos), out.data_ptr(), ws.data_ptr(),
-                                                     ws.numel() * 8, stream))
-                allreduce_sum_(out, world, process_group)
-                hist[step:step + 1].copy_(out[0:1] / B)
-                if similar_fill_quirk:
-                    for s0, s1 in ss_a:
-                        hist[step:step + 1] += torch.log(state.theta[s0:s1].abs()).sum()
-                g = out[1:]
-                for s0, s1 in segs:
-                    _lib.check(L.enf_adagrad_step(dt, s1 - s0, state.theta[s0:].data_ptr(), state.acc[s0:].data_ptr(),
-                                                  g[s0:].data_ptr(), 1.0 / B, optimizer.eta, optimizer.epsilon,
-                                                  stream))
-                for off, k, ldv in hbatches:
-                    _lib.check(L.enf_householder_normalize_strided(dt, D, k, state.theta[off:].data_ptr(), ldv,
-                                                                   stream))
-                step += 1
+        if graph and world == 1 and nepochs > 0:
+            hep = torch.zeros(P, dtype=torch.float64, device=M.device)
+            torch.cuda.synchronize(M.device)
+            cg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(cg):  # captured on torch's capture stream; nothing runs yet
+                one_epoch(hep, torch.cuda.current_stream(M.device).cuda_stream)
+            for ep in range(nepochs):
+                cg.replay()
+                hist[ep * P:(ep + 1) * P].copy_(hep)
+            torch.cuda.synchronize(M.device)
+            del cg
+        else:
+            stream = torch.cuda.current_stream(M.device).cuda_stream
+            for ep in range(nepochs):
+                one_epoch(hist[ep * P:(ep + 1) * P], stream)
     h = hist.cpu().numpy().tolist()
     prev = list(negll_history) if negll_history is not None else []
     return WhiteningResult(state.to_trafo(), state, prev + h)

@@ -369,3 +369,24 @@ def test_whitening_step_fused_equals_unfused(enf, gpu, kind):
         assert abs(float(loss[it]) - ref_loss) <= 2 * np.finfo(dtype).eps * abs(ref_loss), (it, float(loss[it]), ref_loss)
         assert torch.equal(sa.theta, sb.theta), it
         assert torch.equal(sa.acc, sb.acc), it
+
+
+@pytest.mark.parametrize("dtype,quirk", [(np.float32, False), (np.float64, True)])
+def test_optimize_whitening_graph_equals_eager(enf, gpu, dtype, quirk):
+    """optimize_whitening(graph=True) (one epoch captured as a HIP graph, replayed per epoch) gives
+    bit-identical parameters, optimizer state and negll history to the eager launches, including a
+    ragged last minibatch and the similar_fill quirk's extra device ops."""
+    rng = np.random.default_rng(23)
+    D = 32 if dtype == np.float32 else 5
+    ops = [5, 3, 5, 3] if dtype == np.float32 else [0, 5, 3, 1]
+    layers = [(op, rand_params(rng, op, D, dtype)) for op in ops]
+    X = np.asfortranarray(rng.standard_normal((D, 10_007)).astype(dtype))
+    runs = []
+    for graph in (False, True):
+        r = enf.optimize_whitening(colmajor_cuda(X), make_flow(enf, layers), enf.ADAGrad(), nbatches=7, nepochs=3,
+                                   similar_fill_quirk=quirk, graph=graph)
+        runs.append((r.optimizer_state.theta.cpu().numpy(), r.optimizer_state.acc.cpu().numpy(),
+                     np.asarray(r.negll_history)))
+    (t0, a0, h0), (t1, a1, h1) = runs
+    assert h0.shape == (21,)
+    assert np.array_equal(t0, t1) and np.array_equal(a0, a1) and np.array_equal(h0, h1)
