@@ -311,11 +311,12 @@ def test_optimize_whitening_similar_fill_quirk(enf, gpu):
     assert abs(b.negll_history[0] - a.negll_history[0] - np.sum(np.log(np.abs(layers[0][1][0])))) < 1e-12
 
 
-@pytest.mark.parametrize("kind", ["hj_f32", "mixed_f64", "mixed_f32"])
+@pytest.mark.parametrize("kind", ["hj_f32", "hj_f32_d64", "mixed_f64", "mixed_f32"])
 def test_whitening_step_fused_equals_unfused(enf, gpu, kind):
     """enf_whitening_step == enf_flow_negll_grad + enf_adagrad_step per run +
     enf_householder_normalize_strided per batch, bit for bit in the parameters and the ADAGrad state
-    over 6 consecutive steps (the recorded loss to one rounding)."""
+    over 6 consecutive steps (the recorded loss to one rounding); hj_f32_d64 is the D = 64 (J∘H)^4
+    flow (1280 trainable parameters)."""
     import torch
 
     from euclidiannormalizingflows_jl_amd import _lib
@@ -323,8 +324,8 @@ def test_whitening_step_fused_equals_unfused(enf, gpu, kind):
 
     rng = np.random.default_rng(17)
     dtype = np.float64 if kind.endswith("f64") else np.float32
-    if kind == "hj_f32":
-        D = 32
+    if kind.startswith("hj"):
+        D = 64 if kind.endswith("d64") else 32
         layers = []
         for _ in range(4):
             layers += [(5, rand_params(rng, 5, D, dtype)), (3, rand_params(rng, 3, D, dtype))]
