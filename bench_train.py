@@ -116,13 +116,11 @@ def main():
         if ev is not None:
             ev[1].record(stream)
         enf.allreduce_sum_(out, world)
-        g_ = out[1:]
-        for s0, s1 in segs:
-            lib.check(L.enf_adagrad_step(lib.ENF_F32, s1 - s0, state.theta[s0:].data_ptr(), state.acc[s0:].data_ptr(),
-                                         g_[s0:].data_ptr(), 1.0 / B, opt.eta, opt.epsilon, sh))
-        for off, k, ldv in hbatches:
-            lib.check(L.enf_householder_normalize_strided(lib.ENF_F32, D, k, state.theta[off:].data_ptr(), ldv, sh))
-        return out[0:1] / B
+        # loss, ADAGrad and re-normalisation on every rank in one launch
+        lib.check(L.enf_whitening_apply(lib.ENF_F32, D, state.nparams, out.data_ptr(), B, state.theta.data_ptr(),
+                                        state.acc.data_ptr(), runs.ctypes.data, len(segs), hbs.ctypes.data,
+                                        len(hbatches), opt.eta, opt.epsilon, hdev[i:].data_ptr(), sh))
+        return hdev[i:i + 1]
 
     for i in range(args.warmup):
         hist.append(step(i))
@@ -174,8 +172,7 @@ def main():
             "grad_kernel_ms_median" if not fused else "fused_step_ms_median": grad_ms,
             "grad_kernel_ms_max_rank" if not fused else "fused_step_ms_max_rank": grad_ms_max, "dtype": "f32",
             "launch": "HIP graph of the timed steps (torch.cuda.CUDAGraph), replayed" if graph else "eager",
-            "step": "enf_whitening_step (fused, 1 rank)" if fused else "enf_flow_negll_grad + RCCL sum + enf_adagrad_step"
-                    " + enf_householder_normalize_strided",
+            "step": "enf_whitening_step (fused, 1 rank)" if fused else "enf_flow_negll_grad + RCCL sum + enf_whitening_apply",
             "data": "synthetic: X = f_true^-1(Z), Z ~ N(0,1) (torch Philox 0x5EED), f_true seed 7, init seed 42",
             "config": {"workload": f"optimize_whitening D={D}, N={N}, nbatches={args.nbatches} "
                                    f"(B={plan[0][0]}), {args.pairs}x(J∘H), ADAGrad(0.1)",

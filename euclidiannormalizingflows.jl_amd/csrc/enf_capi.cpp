@@ -459,6 +459,19 @@ enf_status enf_whitening_step(enf_dtype dtype, int64_t D, int64_t N, const void*
   ENF_CATCH
 }
 
+enf_status enf_whitening_apply(enf_dtype dtype, int64_t D, int64_t nparams, const void* g, int64_t B, void* theta,
+                               void* acc, const int64_t* runs, int32_t nruns, const int64_t* hbatches, int32_t nhb,
+                               double eta, double epsilon, double* loss_out, void* hip_stream) {
+  ENF_TRY
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
+  if (D < 1 || nparams < 0 || B < 1) return fail(ENF_ERR_INVALID, "D and B must be >= 1, nparams >= 0");
+  if (!g || !theta || !acc || !loss_out) return fail(ENF_ERR_INVALID, "g, theta, acc or loss_out is NULL");
+  if ((nruns > 0 && !runs) || (nhb > 0 && !hbatches)) return fail(ENF_ERR_INVALID, "runs or hbatches is NULL");
+  return enf::whitening_apply(dtype == ENF_F64, D, nparams, g, B, theta, acc, runs, nruns, hbatches, nhb, eta, epsilon,
+                              loss_out, (hipStream_t)hip_stream);
+  ENF_CATCH
+}
+
 enf_status enf_adagrad_step(enf_dtype dtype, int64_t count, void* params, void* acc, const void* grad,
                             double grad_scale, double eta, double epsilon, void* hip_stream) {
   ENF_TRY

@@ -501,6 +501,24 @@ __global__ __launch_bounds__(256) void whitening_tail_kernel(ReduceArgs r, StepA
     for (int64_t c = w; c < a.hb[q][1]; c += 4) normalize_column<T>(th + a.hb[q][0] + c * a.hb[q][2], a.D, lane);
 }
 
+// The update half of a data-parallel step (enf_whitening_apply): the same loss / ADAGrad /
+// re-normalisation as whitening_tail_kernel, reading the cross-rank sum g (1 + nparams values of T,
+// the all-reduced enf_flow_negll_grad output) instead of the totals. Same operations and roundings
+// as out[0:1] / B + enf_adagrad_step per run + enf_householder_normalize_strided per batch.
+template <typename T>
+__global__ __launch_bounds__(256) void whitening_apply_kernel(const T* __restrict__ g, StepArgs a) {
+  T* th = (T*)a.theta;
+  T* ac = (T*)a.acc;
+  if (threadIdx.x == 0) *a.loss_out = (double)(g[0] / (T)a.nsamp);
+  for (int q = 0; q < a.nruns; ++q)
+    for (int64_t i = a.runs[q][0] + threadIdx.x; i < a.runs[q][1]; i += blockDim.x)
+      adagrad_update<T>(th[i], ac[i], g[1 + i], (T)a.scale, (T)a.eta, (T)a.eps);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int q = 0; q < a.nhb; ++q)
+    for (int64_t c = w; c < a.hb[q][1]; c += 4) normalize_column<T>(th + a.hb[q][0] + c * a.hb[q][2], a.D, lane);
+}
+
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
@@ -656,6 +674,41 @@ enf_status negll_grad(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx
   P.ra.out = out;
   if (f64) hipLaunchKernelGGL((grad_finalize_kernel<double>), dim3(1), dim3(256), 0, st, P.ra);
   else hipLaunchKernelGGL((grad_finalize_kernel<float>), dim3(1), dim3(256), 0, st, P.ra);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? ENF_OK : set_error(ENF_ERR_HIP, hipGetErrorString(e));
+}
+
+enf_status whitening_apply(bool f64, int64_t D, int64_t nparams, const void* g, int64_t B, void* theta, void* acc,
+                           const int64_t* runs, int32_t nruns, const int64_t* hb, int32_t nhb, double eta,
+                           double epsilon, double* loss_out, hipStream_t st) {
+  if (nruns < 0 || nruns > kMaxStepRuns || nhb < 0 || nhb > kMaxStepHB)
+    return set_error(ENF_ERR_UNSUPPORTED, "enf_whitening_apply: too many parameter runs or Householder batches");
+  StepArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.theta = theta;
+  a.acc = acc;
+  a.loss_out = loss_out;
+  a.scale = 1.0 / (double)B;
+  a.eta = eta;
+  a.eps = epsilon;
+  a.D = D;
+  a.nsamp = B;
+  a.nruns = nruns;
+  a.nhb = nhb;
+  for (int i = 0; i < nruns; ++i) {
+    a.runs[i][0] = runs[2 * i];
+    a.runs[i][1] = runs[2 * i + 1];
+    if (a.runs[i][0] < 0 || a.runs[i][1] < a.runs[i][0] || a.runs[i][1] > nparams)
+      return set_error(ENF_ERR_INVALID, "enf_whitening_apply: parameter run outside theta");
+  }
+  for (int i = 0; i < nhb; ++i) {
+    for (int q = 0; q < 3; ++q) a.hb[i][q] = hb[3 * i + q];
+    if (a.hb[i][0] < 0 || a.hb[i][1] < 0 || a.hb[i][2] < D ||
+        (a.hb[i][1] > 0 && a.hb[i][0] + (a.hb[i][1] - 1) * a.hb[i][2] + D > nparams))
+      return set_error(ENF_ERR_INVALID, "enf_whitening_apply: Householder batch outside theta");
+  }
+  if (f64) hipLaunchKernelGGL((whitening_apply_kernel<double>), dim3(1), dim3(256), 0, st, (const double*)g, a);
+  else hipLaunchKernelGGL((whitening_apply_kernel<float>), dim3(1), dim3(256), 0, st, (const float*)g, a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? ENF_OK : set_error(ENF_ERR_HIP, hipGetErrorString(e));
 }

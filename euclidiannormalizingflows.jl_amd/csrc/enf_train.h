@@ -30,6 +30,12 @@ enf_status whitening_step(bool f64, int64_t D, int64_t N, const void* X, int64_t
                           const int64_t* hb, int32_t nhb, double eta, double epsilon, double* loss_out,
                           void* workspace, size_t workspace_bytes, hipStream_t st);
 
+// Update half of a data-parallel step after the all-reduce (enf_whitening_apply): g = 1 + nparams
+// summed values of T, B = global batch size.
+enf_status whitening_apply(bool f64, int64_t D, int64_t nparams, const void* g, int64_t B, void* theta, void* acc,
+                           const int64_t* runs, int32_t nruns, const int64_t* hb, int32_t nhb, double eta,
+                           double epsilon, double* loss_out, hipStream_t st);
+
 // Optimisers.jl 0.2 ADAGrad on one parameter (src/optimize_whitening.jl:40): the arithmetic shared
 // by enf_adagrad_step and the fused step, so both round identically.
 template <typename T>

@@ -33,6 +33,7 @@ true negll.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -304,7 +305,12 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
     fused = world == 1
     runs = np.ascontiguousarray(np.array(segs, dtype=np.int64).reshape(-1))
     hbs = np.ascontiguousarray(np.array(hbatches, dtype=np.int64).reshape(-1))
-    if fused and (len(segs) > 64 or len(hbatches) > 16):
+    if len(segs) > 64 or len(hbatches) > 16:
+        fused = False
+    # multi-rank update after the all-reduce: one enf_whitening_apply launch (ENF_UNFUSED_APPLY=1: the
+    # separate enf_adagrad_step / enf_householder_normalize_strided calls, identical arithmetic)
+    apply_fused = len(segs) <= 64 and len(hbatches) <= 16 and os.environ.get("ENF_UNFUSED_APPLY", "0") != "1"
+    if os.environ.get("ENF_FORCE_DP_STEP", "0") == "1":  # testing: the data-parallel step on one rank
         fused = False
     def one_epoch(hbuf: torch.Tensor, stream: int) -> None:
         """Enqueue the steps of one epoch on `stream`; the loss of step j goes to hbuf[j]."""
@@ -321,6 +327,10 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
                 for t in q:
                     hbuf[j:j + 1] += t
                 continue
+            # data-parallel: local sums, cross-rank sum, then the update on every rank
+            q = []
+            if similar_fill_quirk:  # with the parameters of this step's forward
+                q = [torch.log(state.theta[s0:s1].abs()).sum() for s0, s1 in ss_a]
             out.zero_()
             if hi > lo:
                 Xb = M[:, lo:hi]
@@ -328,18 +338,23 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
                                                  len(state.trafos), out.data_ptr(), ws.data_ptr(),
                                                  ws.numel() * 8, stream))
             allreduce_sum_(out, world, process_group)
-            hbuf[j:j + 1].copy_(out[0:1] / B)
-            if similar_fill_quirk:
-                for s0, s1 in ss_a:
-                    hbuf[j:j + 1] += torch.log(state.theta[s0:s1].abs()).sum()
-            g = out[1:]
-            for s0, s1 in segs:
-                _lib.check(L.enf_adagrad_step(dt, s1 - s0, state.theta[s0:].data_ptr(), state.acc[s0:].data_ptr(),
-                                              g[s0:].data_ptr(), 1.0 / B, optimizer.eta, optimizer.epsilon,
-                                              stream))
-            for off, k, ldv in hbatches:
-                _lib.check(L.enf_householder_normalize_strided(dt, D, k, state.theta[off:].data_ptr(), ldv,
-                                                               stream))
+            if apply_fused:  # loss, ADAGrad and re-normalisation in one launch (enf_whitening_apply)
+                _lib.check(L.enf_whitening_apply(dt, D, state.nparams, out.data_ptr(), B, state.theta.data_ptr(),
+                                                 state.acc.data_ptr(), runs.ctypes.data, len(segs), hbs.ctypes.data,
+                                                 len(hbatches), optimizer.eta, optimizer.epsilon, hbuf[j:].data_ptr(),
+                                                 stream))
+            else:
+                hbuf[j:j + 1].copy_(out[0:1] / B)
+                g = out[1:]
+                for s0, s1 in segs:
+                    _lib.check(L.enf_adagrad_step(dt, s1 - s0, state.theta[s0:].data_ptr(),
+                                                  state.acc[s0:].data_ptr(), g[s0:].data_ptr(), 1.0 / B,
+                                                  optimizer.eta, optimizer.epsilon, stream))
+                for off, k, ldv in hbatches:
+                    _lib.check(L.enf_householder_normalize_strided(dt, D, k, state.theta[off:].data_ptr(), ldv,
+                                                                   stream))
+            for t in q:
+                hbuf[j:j + 1] += t
 
     P = len(plan)
     with torch.cuda.device(M.device):

@@ -141,12 +141,23 @@ enf_status enf_adagrad_step(enf_dtype dtype, int64_t count, void* params, void* 
  * of the nhb Householder column batches (hbatches[3i..3i+2] = offset in theta, column count, column
  * stride). Identical arithmetic to enf_flow_negll_grad + enf_adagrad_step per range +
  * enf_householder_normalize_strided per batch on one rank, in three launches instead of eight.
- * Multi-GPU training keeps the separate calls (the all-reduce sits between gradient and update). */
+ * Multi-GPU training: enf_flow_negll_grad, the all-reduce, then enf_whitening_apply. */
 enf_status enf_whitening_step(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
                               const enf_layer* layers, int32_t nlayers, void* theta, void* acc,
                               const int64_t* runs, int32_t nruns, const int64_t* hbatches, int32_t nhb,
                               double eta, double epsilon, double* loss_out, void* workspace,
                               size_t workspace_bytes, void* hip_stream);
+/* The update half of a DATA-PARALLEL optimize_whitening minibatch step (src/optimize_whitening.jl:38-41),
+ * run on every rank after the cross-GPU sum (enf_allreduce_sum / RCCL) of enf_flow_negll_grad's out
+ * buffer g (1 + nparams values of the dtype, nparams = enf_flow_param_count): *loss_out = g[0] / B
+ * (device double; B = global batch size), ADAGrad (eta, epsilon) with gradient g[1 + i] / B on the
+ * nruns ranges [runs[2i], runs[2i+1]) of theta, and the re-normalisation of the nhb Householder column
+ * batches, in one launch. Identical arithmetic to g[0] / B + enf_adagrad_step per range +
+ * enf_householder_normalize_strided per batch; every rank applies the same update (no broadcast). */
+enf_status enf_whitening_apply(enf_dtype dtype, int64_t D, int64_t nparams, const void* g, int64_t B,
+                               void* theta, void* acc, const int64_t* runs, int32_t nruns,
+                               const int64_t* hbatches, int32_t nhb, double eta, double epsilon,
+                               double* loss_out, void* hip_stream);
 /* HouseholderTrafo functor reconstruction (src/householder_trafo.jl:134-146): normalise each of
  * the k columns of the D x k device matrix V to unit 2-norm, in place. */
 enf_status enf_householder_normalize(enf_dtype dtype, int64_t D, int64_t k, void* V,

@@ -391,3 +391,32 @@ def test_optimize_whitening_graph_equals_eager(enf, gpu, dtype, quirk):
     (t0, a0, h0), (t1, a1, h1) = runs
     assert h0.shape == (21,)
     assert np.array_equal(t0, t1) and np.array_equal(a0, a1) and np.array_equal(h0, h1)
+
+
+@pytest.mark.parametrize("dtype,quirk", [(np.float32, False), (np.float64, True)])
+def test_data_parallel_step_apply_equals_separate_calls(enf, gpu, monkeypatch, dtype, quirk):
+    """The data-parallel step (enf_flow_negll_grad, all-reduce, enf_whitening_apply), forced on one
+    rank, gives bit-identical parameters and optimizer state to the same step with the separate
+    enf_adagrad_step / enf_householder_normalize_strided calls and to the fused single-rank step
+    (enf_whitening_step); its negll history equals the fused step's bit for bit and the separate
+    calls' to one rounding."""
+    rng = np.random.default_rng(29)
+    D = 32 if dtype == np.float32 else 6
+    ops = [5, 3, 5, 3] if dtype == np.float32 else [0, 5, 3, 2, 5]
+    layers = [(op, rand_params(rng, op, D, dtype, K=2 if op == 5 else 1)) for op in ops]
+    X = np.asfortranarray(rng.standard_normal((D, 9_001)).astype(dtype))
+    res = []
+    for env in ({"ENF_FORCE_DP_STEP": "1"}, {"ENF_FORCE_DP_STEP": "1", "ENF_UNFUSED_APPLY": "1"}, {}):
+        for k in ("ENF_FORCE_DP_STEP", "ENF_UNFUSED_APPLY"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        r = enf.optimize_whitening(colmajor_cuda(X), make_flow(enf, layers), enf.ADAGrad(), nbatches=4, nepochs=2,
+                                   similar_fill_quirk=quirk)
+        res.append((r.optimizer_state.theta.cpu().numpy(), r.optimizer_state.acc.cpu().numpy(),
+                    np.asarray(r.negll_history)))
+    for t, a, h in res[1:]:
+        assert np.array_equal(res[0][0], t) and np.array_equal(res[0][1], a)
+    # the fused paths divide the loss sum by B; torch's out[0:1] / B multiplies by 1/B (one rounding)
+    assert np.array_equal(res[0][2], res[2][2])
+    assert np.allclose(res[0][2], res[1][2], rtol=2.0 * np.finfo(dtype).eps, atol=0)
