@@ -143,9 +143,9 @@ __device__ __forceinline__ double generic_column(const FlowArgs& a, const T* __r
           acc += 0.5 * log1p((double)sh * sh);
         } else {
           const double w = (y[d] - r[4 * d]) * r[4 * d + 1];
-          const double sh = sinh(w);
+          const double sh = sinh64(w);
           y[d] = fma(r[4 * d + 3], sh, r[4 * d + 2]);
-          acc += 0.5 * log1p(sh * sh);
+          acc += 0.5 * log1p64_ge0(sh * sh);
         }
       }
     } else if (op == OP_CENTER_STRETCH || op == OP_CENTER_CONTRACT) {

@@ -1,5 +1,6 @@
-// enf_math64.h -- fp64 asinh and log for the Johnson layer (johnson_trafo.jl:31,41-57) on the
-// hardware reciprocal / reciprocal-square-root seeds, branch-free.
+// enf_math64.h -- fp64 asinh / log (JohnsonTrafo, johnson_trafo.jl:31,41-57) and sinh / log1p
+// (JohnsonTrafoInv, :36,103-104) on the hardware reciprocal / reciprocal-square-root seeds,
+// branch-free.
 //
 // Why: ocml's double asinh carries its argument in double-double through an extended-precision log
 // (~193 VALU instructions per element, PMC ~255 per element and layer at config 2), which makes the
@@ -89,6 +90,62 @@ __device__ __forceinline__ double asinh64(double x) {
   r = huge ? r + 6.93147180559945309417e-01 : r;
   r = a < __builtin_huge_val() ? r : a;  // Inf stays Inf, NaN stays NaN
   return __builtin_copysign(r, x);
+}
+
+// log(1 + t) for t >= 0 (t = +Inf gives +Inf): u = 1 + t rounded, c its TwoSum error, log(u) + c/u
+__device__ __forceinline__ double log1p64_ge0(double t) {
+  const double u = 1.0 + t;
+  const double bv = u - 1.0;
+  const double c = (1.0 - (u - bv)) + (t - bv);
+  const double r = log64_ge1(u) + c * __builtin_amdgcn_rcp(u);
+  return u < __builtin_huge_val() ? r : u;
+}
+
+// sinh(w) over the whole double range (johnson_trafo.jl:36), odd, +-Inf -> +-Inf, NaN -> NaN:
+//   |w| < 1: the odd Taylor series to w^17 (truncation < 1e-17 relative);
+//   else e^|w|/2 - e^-|w|/2 with e^|w| = 2^k e^r (msun e_exp.c reduction, |r| <= ln2/2, e^r by its
+//   Taylor series to r^13, truncation < 2^-57) and both halves scaled by ldexp, so sinh stays finite
+//   up to its own overflow (|w| ~ 710.48) although e^|w| overflows first.
+__device__ __forceinline__ double sinh64(double w) {
+  constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double a = __builtin_fabs(w);
+  // series: a + a^3 (1/3! + a^2 (1/5! + ...))
+  const double a2 = a * a;
+  double sp = 2.8114572543455207632e-15;                 // 1/17!
+  sp = fma(sp, a2, 7.6471637318198164759e-13);            // 1/15!
+  sp = fma(sp, a2, 1.6059043836821614599e-10);            // 1/13!
+  sp = fma(sp, a2, 2.5052108385441718775e-08);            // 1/11!
+  sp = fma(sp, a2, 2.7557319223985890653e-06);            // 1/9!
+  sp = fma(sp, a2, 1.9841269841269841270e-04);            // 1/7!
+  sp = fma(sp, a2, 8.3333333333333333333e-03);            // 1/5!
+  sp = fma(sp, a2, 1.6666666666666666667e-01);            // 1/3!
+  const double small = fma(a * a2, sp, a);
+  // exponential form
+  const double am = a < 1000.0 ? a : 1000.0;              // keeps k finite; Inf/NaN handled below
+  const double kd = __builtin_rint(am * 1.44269504088896340736);
+  const double r = fma(-kd, ln2_lo, fma(-kd, ln2_hi, am));
+  double p = 1.6059043836821614599e-10;                    // 1/13!
+  p = fma(p, r, 2.0876756987868098979e-09);                // 1/12!
+  p = fma(p, r, 2.5052108385441718775e-08);                // 1/11!
+  p = fma(p, r, 2.7557319223985890653e-07);                // 1/10!
+  p = fma(p, r, 2.7557319223985890653e-06);                // 1/9!
+  p = fma(p, r, 2.4801587301587301587e-05);                // 1/8!
+  p = fma(p, r, 1.9841269841269841270e-04);                // 1/7!
+  p = fma(p, r, 1.3888888888888888889e-03);                // 1/6!
+  p = fma(p, r, 8.3333333333333333333e-03);                // 1/5!
+  p = fma(p, r, 4.1666666666666666667e-02);                // 1/4!
+  p = fma(p, r, 1.6666666666666666667e-01);                // 1/3!
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);                                      // e^r in [0.70, 1.42]
+  double q = __builtin_amdgcn_rcp(p);                      // e^-r: seed + two Newton steps
+  q = fma(q, fma(-p, q, 1.0), q);
+  q = fma(q, fma(-p, q, 1.0), q);
+  const int k = (int)kd;
+  const double big = __builtin_amdgcn_ldexp(p, k - 1) - __builtin_amdgcn_ldexp(q, -k - 1);
+  double res = a < 1.0 ? small : big;
+  res = a < __builtin_huge_val() ? res : a;  // Inf stays Inf, NaN stays NaN
+  return __builtin_copysign(res, w);
 }
 
 }  // namespace enf

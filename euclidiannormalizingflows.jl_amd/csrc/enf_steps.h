@@ -272,9 +272,9 @@ __device__ __forceinline__ void step_johnson_inv(Tile<T, D, U>& x, Acc<T, D, U>&
             // the reference's ladj is from the output, log(1 + ((x_out - xi)/lambda)^2)/2, and
             // (x_out - xi)/lambda = sinh(w) up to the rounding of x_out
             const double w = (x[u][e] - pg[e]) * pd[e];
-            const double sh = sinh(w);
+            const double sh = sinh64(w);
             x[u][e] = fma(pl[e], sh, px[e]);
-            if (LADJ) acc[u][e / SEG] += 0.5 * log1p(sh * sh);
+            if (LADJ) acc[u][e / SEG] += 0.5 * log1p64_ge0(sh * sh);
           }
         }
       }
