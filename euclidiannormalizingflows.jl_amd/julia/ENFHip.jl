@@ -164,6 +164,90 @@ function mvnormal_negll_trafograd(f::_Supported, X::HipMatrix{T}) where {T}
     g[1], g[2:end]
 end
 
+# optimize_whitening (src/optimize_whitening.jl:25-45) over a device-resident sample matrix: one
+# enf_whitening_step per minibatch (gradient, negll, the Optimisers ADAGrad update and the
+# HouseholderTrafo re-normalisation, three launches) on one flat device parameter vector theta in
+# the enf_flow_param_count layout, the layer pointers pointing into theta. Array fields are
+# trainable, as Optimisers treats them; scalar fields are broadcast for the kernels and kept.
+# Minibatches as the reference's: batchsize = round(Int, N/nbatches), Iterators.partition over the
+# columns, the last one possibly shorter. optimizer_state is the device pair (theta, acc). A method
+# of the reference's own generic function (dispatch on the shim's HipMatrix, no type piracy).
+import Optimisers
+import EuclidianNormalizingFlows: optimize_whitening
+
+_fieldvec(p, D, ::Type{T}) where {T} = p isa AbstractArray ? _vec(vec(p), D, T) : fill(T(p), D)
+
+function optimize_whitening(smpls::HipMatrix{T}, initial_trafo::Function, optimizer::Optimisers.ADAGrad;
+                            nbatches::Integer = 100, nepochs::Integer = 100,
+                            negll_history = Vector{Float64}()) where {T}
+    D, N = smpls.D, smpls.N
+    fs = _leaves(initial_trafo)
+    host, offs, runs, hb = T[], Int[], Int64[], Int64[]
+    for f in fs
+        op, names = _op(f)
+        for nm in names
+            p = getfield(f, nm)
+            v = op == OP_HOUSEHOLDER ? vec(Matrix{T}(reshape(p, D, :))) : _fieldvec(p, D, T)
+            o = length(host)
+            push!(offs, o)
+            append!(host, v)
+            p isa AbstractArray && append!(runs, (o, o + length(v)))      # [start, end) of theta
+            op == OP_HOUSEHOLDER && append!(hb, (o, length(v) ÷ D, D))    # (offset, columns, stride)
+        end
+    end
+    theta = HipMatrix(reshape(host, :, 1))
+    acc = HipMatrix(fill(T(optimizer.epsilon), length(host), 1))  # Optimisers.init(ADAGrad, x)
+    layers = EnfLayer[]
+    i = 0
+    for f in fs
+        op, names = _op(f)
+        ptrs = Ptr{Cvoid}[C_NULL, C_NULL, C_NULL, C_NULL]
+        for q in eachindex(names)
+            i += 1
+            ptrs[q] = theta.buf.ptr + offs[i] * sizeof(T)
+        end
+        k = op == OP_HOUSEHOLDER ? Int32(length(getfield(f, :V)) ÷ D) : Int32(0)
+        push!(layers, EnfLayer(op, k, Tuple(ptrs)))
+    end
+    dt = T === Float64 ? ENF_F64 : ENF_F32
+    batchsize = max(round(Int, N / nbatches), 1)
+    starts = 0:batchsize:N-1
+    wsb = Ref{Csize_t}(0)
+    check(ccall((:enf_flow_negll_grad_workspace, libenf), Cint,
+                (Cint, Int64, Int64, Ptr{EnfLayer}, Int32, Ref{Csize_t}),
+                dt, D, batchsize, layers, length(layers), wsb))
+    ws = HipBuffer(max(Int(wsb[]), 1))
+    hist = HipMatrix{Float64}(1, nepochs * length(starts))
+    s = 0
+    for _ in 1:nepochs, b0 in starts
+        B = min(b0 + batchsize, N) - b0
+        check(ccall((:enf_whitening_step, libenf), Cint,
+                    (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Ptr{EnfLayer}, Int32, Ptr{Cvoid}, Ptr{Cvoid},
+                     Ptr{Int64}, Int32, Ptr{Int64}, Int32, Cdouble, Cdouble, Ptr{Cvoid}, Ptr{Cvoid}, Csize_t,
+                     Ptr{Cvoid}),
+                    dt, D, B, smpls.buf.ptr + b0 * D * sizeof(T), D, layers, length(layers), theta.buf.ptr,
+                    acc.buf.ptr, runs, length(runs) ÷ 2, hb, length(hb) ÷ 3, optimizer.eta, optimizer.epsilon,
+                    hist.buf.ptr + s * sizeof(Float64), ws.ptr, wsb[], C_NULL))
+        s += 1
+    end
+    # Functors-style reconstruction of the trained flow from theta
+    th = vec(Array(theta))
+    i = 0
+    rebuilt = map(fs) do f
+        op, names = _op(f)
+        vals = map(names) do nm
+            i += 1
+            p = getfield(f, nm)
+            p isa AbstractArray || return p
+            reshape(eltype(p).(th[offs[i]+1:offs[i]+length(p)]), size(p))
+        end
+        typeof(f).name.wrapper(vals...)
+    end
+    trafo = foldl((acc_, f) -> f ∘ acc_, rebuilt[2:end]; init = rebuilt[1])
+    (result = trafo, optimizer_state = (theta = theta, acc = acc),
+     negll_history = vcat(negll_history, vec(Array(hist))))
+end
+
 # JohnsonSU (src/johnson_trafo.jl:120-129) over a 1 x n HipMatrix of values: pdf.(d, X) etc. on the
 # device (enf_johnsonsu_eval), rand(d, n) as quantile of a Philox4x32-10 stream (enf_johnsonsu_sample).
 using EuclidianNormalizingFlows: JohnsonSU
@@ -198,7 +282,7 @@ function jsu_rand(d::JohnsonSU, ::Type{T}, n::Integer; seed::UInt64 = UInt64(0),
     out
 end
 
-export HipMatrix, mvnormal_negll_trafograd, jsu_pdf, jsu_logpdf, jsu_cdf, jsu_logcdf, jsu_ccdf,
+export HipMatrix, mvnormal_negll_trafograd, optimize_whitening, jsu_pdf, jsu_logpdf, jsu_cdf, jsu_logcdf, jsu_ccdf,
        jsu_logccdf, jsu_quantile, jsu_rand
 
 end # module
