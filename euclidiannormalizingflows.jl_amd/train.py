@@ -33,7 +33,6 @@ true negll.
 from __future__ import annotations
 
 import ctypes
-import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -267,7 +266,8 @@ def allreduce_sum_(buf: torch.Tensor, world: int, group=None) -> torch.Tensor:
 def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None, nbatches: int = 100,
                        nepochs: int = 100, optstate: Optional[FlowState] = None,
                        negll_history: Optional[List[float]] = None, process_group=None,
-                       similar_fill_quirk: bool = False, graph: bool = False) -> WhiteningResult:
+                       similar_fill_quirk: bool = False, graph: bool = False,
+                       _dp_step: bool = False, _separate_update: bool = False) -> WhiteningResult:
     """src/optimize_whitening.jl:25-45 on the device (see module docstring). similar_fill_quirk=True
     records the negll the reference records under Zygote (ScaleShiftTrafo's primal ladj taken as 0,
     src/abstract_trafo.jl:30-33: + sum log|a| per sample); the updates are the same either way.
@@ -275,7 +275,11 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
     graph=True (one rank): the launches of one epoch are captured once into a HIP graph
     (torch.cuda.CUDAGraph) and the graph is replayed per epoch, which removes the host launch gaps
     between the ~3 launches of each minibatch step; the parameters, optimizer state and history are
-    bit-identical to the eager loop (same kernels in the same order). Multi-rank runs stay eager."""
+    bit-identical to the eager loop (same kernels in the same order). Multi-rank runs stay eager.
+
+    Test hooks: _dp_step=True runs the data-parallel step (gradient, all-reduce, enf_whitening_apply)
+    on one rank; _separate_update=True replaces enf_whitening_apply by the separate
+    enf_adagrad_step / enf_householder_normalize_strided calls (identical arithmetic)."""
     import torch.distributed as dist
 
     optimizer = optimizer or ADAGrad()
@@ -307,10 +311,9 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
     hbs = np.ascontiguousarray(np.array(hbatches, dtype=np.int64).reshape(-1))
     if len(segs) > 64 or len(hbatches) > 16:
         fused = False
-    # multi-rank update after the all-reduce: one enf_whitening_apply launch (ENF_UNFUSED_APPLY=1: the
-    # separate enf_adagrad_step / enf_householder_normalize_strided calls, identical arithmetic)
-    apply_fused = len(segs) <= 64 and len(hbatches) <= 16 and os.environ.get("ENF_UNFUSED_APPLY", "0") != "1"
-    if os.environ.get("ENF_FORCE_DP_STEP", "0") == "1":  # testing: the data-parallel step on one rank
+    # multi-rank update after the all-reduce: one enf_whitening_apply launch
+    apply_fused = len(segs) <= 64 and len(hbatches) <= 16 and not _separate_update
+    if _dp_step:
         fused = False
     def one_epoch(hbuf: torch.Tensor, stream: int) -> None:
         """Enqueue the steps of one epoch on `stream`; the loss of step j goes to hbuf[j]."""

@@ -394,7 +394,7 @@ def test_optimize_whitening_graph_equals_eager(enf, gpu, dtype, quirk):
 
 
 @pytest.mark.parametrize("dtype,quirk", [(np.float32, False), (np.float64, True)])
-def test_data_parallel_step_apply_equals_separate_calls(enf, gpu, monkeypatch, dtype, quirk):
+def test_data_parallel_step_apply_equals_separate_calls(enf, gpu, dtype, quirk):
     """The data-parallel step (enf_flow_negll_grad, all-reduce, enf_whitening_apply), forced on one
     rank, gives bit-identical parameters and optimizer state to the same step with the separate
     enf_adagrad_step / enf_householder_normalize_strided calls and to the fused single-rank step
@@ -406,13 +406,9 @@ def test_data_parallel_step_apply_equals_separate_calls(enf, gpu, monkeypatch, d
     layers = [(op, rand_params(rng, op, D, dtype, K=2 if op == 5 else 1)) for op in ops]
     X = np.asfortranarray(rng.standard_normal((D, 9_001)).astype(dtype))
     res = []
-    for env in ({"ENF_FORCE_DP_STEP": "1"}, {"ENF_FORCE_DP_STEP": "1", "ENF_UNFUSED_APPLY": "1"}, {}):
-        for k in ("ENF_FORCE_DP_STEP", "ENF_UNFUSED_APPLY"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
+    for kw in ({"_dp_step": True}, {"_dp_step": True, "_separate_update": True}, {}):
         r = enf.optimize_whitening(colmajor_cuda(X), make_flow(enf, layers), enf.ADAGrad(), nbatches=4, nepochs=2,
-                                   similar_fill_quirk=quirk)
+                                   similar_fill_quirk=quirk, **kw)
         res.append((r.optimizer_state.theta.cpu().numpy(), r.optimizer_state.acc.cpu().numpy(),
                     np.asarray(r.negll_history)))
     for t, a, h in res[1:]:
