@@ -1,4 +1,6 @@
 #!/bin/bash
+# NOTE: the dispatch knob this script sets was measured and then removed from the library (no variant
+# beat the default; results under profiles/). Re-add the knob to the dispatcher to reproduce.
 # A/B of the D = 2 fragment-kernel variants (ENF_D2_VARIANT: 0 = U4, 1 = U2, 2 = U4 occ4,
 # 3 = U2 occ4, 4 = U1 occ4) on config 2 (J o H, D = 2, N = 1e6, fp64) and its fp32 twin.
 cd "${GRAFT_REPO_ROOT:-.}"

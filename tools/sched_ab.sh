@@ -2,7 +2,9 @@
 # A/B of compiler scheduling variants of the compiled (J o H)^n program (design probe): each
 # euclidiannormalizingflows.jl_amd/libenf_altN.so differs from libenf.so only in enf_flow_hj.hip's
 # LLVM scheduler options (1: max-ilp, 2: schedule-metric-bias=100, 3: max-memory-clause). Runs in the
-# gpurun snapshot, swapping the library file there.
+# gpurun snapshot, swapping the library file there. The alternative libraries are built by hand
+# (hipcc with the extra -mllvm option on enf_flow_hj.hip, linked with the other objects) and were
+# deleted after the measurement (profiles/r01_sched_variants.txt).
 cd "${GRAFT_REPO_ROOT:-.}"
 L=euclidiannormalizingflows.jl_amd
 cp $L/libenf.so $L/libenf_base.so

@@ -1,4 +1,6 @@
 #!/bin/bash
+# NOTE: the dispatch knob this script sets was measured and then removed from the library (no variant
+# beat the default; results under profiles/). Re-add the knob to the dispatcher to reproduce.
 # A/B of the config-3 compiled program at higher occupancy: ENF_HJ_U1OCC = 0 (default R8 U2, 4
 # waves/SIMD), 1 (R8 U1, 88 VGPRs, 5 waves), 6 / 8 (R8 U1 forced to 6 / 8 waves, spills), 9 (R8 U2
 # forced to 5 waves, spills).
