@@ -6,9 +6,14 @@ Y (D x N) and ladj (N) are written once, inputs already resident in HBM.
 
     python bench.py [--gpus N --steps K --warmup W] [--D 32 --N 10000000 --pairs 4 --dtype f32]
 
-Multi-GPU (one process per GPU, launched by torch.distributed.run): every rank processes its own
-N-sample shard of the batch (columns are independent, no data-path collective) -> weak scaling;
-the timed region is bracketed by barriers + device syncs and the max over ranks is reported.
+Multi-GPU: one process per GPU. Under torch.distributed.run (WORLD_SIZE set) each process is one
+rank; `python bench.py --gpus N` started by hand starts the N ranks itself (enf_launch.py: child
+processes under torch.distributed.run, before anything touches a GPU). Every rank processes its own
+N-sample shard of the batch (columns are independent, src/abstract_trafo.jl:9: no data-path
+collective) -> weak scaling; the timed region is bracketed by barriers + device syncs, value = all
+ranks' samples / the max over ranks of the timed wall time, and the per-rank kernel times are
+printed. `--selftest-cpu` runs the same harness (launch, barriers, max-over-ranks, aggregation) on
+gloo with a CPU stand-in step, for the CPU tests; it measures nothing.
 """
 from __future__ import annotations
 
@@ -19,10 +24,11 @@ import sys
 import time
 
 import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+import enf_launch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
 MFMA_NOTE = "elementwise/rank-1 maps: HBM roofline (SURVEY.md §8(d))"
@@ -44,42 +50,74 @@ def build_flow(D, pairs, np_dtype, seed=42, pattern=None):
     return layers
 
 
-def pmc_evidence(D, N, args, kern_ms):
-    """HBM traffic per launch and the VALU issue picture of the same kernel on the same workload,
-    from the committed rocprofv3 PMC passes (profiles/r01_pmc_traffic.json, tools/pmc.sh): traffic =
-    FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE; VALU issue cycles per SIMD = (4 x plain +
-    8 x transcendental wave64 instructions) / 1024 SIMDs (MI355X_MICROARCH.md issue costs)."""
-    prof = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-    try:
-        with open(prof) as f:
-            tr = json.load(f)
-    except (OSError, ValueError):
-        return None, None
-    if not (tr.get("D") == D and tr.get("N") == N and tr.get("dtype") == args.dtype and tr.get("pairs") == args.pairs
-            and args.pattern is None):
-        return None, None
-    c = tr.get("counters", {})
-    valu = None
-    if "SQ_INSTS_VALU" in c and "SQ_INSTS_VALU_TRANS_F32" in c:
-        trans = c["SQ_INSTS_VALU_TRANS_F32"]
-        cyc = (4.0 * (c["SQ_INSTS_VALU"] - trans) + 8.0 * trans) / 1024.0
-        clk = tr.get("effective_clock_ghz")
-        valu = {"insts_per_launch": c["SQ_INSTS_VALU"], "trans_insts_per_launch": trans,
-                "issue_cycles_per_simd": cyc, "pmc_effective_clock_ghz": clk,
-                "pmc_kernel_ms": tr.get("median_duration_ns_profiled", 0) / 1e6,
-                "issue_frac_in_pmc_run": (cyc / (clk * 1e9 * tr["median_duration_ns_profiled"] * 1e-9)
-                                          if clk and tr.get("median_duration_ns_profiled") else None),
-                "source": "profiles/r01_pmc_traffic.json"}
-    return tr.get("hbm_bytes_per_launch"), valu
+# Issue costs of gfx950 VALU wave-instructions at 4 waves per SIMD, measured on MI355X
+# (tools/microbench5-8, profiles/r02_microbench_issue_costs.txt), in cycles at the microbenchmarks'
+# clock: full-rate f32 fma/mul/add/sub and bit ops 2, half-rate ops (v_cmp, v_cndmask, v_bfi, DPP,
+# v_max/min, any SGPR source or three source VGPRs in one bank) 4, transcendentals 7.5 (3.4 vs 1.0 ns)
+ISSUE_CYC_FAST, ISSUE_CYC_TRANS = 2.0, 7.5
+
+
+def pmc_evidence(D, N, args):
+    """HBM traffic per launch and the VALU issue picture of the same kernel on the same workload from
+    the newest committed rocprofv3 PMC summary (tools/pmc.sh + tools/pmc_summary.py; collected by
+    separate `rocprofv3 --pmc` passes of `bench.py --no-cpu`, NOT in this run -- labelled as such):
+    traffic = FETCH_SIZE x 2 (gfx950 correction, MI355X_MICROARCH.md §HBM) + WRITE_SIZE; issue-cycle
+    floor per SIMD = (2 x non-transcendental + 7.5 x transcendental wave64 VALU instructions) / 1024
+    SIMDs (a lower bound: half-rate instructions cost 4), against the cycles of the profiled launch
+    (GRBM_GUI_ACTIVE clock x duration); SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES is the fraction of wave time
+    spent waiting to issue (shared SIMD or dependency), SQ_INSTS_LDS the LDS instructions per launch."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_bench.json")))
+    for prof in reversed(files):
+        try:
+            with open(prof) as f:
+                tr = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if not (tr.get("D") == D and tr.get("N") == N and tr.get("dtype") == args.dtype
+                and tr.get("pairs") == args.pairs and args.pattern is None):
+            continue
+        c = tr.get("counters", {})
+        rel = os.path.relpath(prof, ROOT)
+        traffic = {"bytes_per_launch": tr.get("hbm_bytes_per_launch"), "source": f"{rel} (rocprofv3 PMC passes, not this run)",
+                   "kernel_git": tr.get("git")}
+        valu = None
+        if "SQ_INSTS_VALU" in c and "SQ_INSTS_VALU_TRANS_F32" in c:
+            trans = c["SQ_INSTS_VALU_TRANS_F32"]
+            cyc = (ISSUE_CYC_FAST * (c["SQ_INSTS_VALU"] - trans) + ISSUE_CYC_TRANS * trans) / 1024.0
+            clk, dur = tr.get("effective_clock_ghz"), tr.get("median_duration_ns_profiled")
+            valu = {"insts_per_launch": c["SQ_INSTS_VALU"], "trans_insts_per_launch": trans,
+                    "issue_cycle_floor_per_simd": cyc, "pmc_effective_clock_ghz": clk,
+                    "pmc_kernel_ms": dur / 1e6 if dur else None,
+                    "issue_floor_frac": cyc / (clk * dur) if clk and dur else None,
+                    "wait_inst_any_frac": c.get("SQ_WAIT_INST_ANY_frac"),
+                    "lds_insts_per_launch": c.get("SQ_INSTS_LDS"),
+                    "source": f"{rel} (not this run)"}
+        return traffic, valu
+    return None, None
 
 
 def max_over_ranks(values, device, world):
     """Element-wise max over ranks of per-rank values (the timed region's wall time and kernel
     time): the whole job is as slow as its slowest GPU. torch.distributed all-reduce(MAX)
     (RCCL between GPUs; gloo in the CPU tests)."""
+    import torch
+
     t = torch.tensor(values, device=device, dtype=torch.float64)
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return [float(v) for v in t]
+
+
+def gather_ranks(value, device, world, rank):
+    """Every rank's value (list of world floats), by a sum all-reduce of one-hot slots."""
+    import torch
+
+    t = torch.zeros(world, device=device, dtype=torch.float64)
+    t[rank] = value
+    if world > 1:
+        torch.distributed.all_reduce(t)
     return [float(v) for v in t]
 
 
@@ -93,83 +131,113 @@ def main():
     ap.add_argument("--pairs", type=int, default=4, help="number of (Householder, Johnson) pairs")
     ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-samples", type=int, default=3_000_000)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of each CPU baseline leg")
     ap.add_argument("--pattern", default=None, help="diagnostic layer pattern, e.g. HHHHHHHH (overrides --pairs)")
+    ap.add_argument("--selftest-cpu", action="store_true",
+                    help="CPU tests only: the launch / barrier / max-over-ranks harness on gloo with a CPU "
+                         "stand-in step (measures nothing)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
+    # N > 1 started by hand: start the N ranks as child processes before anything touches a GPU
+    rc = enf_launch.spawn_ranks_if_needed(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
+    world, rank, local_rank = enf_launch.rank_env()
+    enf_launch.check_world(args.gpus, world)
+    import torch
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    backend = "gloo" if args.selftest_cpu else "nccl"
+    if args.selftest_cpu:
+        dev = torch.device("cpu")
+        if world > 1:
+            torch.distributed.init_process_group("gloo")
     else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
-
-    from enf_pkg import load
-
-    enf = load()
-    lib = enf._lib
+        if world > 1:
+            torch.cuda.set_device(local_rank)
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            torch.cuda.set_device(0)
+        dev = torch.device("cuda", torch.cuda.current_device())
     np_dtype = np.float32 if args.dtype == "f32" else np.float64
     t_dtype = torch.float32 if args.dtype == "f32" else torch.float64
     esz = 4 if args.dtype == "f32" else 8
     D, N = args.D, args.N
     layers = build_flow(D, args.pairs, np_dtype, pattern=args.pattern)
 
-    # synthetic X: N(0,1) columns from torch's counter-based (Philox) CUDA generator; each rank
-    # draws its own shard (global column offset = rank * N)
-    g = torch.Generator(device=dev).manual_seed(0x5EED + rank)
-    X = torch.randn((N, D), generator=g, device=dev, dtype=t_dtype)  # row-major N x D == column-major D x N
-    Y = torch.empty_like(X)
-    ladj = torch.empty(N, device=dev, dtype=t_dtype)
-    dparams = [[torch.from_numpy(np.ascontiguousarray(np.asarray(p))).to(dev) for p in ps] for _, ps in layers]
-    arr = (lib.Layer * len(layers))()
-    for i, ((op, ps), dp) in enumerate(zip(layers, dparams)):
-        arr[i].op, arr[i].k = op, 1 if op == 5 else 0
-        for q, t in enumerate(dp):
-            arr[i].p[q] = t.data_ptr()
-    L = lib.lib()
-    stream = torch.cuda.current_stream(dev)
-    sh = stream.cuda_stream
-    dt_code = lib.ENF_F32 if args.dtype == "f32" else lib.ENF_F64
+    if args.selftest_cpu:
+        Xs = np.ones((D, min(N, 4096)), dtype=np_dtype)
 
-    def step():
-        lib.check(L.enf_flow_apply(dt_code, D, N, X.data_ptr(), D, Y.data_ptr(), D, ladj.data_ptr(), 0,
-                                   arr, len(layers), sh))
+        def step():
+            np.tanh(Xs).sum()
+
+        def sync():
+            pass
+        stream = None
+    else:
+        from enf_pkg import load
+
+        enf = load()
+        lib = enf._lib
+        L = lib.lib()
+        # the shipping library only (diagnostic knobs live in libenf_diag.so, never here)
+        assert os.path.basename(lib.loaded_path()) == "libenf.so", lib.loaded_path()
+        # synthetic X: N(0,1) columns from torch's counter-based (Philox) CUDA generator; each rank
+        # draws its own shard (seed 0x5EED + rank)
+        g = torch.Generator(device=dev).manual_seed(0x5EED + rank)
+        X = torch.randn((N, D), generator=g, device=dev, dtype=t_dtype)  # row-major N x D == column-major D x N
+        Y = torch.empty_like(X)
+        ladj = torch.empty(N, device=dev, dtype=t_dtype)
+        dparams = [[torch.from_numpy(np.ascontiguousarray(np.asarray(p))).to(dev) for p in ps] for _, ps in layers]
+        arr = (lib.Layer * len(layers))()
+        for i, ((op, ps), dp) in enumerate(zip(layers, dparams)):
+            arr[i].op, arr[i].k = op, 1 if op == 5 else 0
+            for q, t in enumerate(dp):
+                arr[i].p[q] = t.data_ptr()
+        stream = torch.cuda.current_stream(dev)
+        sh = stream.cuda_stream
+        dt_code = lib.ENF_F32 if args.dtype == "f32" else lib.ENF_F64
+
+        def step():
+            lib.check(L.enf_flow_apply(dt_code, D, N, X.data_ptr(), D, Y.data_ptr(), D, ladj.data_ptr(), 0,
+                                       arr, len(layers), sh))
+
+        sync = torch.cuda.synchronize
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         torch.distributed.barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    sync()
+    if stream is not None:
+        # HIP events on the launch stream (torch.cuda.Event on the stream the kernel is launched on)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(stream)
+    if stream is not None:
+        ev0.record(stream)
     for _ in range(args.steps):
         step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
+    if stream is not None:
+        ev1.record(stream)
+    sync()
     if world > 1:
         torch.distributed.barrier()
-    torch.cuda.synchronize()
+    sync()
     wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # HIP events on the launch stream
+    kern_ms = ev0.elapsed_time(ev1) / args.steps if stream is not None else wall / args.steps * 1e3
     t_local, kern_ms_max = max_over_ranks([wall, kern_ms], dev, world)
+    per_rank_kernel_ms = gather_ranks(kern_ms, dev, world, rank)
     ms_per_step = t_local / args.steps * 1e3
     total_samples = N * world * args.steps
     value = total_samples / t_local
 
     bytes_per_launch = N * (2 * D + 1) * esz  # read X, write Y, write ladj
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    traffic, valu = pmc_evidence(D, N, args, kern_ms)
-    copy_gbs = copy_ceiling(X, Y, stream)
+    traffic, valu = (None, None) if args.selftest_cpu else pmc_evidence(D, N, args)
+    copy_gbs = None if args.selftest_cpu else copy_ceiling(X, Y, stream)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(layers, D, np_dtype, args.cpu_samples)
+    if rank == 0 and world == 1 and not args.no_cpu and not args.selftest_cpu:
+        cpu = cpu_baseline(layers, D, np_dtype, args.cpu_seconds)
 
     if rank == 0:
         out = {
@@ -184,15 +252,20 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.dtype,
-            "data": "synthetic: X ~ N(0,1) (torch Philox, seed 0x5EED+rank); params seed 42",
+            "data": ("selftest (CPU stand-in step, measures nothing)" if args.selftest_cpu else
+                     "synthetic: X ~ N(0,1) (torch Philox, seed 0x5EED+rank); params seed 42"),
             "config": {"workload": f"{'∘'.join(reversed(args.pattern or 'HJ' * args.pairs))} composed flow "
                                    f"fwd+ladj, D={D}, N={N} per GPU",
                        "D": D, "N_per_gpu": N, "layers": len(layers), "parallelism": f"sample-shard x{world}"},
+            "distributed": {"world_size": world, "backend": backend if world > 1 else None,
+                            "data_path_collective": None, "per_rank_kernel_ms": per_rank_kernel_ms},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic["bytes_per_launch"] if traffic else None,
+                         "traffic_source": traffic["source"] if traffic else None,
                          "kernel_ms": kern_ms, "kernel_ms_max_rank": kern_ms_max,
                          "algorithmic_bytes_per_launch": bytes_per_launch,
-                         "torch_copy_GBps": copy_gbs, "frac_of_torch_copy": achieved / copy_gbs},
+                         "torch_copy_GBps": copy_gbs, "frac_of_torch_copy": achieved / copy_gbs if copy_gbs else None},
             "valu": valu,
             "cpu_baseline": cpu,
         }
@@ -205,6 +278,8 @@ def copy_ceiling(X, Y, stream, reps=10):
     """Practical streaming ceiling of this GPU for the same bytes (confirm the HBM
     peak with a copy): torch's device copy of X into Y (N*D values read and written), timed with HIP
     events on the launch stream. Y is overwritten (after the timed steps)."""
+    import torch
+
     Y.copy_(X)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -217,27 +292,63 @@ def copy_ceiling(X, Y, stream, reps=10):
     return 2 * X.numel() * X.element_size() / (ms * 1e-3) / 1e9
 
 
-def cpu_baseline(layers, D, np_dtype, nsamp):
+def host_info():
+    """nproc and the CPU model of this host (lscpu), for the CPU baseline record."""
+    import subprocess
+
+    info = {"nproc": os.cpu_count()}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core", "CPU(s)"):
+                info[k.strip()] = v.strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except OSError:
+        pass
+    return info
+
+
+def cpu_baseline(layers, D, np_dtype, seconds):
     """The oracle (CPU restatement of the reference algorithm; Julia is unavailable) timed on a bounded
-    sample of the same workload on this host: reference-structured, 1 thread (layer by layer,
-    materialising Y and the D x N ladj temporaries as the Julia broadcasts do)."""
+    sample of the same workload on this host, in two legs of ~`seconds` each: reference-structured,
+    1 thread (layer by layer, materialising Y and the D x N ladj temporaries as the Julia broadcasts
+    do), and the same arithmetic on all usable host cores (OpenMP column blocks). The sample size is
+    calibrated on a short probe so each leg runs about `seconds`."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # bench cpu_baseline leg only
 
     oracle.build()
+    info = host_info()
+    ncores = info.get("affinity_cpus") or os.cpu_count() or 1
     rng = np.random.default_rng(1)
-    X = np.asfortranarray(rng.standard_normal((D, nsamp)).astype(np_dtype))
+    probe = np.asfortranarray(rng.standard_normal((D, 20_000)).astype(np_dtype))
+    t0 = time.perf_counter()
+    oracle.flow_apply(layers, probe)
+    rate1 = probe.shape[1] / (time.perf_counter() - t0)
+    n1 = max(20_000, int(rate1 * seconds))
+    X = np.asfortranarray(rng.standard_normal((D, n1)).astype(np_dtype))
     t0 = time.perf_counter()
     oracle.flow_apply(layers, X)
     t1 = time.perf_counter() - t0
-    nthr = min(os.cpu_count() or 1, 16)
+    del X
     t0 = time.perf_counter()
-    oracle.flow_apply(layers, X, nthreads=nthr)
+    oracle.flow_apply(layers, probe, nthreads=ncores)
+    ratem = probe.shape[1] / (time.perf_counter() - t0)
+    nm = max(20_000, min(int(ratem * seconds), 50_000_000))
+    X = np.asfortranarray(rng.standard_normal((D, nm)).astype(np_dtype))
+    t0 = time.perf_counter()
+    oracle.flow_apply(layers, X, nthreads=ncores)
     tm = time.perf_counter() - t0
-    return {"value": nsamp / t1, "unit": "samples/s", "cores": 1, "kind": "port",
-            "sample": f"{nsamp} samples of the same flow (D={D}), reference-structured C restatement, 1 thread, "
-                      f"{t1:.1f} s",
-            "openmp": {"value": nsamp / tm, "cores": nthr, "seconds": tm}}
+    return {"value": nm / tm, "unit": "samples/s", "cores": ncores, "kind": "port",
+            "sample": f"{nm} samples of the same flow (D={D}), CPU restatement of the reference algorithm "
+                      f"(Julia unavailable), OpenMP over {ncores} threads, {tm:.1f} s",
+            "single_thread": {"value": n1 / t1, "cores": 1, "samples": n1, "seconds": t1,
+                              "structure": "reference-structured: layer by layer, D x N ladj temporaries"},
+            "host": info}
 
 
 if __name__ == "__main__":

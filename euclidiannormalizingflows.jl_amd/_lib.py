@@ -11,6 +11,9 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libenf.so")
+# ENF_DIAG=1 build of the same sources (csrc/Makefile `diag`): tuning knobs and diagnostic kernel
+# variants read from ENF_* environment variables. tools/ only; see use_diagnostics_library().
+DIAG_LIB_PATH = os.path.join(_HERE, "libenf_diag.so")
 
 ENF_OK, ENF_ERR_INVALID, ENF_ERR_HIP, ENF_ERR_UNSUPPORTED, ENF_ERR_RCCL = range(5)
 ENF_F32, ENF_F64 = 0, 1
@@ -79,6 +82,21 @@ _SIGS = {
     "enf_johnsonsu_sample": (ctypes.c_int, [ctypes.c_int, _i64, _vp, _dbl, _dbl, _dbl, _dbl, ctypes.c_uint64,
                                             ctypes.c_uint64, _vp]),
 }
+
+
+def use_diagnostics_library() -> None:
+    """Bind libenf_diag.so instead of libenf.so (A/B tools under tools/ only; bench.py, the tests
+    and the package never call this). Must run before the first lib() call."""
+    global LIB_PATH
+    if _lib is not None:
+        raise RuntimeError("libenf is already loaded")
+    LIB_PATH = DIAG_LIB_PATH
+
+
+def loaded_path() -> str:
+    """Path of the bound library (bench.py asserts it is the shipping libenf.so)."""
+    lib()
+    return LIB_PATH
 
 
 def lib() -> ctypes.CDLL:

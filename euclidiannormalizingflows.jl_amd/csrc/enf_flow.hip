@@ -273,21 +273,23 @@ size_t program_lds_bytes(const FlowArgs& a, size_t elem) {
   return kLdsHeader + n * elem;
 }
 
-// Tuning knobs (development only): ENF_BLOCKS_PER_CU caps resident blocks per CU in the grid size,
-// ENF_FRAG_U / ENF_FRAG_OCC select fp32 D = 32 interpreter variants, ENF_DEBUG_MODE the diagnostic
-// builds (1: synthesized tile instead of loads, 2: also no stores), ENF_NO_SPECIALIZE=1 disables the
-// compiled (H o J)^n programs (enf_flow_hj.hip).
+// Tuning knobs of the diagnostics build only (enf_internal.h ENF_KNOB): ENF_BLOCKS_PER_CU caps
+// resident blocks per CU in the grid size, ENF_FRAG_U / ENF_FRAG_OCC select fp32 D = 32 interpreter
+// variants, ENF_DEBUG_MODE the diagnostic kernels (1: synthesized tile instead of loads, 2: also no
+// stores), ENF_NO_SPECIALIZE=1 disables the compiled (H o J)^n programs (enf_flow_hj.hip).
+#if ENF_DIAG
 int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v && *v ? atoi(v) : dflt;
 }
+#endif
 
 hipError_t frag_grid(const void* kernel, int64_t N, int64_t cols_per_block, size_t lds, const DeviceInfo& dev,
                      int64_t* blocks) {
   int per_cu = 0;
   hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, lds);
   if (e != hipSuccess) return e;
-  static const int cap_env = env_int("ENF_BLOCKS_PER_CU", 0);
+  static const int cap_env = ENF_KNOB("ENF_BLOCKS_PER_CU", 0);
   if (cap_env > 0 && per_cu > cap_env) per_cu = cap_env;
   if (per_cu < 1) per_cu = 1;
   int64_t b = (N + cols_per_block - 1) / cols_per_block;
@@ -311,20 +313,22 @@ static hipError_t launch_frag(const FlowArgs& a, size_t lds, hipStream_t st, con
 template <typename T, int LADJ>
 static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
   if constexpr (std::is_same_v<T, float>) {
-    static const int nospec = env_int("ENF_NO_SPECIALIZE", 0);
-    static const int dbg = env_int("ENF_DEBUG_MODE", 0);
+    static const int nospec = ENF_KNOB("ENF_NO_SPECIALIZE", 0);
+    static const int dbg = ENF_KNOB("ENF_DEBUG_MODE", 0);
     if (!nospec && hj_program_pairs(a) > 0) {
       hipError_t e = launch_hj_program(a, LADJ, dbg, st, dev);
       if (e != hipErrorNotSupported) return e;
     }
+#if ENF_DIAG
     if (a.D == 32) {
-      static const int u = env_int("ENF_FRAG_U", 4);
-      static const int occ = env_int("ENF_FRAG_OCC", 1);
+      static const int u = ENF_KNOB("ENF_FRAG_U", 4);
+      static const int occ = ENF_KNOB("ENF_FRAG_OCC", 1);
       if (dbg == 1) return launch_frag<T, 32, 4, LADJ, 1, 1>(a, lds, st, dev);
       if (dbg == 2) return launch_frag<T, 32, 4, LADJ, 1, 2>(a, lds, st, dev);
       if (u == 2) return launch_frag<T, 32, 2, LADJ>(a, lds, st, dev);
       if (u == 4 && occ == 5) return launch_frag<T, 32, 4, LADJ, 5>(a, lds, st, dev);
     }
+#endif
   }
   switch (a.D) {
     case 1: return launch_frag<T, 1, 4, LADJ>(a, lds, st, dev);
@@ -366,8 +370,8 @@ hipError_t launch_flow(const FlowArgs& a, bool f64, hipStream_t st, const Device
   }
   // LDS-staged generic kernel when a tile of >= 16 columns fits 16 KB per wave (ENF_NO_LDS_GENERIC=1:
   // the one-column-per-lane kernel)
-  static const int no_lds = env_int("ENF_NO_LDS_GENERIC", 0);
-  static const size_t wave_kb = (size_t)env_int("ENF_LDS_GENERIC_KB", 16) * 1024;  // image bytes per wave
+  static const int no_lds = ENF_KNOB("ENF_NO_LDS_GENERIC", 0);
+  static const size_t wave_kb = (size_t)ENF_KNOB("ENF_LDS_GENERIC_KB", 16) * 1024;  // image bytes per wave
   const int dp = (a.D | 1);
   int ct = 64;
   while (ct > 8 && (size_t)ct * dp * elem > wave_kb) ct >>= 1;

@@ -93,6 +93,14 @@ struct HJLay {
 template <int D, int R, int U>
 using HJTile = float[U][R];
 
+// VGPR banks (register index mod 4): an FMA whose three source VGPRs sit in one bank issues at
+// half rate on gfx950 (tools/microbench5: 1.8 vs 1.0-1.2 ns per wave-instruction). The tile x and
+// the records arrive by 16-byte loads into 4-register tuples whose bases the compiler aligns to
+// even registers, so x[e], P[e], Q[e] would share a bank for every e. a, P and R are therefore
+// stored one slot rotated within each 16-byte vector: row e of the lane uses slot hj_rot(e), whose
+// register is an odd distance from x[e]'s -- no FMA of the pair loop has three sources in one bank.
+__host__ __device__ constexpr int hj_rot(int e) { return (e & ~3) | ((e + 1) & 3); }
+
 // DBG (diagnostic builds, ENF_DEBUG_MODE): 1 = synthesize the tile instead of loading it, 2 = also
 // skip the stores (compute-only timing).
 template <int D, int R, int U, bool TAIL, int DBG>
@@ -213,7 +221,7 @@ __device__ void build_hj_program(const HJArgs& a, int n, float* __restrict__ rec
   for (int i = threadIdx.x; i < (n + 1) * D; i += blockDim.x) {
     const int p = i / D, d = i % D;
     const int h = d / (D / NF), w = d % (D / NF), g = w / 4, e = w % 4;
-    float* r = rec + (size_t)p * 4 * D + g * 4 * R + 4 * h + e;
+    float* r = rec + (size_t)p * 4 * D + g * 4 * R + 4 * h;
     double q0, q1, q2, q3;
     if (p < n) {
       const double vh = (double)a.v[p][d] * scr[3 * p];
@@ -236,10 +244,11 @@ __device__ void build_hj_program(const HJArgs& a, int n, float* __restrict__ rec
       q1 = (double)a.d[n - 1][d] * kLn2;
       q2 = q3 = 0.0;
     }
-    r[0] = (float)q0;
-    r[R] = (float)q1;
-    r[2 * R] = (float)q2;
-    r[3 * R] = (float)q3;
+    // a, P, R at the rotated slot hj_rot(e) of the row's 16-byte vector, Q at slot e (see HJParams)
+    r[hj_rot(e)] = (float)q0;
+    r[R + hj_rot(e)] = (float)q1;
+    r[2 * R + e] = (float)q2;
+    r[3 * R + hj_rot(e)] = (float)q3;
   }
   if (threadIdx.x == 0) {
     double c = 0.0;
@@ -248,6 +257,7 @@ __device__ void build_hj_program(const HJArgs& a, int n, float* __restrict__ rec
   }
   __syncthreads();
 }
+
 
 template <int R>
 struct HJParams {
@@ -268,12 +278,18 @@ struct HJParams {
 template <int D, int R, int U>
 __device__ __forceinline__ void hj_dots(const float (&x)[U][R], const float (&w)[R], float (&dot)[U]) {
   constexpr int G = HJLay<D, R, U>::G;
+  // two independent partial chains per column (even / odd rows): 2U chains of R/2 dependent FMAs
+  float d2[U][2];
 #pragma unroll
-  for (int u = 0; u < U; ++u) dot[u] = w[0] * x[u][0];
+  for (int u = 0; u < U; ++u)
 #pragma unroll
-  for (int e = 1; e < R; ++e)
+    for (int c = 0; c < 2; ++c) d2[u][c] = w[hj_rot(c)] * x[u][c];
 #pragma unroll
-    for (int u = 0; u < U; ++u) dot[u] = fmaf(w[e], x[u][e], dot[u]);
+  for (int e = 2; e < R; ++e)
+#pragma unroll
+    for (int u = 0; u < U; ++u) d2[u][e & 1] = fmaf(w[hj_rot(e)], x[u][e], d2[u][e & 1]);
+#pragma unroll
+  for (int u = 0; u < U; ++u) dot[u] = d2[u][0] + d2[u][1];
   if constexpr (G >= 2) {
 #pragma unroll
     for (int u = 0; u < U; ++u) dot[u] += dpp<0xB1>(dot[u]);
@@ -322,49 +338,84 @@ __device__ __forceinline__ float prod_tree(const float (&q)[R]) {
 // on entry and the new L on exit; r points at the lane's record group of this pair and is advanced
 // to the next record (prm is reloaded for it). Returns the largest product of q = 1 + z^2 over a
 // lane's R rows of one column (+Inf / NaN: the fast form is not valid for the tile).
-template <int D, int R, int U, bool LADJ>
-__device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U], const float*& r, HJParams<R>& prm) {
+template <int D, int R, int U, bool LADJ, bool ACC = true>
+__device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U], const float*& r, HJParams<R>& prm,
+                                              uint32_t csign) {
   float dot[U];
   hj_dots<D, R, U>(x, prm.a, dot);
   // z = L P + Q - dotL R (in place; the first FMA does not wait for the dot reduction)
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.P[e], prm.Q[e]);
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.P[hj_rot(e)], prm.Q[e]);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < R; ++e) x[u][e] = fmaf(-dot[u], prm.Rv[e], x[u][e]);
-  // next pair's records (record n holds gamma_n, delta'_n for the output)
-  r += 4 * D;
-  prm.load(r);
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(-dot[u], prm.Rv[hj_rot(e)], x[u][e]);
+  // next pair's records (record n holds gamma_n, delta'_n for the output): read here, during the
+  // Johnson part, or (ACC: 32 fewer VGPRs live across it, 4 waves per SIMD) at the end of the pair
+  if constexpr (!ACC) {
+    r += 4 * D;
+    prm.load(r);
+  }
   // stage by stage over the whole tile (U*R independent chains per stage)
   float q[U][R], t[U][R], pr[U];
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) q[u][e] = fmaf(x[u][e], x[u][e], 1.0f);
+  if constexpr (R == 8 && ACC) {
 #pragma unroll
-  for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) sqrt8(t[u], q[u]);
+  } else {
 #pragma unroll
-    for (int e = 0; e < R; ++e) t[u][e] = hw_sqrt(q[u][e]);
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < R; ++e) t[u][e] = hw_sqrt(q[u][e]);
+  }
 #pragma unroll
   for (int u = 0; u < U; ++u) pr[u] = prod_tree<R>(q[u]);
+  // small |z|: the Taylor form of asinh2_small (enf_frag.h) in place of q
+  if constexpr (ACC) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < R; ++e) q[u][e] = asinh2_small(x[u][e], q[u][e]);
+  }
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) t[u][e] = fabsf(x[u][e]) + t[u][e];
+  if constexpr (R == 8 && ACC) {
 #pragma unroll
-  for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
+      float w8[8];
 #pragma unroll
-    for (int e = 0; e < R; ++e) t[u][e] = hw_log2(t[u][e]);
+      for (int e = 0; e < 8; ++e) w8[e] = t[u][e];
+      log2_8(t[u], w8);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < R; ++e) t[u][e] = hw_log2(t[u][e]);
+  }
   if (LADJ)
 #pragma unroll
     for (int u = 0; u < U; ++u) acc[u] = fmaf(-0.5f, hw_log2(pr[u]), acc[u]);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < R; ++e) x[u][e] = copysignf(t[u][e], x[u][e]);
+    for (int e = 0; e < R; ++e) {
+      if constexpr (ACC)
+        x[u][e] = asinh2_merge(x[u][e], q[u][e], t[u][e], csign);
+      else
+        x[u][e] = copysignf(t[u][e], x[u][e]);
+    }
+  if constexpr (ACC) {
+    r += 4 * D;
+    prm.load(r);
+  }
   float m = pr[0];
 #pragma unroll
   for (int u = 1; u < U; ++u) m = fmaxf(m, pr[u]);
@@ -381,7 +432,7 @@ __device__ __forceinline__ void hj_pair_exact(float (&x)[U][R], float (&acc)[U],
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) {
-      const YL yl = johnson_fwd_f32_slow(fmaf(-dot[u], prm.Rv[e], fmaf(x[u][e], prm.P[e], prm.Q[e])), 0.f, 1.f);
+      const YL yl = johnson_fwd_f32_slow(fmaf(-dot[u], prm.Rv[hj_rot(e)], fmaf(x[u][e], prm.P[hj_rot(e)], prm.Q[e])), 0.f, 1.f);
       x[u][e] = yl.y;
       if (LADJ) acc[u] += yl.l;
     }
@@ -391,7 +442,7 @@ __device__ __forceinline__ void hj_pair_exact(float (&x)[U][R], float (&acc)[U],
 
 // NP > 0: the pair loop unrolled for exactly NP pairs (no loop-carried register copies between
 // the pair loop and the tile loop); NP == 0: runtime pair count a.n.
-template <int D, int R, int U, int LM, int NP>
+template <int D, int R, int U, int LM, int NP, bool ACC = true>
 struct HJBody {
   const HJArgs& a;
   const float* rec;  // this lane's record group
@@ -411,13 +462,14 @@ struct HJBody {
     const float* r = rec;
     HJParams<R> prm;
     prm.load(r);
+    const uint32_t csign = sign_mask_vgpr();
     // branch-free pair loop; a tile with a product overflow (|z| large, Inf, NaN) is redone below
     float m = 0.f;
     if constexpr (NP > 0) {
 #pragma unroll
-      for (int p = 0; p < NP; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ>(x, acc, r, prm));
+      for (int p = 0; p < NP; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ, ACC>(x, acc, r, prm, csign));
     } else {
-      for (int p = 0; p < n; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ>(x, acc, r, prm));
+      for (int p = 0; p < n; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ, ACC>(x, acc, r, prm, csign));
     }
     // column-uniform: the exact form's dot products read every lane of a column (DPP)
     m = group_max<HJLay<D, R, U>::G>(m);
@@ -433,7 +485,7 @@ struct HJBody {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.P[e], prm.a[e]);
+      for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.P[hj_rot(e)], prm.a[hj_rot(e)]);
     hj_store<D, R, U, LM, TAIL, DBG>(a, ctot, col0, x, acc, old, stage);
   }
 };
@@ -548,7 +600,7 @@ __device__ __forceinline__ void hj_stream_lds(const HJArgs& a, Body& body, float
 }
 
 // GLDS: stage the next tile through LDS (hj_stream_lds) instead of a second register tile.
-template <int D, int R, int U, int LM, int OCC, int DBG, int NP, int GLDS = 0>
+template <int D, int R, int U, int LM, int OCC, int DBG, int NP, int GLDS = 0, bool ACC = true>
 __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   const int n = a.n;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -558,7 +610,7 @@ __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   float* rec = reinterpret_cast<float*>(smem + kHjHeader);
   build_hj_program<D, R>(a, n, rec, scr, ctotp);
   constexpr int G = HJLay<D, R, U>::G;
-  HJBody<D, R, U, LM, NP> body{a, rec + ((threadIdx.x & 63) % G) * 4 * R, *ctotp, stage, n};
+  HJBody<D, R, U, LM, NP, ACC> body{a, rec + ((threadIdx.x & 63) % G) * 4 * R, *ctotp, stage, n};
   if constexpr (GLDS && DBG == 0) {
     float* xbuf = rec + (size_t)(n + 1) * 4 * D + (threadIdx.x >> 6) * (U * R * 64);
     hj_stream_lds<D, R, U, LM>(a, body, xbuf);
@@ -576,14 +628,14 @@ int hj_program_pairs(const FlowArgs& a) {
   return a.nsteps / 2;
 }
 
-template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, int NP = 0, int GLDS = 0>
+template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, int NP = 0, int GLDS = 0, bool ACC = true>
 static hipError_t launch_hj(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
   const size_t lds = hj_lds_bytes(D, h.n) + (GLDS ? (size_t)4 * U * R * 64 * sizeof(float) : 0);
-  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, NP, GLDS>);
+  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, NP, GLDS, ACC>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)HJLay<D, R, U>::TC * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, NP, GLDS>), dim3((unsigned)blocks), dim3(256), lds, st,
+  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, NP, GLDS, ACC>), dim3((unsigned)blocks), dim3(256), lds, st,
                      h);
   return hipGetLastError();
 }
@@ -592,19 +644,24 @@ static hipError_t launch_hj(const HJArgs& h, hipStream_t st, const DeviceInfo& d
 // fp32 D = 32 with ladj): ENF_HJ_R in {4, 8, 16} (U = 16 / R), ENF_HJ_U2 = 1 doubles U.
 template <int LM>
 static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, const DeviceInfo& dev) {
+  (void)dbg;
   if (D == 32) {
+#if ENF_DIAG
     if constexpr (LM == 1) {
-      static const int r = env_int("ENF_HJ_R", 8);
-      static const int u2 = env_int("ENF_HJ_U2", 0);
-      if (dbg == 1) return launch_hj<32, 8, 2, 1, 1, 1>(a, st, dev);
-      if (dbg == 2) return launch_hj<32, 8, 2, 1, 1, 2>(a, st, dev);
+      static const int r = ENF_KNOB("ENF_HJ_R", 8);
+      static const int u2 = ENF_KNOB("ENF_HJ_U2", 0);
+      static const int fast = ENF_KNOB("ENF_HJ_FASTASINH", 0);
+      if (dbg == 1) return fast ? launch_hj<32, 8, 2, 1, 4, 1, 0, 0, false>(a, st, dev) : launch_hj<32, 8, 2, 1, 4, 1>(a, st, dev);
+      if (dbg == 2) return fast ? launch_hj<32, 8, 2, 1, 4, 2, 0, 0, false>(a, st, dev) : launch_hj<32, 8, 2, 1, 4, 2>(a, st, dev);
+      if (fast) return launch_hj<32, 8, 2, 1, 4, 0, 0, 0, false>(a, st, dev);
       if (r == 4) return u2 ? launch_hj<32, 4, 8, 1>(a, st, dev) : launch_hj<32, 4, 4, 1>(a, st, dev);
       if (r == 16) return launch_hj<32, 16, 1, 1>(a, st, dev);
       if (u2) return launch_hj<32, 8, 4, 1>(a, st, dev);
-      static const int glds = env_int("ENF_HJ_GLDS", 0);
-      if (glds) return launch_hj<32, 8, 2, 1, 1, 0, 0, 1>(a, st, dev);
+      static const int glds = ENF_KNOB("ENF_HJ_GLDS", 0);
+      if (glds) return launch_hj<32, 8, 2, 1, 4, 0, 0, 1>(a, st, dev);
     }
-    return launch_hj<32, 8, 2, LM>(a, st, dev);
+#endif
+    return launch_hj<32, 8, 2, LM, 4>(a, st, dev);
   }
   return launch_hj<64, 8, 2, LM>(a, st, dev);
 }

@@ -367,7 +367,7 @@ bool wy_supported(int64_t D, bool frag) { return frag && (D == 32 || D == 64); }
 
 // ENF_WY_MIN_K: smallest reflection count of a chained HouseholderTrafo that runs as a dense product
 int wy_min_k() {
-  static const int k = env_int("ENF_WY_MIN_K", 8);
+  static const int k = ENF_KNOB("ENF_WY_MIN_K", 8);
   return k;
 }
 

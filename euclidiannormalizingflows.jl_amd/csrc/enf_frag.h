@@ -26,6 +26,20 @@ __device__ __forceinline__ float hw_exp2(float x) { return __builtin_amdgcn_exp2
 __device__ __forceinline__ float hw_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ float hw_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
+// Eight independent transcendentals issued back to back (one inline-asm block the scheduler cannot
+// interleave). On gfx950 a v_sqrt/v_log costs ~3.4 ns of SIMD issue when transcendentals come in runs
+// and ~5 ns when the compiler spreads them between dependent full-rate instructions (pair loop of the
+// compiled (J o H)^n program replayed register-only: tools/replay_loop.py, profiles/r02_*). The
+// trailing s_nop 0 is the one wait state a VALU reading a transcendental's result needs on gfx950,
+// which the compiler's hazard recognizer cannot see inside asm.
+#define ENF_TRANS8(OP, o, i)                                                                          \
+  asm(OP " %0, %8\n" OP " %1, %9\n" OP " %2, %10\n" OP " %3, %11\n" OP " %4, %12\n" OP " %5, %13\n" OP \
+      " %6, %14\n" OP " %7, %15\ns_nop 0"                                                             \
+      : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]), "=&v"(o[6]), "=&v"(o[7]) \
+      : "v"(i[0]), "v"(i[1]), "v"(i[2]), "v"(i[3]), "v"(i[4]), "v"(i[5]), "v"(i[6]), "v"(i[7]))
+__device__ __forceinline__ void sqrt8(float (&o)[8], const float (&i)[8]) { ENF_TRANS8("v_sqrt_f32", o, i); }
+__device__ __forceinline__ void log2_8(float (&o)[8], const float (&i)[8]) { ENF_TRANS8("v_log_f32", o, i); }
+
 // DPP cross-lane sum over aligned groups of G lanes (G <= 64, power of two). All 64 lanes must
 // be active. quad_perm(1,0,3,2) = 0xB1, quad_perm(2,3,0,1) = 0x4E, row_half_mirror = 0x141,
 // row_mirror = 0x140: after the quad steps every lane of a quad holds the quad sum, so a
@@ -81,6 +95,47 @@ struct Unit<float> { static constexpr float v = (float)kLn2; };
 template <>
 struct Unit<double> { static constexpr double v = 1.0; };
 
+// asinh(z)/ln2 in fp32 with a small relative error everywhere (johnson_trafo.jl:31 computes
+// asinh in the data precision; Julia's asinh(::Float32) is accurate to a few ulp). The fast form
+// log2(|z| + sqrt(q)), q = 1 + z^2, loses the low bits of |z| when |z| + sqrt(q) rounds near 1:
+// relative error ~1.5e-7/|z| (1e-4 at |z| ~ 2^-12, where the rounding of q drops the z^2/2 term
+// that cancels log's -t^2/2). Below kAsinhSmall the Taylor series to z^5 written in q replaces it:
+//   asinh z = z (1 - u/6 + 3u^2/40),  u = q - 1,  i.e. z (A0 + A1 q + A2 q^2)
+// (max relative error 2.4e-7 on |z| < 1/8; the log form is within 1e-6 on |z| >= 1/8; a tile of
+// z ~ N(0,1) values: tools/asinh32_err.py). Signed zeros pass through z * p.
+constexpr float kAsinhSmall = 0.125f;
+constexpr double kAsinhA2 = 3.0 / 40.0, kAsinhA1 = -1.0 / 6.0 - 2.0 * kAsinhA2, kAsinhA0 = 1.0 + 1.0 / 6.0 + kAsinhA2;
+__device__ __forceinline__ float asinh2_small(float z, float q) {
+  return z * fmaf(q, fmaf(q, (float)(kAsinhA2 * kLog2e), (float)(kAsinhA1 * kLog2e)), (float)(kAsinhA0 * kLog2e));
+}
+// Branch-free merge of the two forms, given t = log2(|z| + sqrt(q)) >= 0 and the small form S:
+//   asinh(z)/ln2 = |z| < kAsinhSmall ? S : copysign(t, z)
+// in four full-rate VALU instructions on gfx950 and no compare / select / copysign (v_cmp, v_cndmask
+// and v_bfi each issue at half rate there; tools/microbench5-9, profiles/r02_microbench_issue_costs.txt):
+//   T' = t | (z & 0x80000000)            v_bitop3_b32 0xF8 (sign constant in a VGPR, csign)
+//   M  = (t - kAsinhSmallL2) >> 31        v_subrev_f32 (literal) + v_ashrrev_i32: all ones iff |z| < T
+//                                         (t is monotone in |z|; log2(T + sqrt(1 + T^2)) = asinh(T)/ln2)
+//   L  = M ? S : T'                       v_bitop3_b32 0xE4
+// S = z * p with p > 0 for every q carries z's sign. NaN z gives NaN t and NaN S: NaN either way.
+// (A plain ?: on values computed only for it was also turned by hipcc 7.2 into an exec-masked branch
+// around one element's sqrt/log.)
+constexpr float kAsinhSmallL2 = 0.17987053f;  // asinh(1/8)/ln2 (mpmath: 0.1798705244977...)
+__device__ __forceinline__ uint32_t sign_mask_vgpr() {
+  uint32_t c;
+  asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(c));  // a VGPR operand: an SGPR source halves the issue rate
+  return c;
+}
+__device__ __forceinline__ float asinh2_merge(float z, float small, float t, uint32_t csign) {
+  const uint32_t ts = __builtin_amdgcn_bitop3_b32(__builtin_bit_cast(uint32_t, t), __builtin_bit_cast(uint32_t, z),
+                                                 csign, 0xF8);
+  const uint32_t m = (uint32_t)(__builtin_bit_cast(int32_t, t - kAsinhSmallL2) >> 31);
+  return __builtin_bit_cast(float, __builtin_amdgcn_bitop3_b32(__builtin_bit_cast(uint32_t, small), ts, m, 0xE4));
+}
+// the full fp32 form given q = fma(z, z, 1) and s = sqrt(q): asinh(z)/ln2
+__device__ __forceinline__ float asinh2_f32(float z, float q, float s, uint32_t csign) {
+  return asinh2_merge(z, asinh2_small(z, q), hw_log2(fabsf(z) + s), csign);
+}
+
 // fp32 robust Johnson element (huge |z|, Inf, NaN): the rare path of the fragment kernel and the
 // generic kernel's form. asinh stays finite for |z| up to FLT_MAX; log(1+z^2) overflows to +Inf
 // exactly where the reference's fp32 `1 + ((x-xi)/lambda)^2` does (johnson_trafo.jl:41), so
@@ -89,8 +144,9 @@ struct YL { float y, l; };
 __device__ __forceinline__ YL johnson_fwd_f32_slow(float z, float g, float d2) {
   const float t = fabsf(z);
   const float q = fmaf(z, z, 1.0f);
-  const float L = t > 1e18f ? hw_log2(t) + 1.0f : hw_log2(t + hw_sqrt(q));  // log2(2|z|) when huge
-  return {fmaf(d2, copysignf(L, z), g), -0.5f * hw_log2(q)};             // ladj part in log2 units
+  const float L = t > 1e18f ? copysignf(hw_log2(t) + 1.0f, z)  // log2(2|z|) when huge
+                            : asinh2_f32(z, q, hw_sqrt(q), sign_mask_vgpr());
+  return {fmaf(d2, L, g), -0.5f * hw_log2(q)};  // ladj part in log2 units
 }
 
 // ------------------------------------------------------------------------------------------

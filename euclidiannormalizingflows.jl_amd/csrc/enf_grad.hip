@@ -588,7 +588,7 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
   DeviceInfo dev;
   if (current_device_info(&dev) != ENF_OK) return ENF_ERR_HIP;
   // blocks per CU (2: what the fused kernel's LDS lets stay resident; measured best at config 5)
-  static const int per_cu = env_int("ENF_GRAD_BPC", 2);
+  static const int per_cu = ENF_KNOB("ENF_GRAD_BPC", 2);
   const int64_t cap = (int64_t)dev.num_cu * per_cu;
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
@@ -648,7 +648,7 @@ enf_status grad_parts(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx
   P.ra.partial = (const double*)workspace;
   P.ra.tot = (double*)workspace + (size_t)P.blocks * (1 + (size_t)P.ga.nparams);
   hipError_t e;
-  static const int generic = env_int("ENF_GRAD_GENERIC", 0);
+  static const int generic = ENF_KNOB("ENF_GRAD_GENERIC", 0);
   if (!f64 && !generic && hj_grad_eligible(D, ldx, X, layers, nlayers)) {
     e = launch_hj_grad(D, N, X, layers, nlayers, P.ga.nparams, (double*)workspace, P.blocks, st);
   } else {

@@ -548,13 +548,13 @@ hipError_t launch_hj_grad(int64_t D, int64_t N, const void* X, const enf_layer* 
   }
   if (off != nparams) return hipErrorInvalidValue;
   // register variant for <= 4 pairs (ENF_GRAD_REG=0: the LDS variant; ENF_GRAD_RU: its KU)
-  static const int reg = env_int("ENF_GRAD_REG", 1);
-  static const int ru = env_int("ENF_GRAD_RU", 1) == 2 ? 2 : 1;  // 1: 215 VGPRs at 4 pairs (2 waves/SIMD)
+  static const int reg = ENF_KNOB("ENF_GRAD_REG", 1);
+  static const int ru = ENF_KNOB("ENF_GRAD_RU", 1) == 2 ? 2 : 1;  // 1: 215 VGPRs at 4 pairs (2 waves/SIMD)
   if (reg && a.n <= 4) {
     if (D == 32) return ru == 1 ? launch_reg<32, 1>(a, blocks, st) : launch_reg<32, 2>(a, blocks, st);
     return ru == 1 ? launch_reg<64, 1>(a, blocks, st) : launch_reg<64, 2>(a, blocks, st);
   }
-  static const int ku = env_int("ENF_GRAD_U", 2) == 1 ? 1 : 2;  // 2: measured 72 vs 93 us at config 5
+  static const int ku = ENF_KNOB("ENF_GRAD_U", 2) == 1 ? 1 : 2;  // 2: measured 72 vs 93 us at config 5
   const size_t lds = D == 32 ? (ku == 1 ? hj_grad_lds<32, 1>(a.n) : hj_grad_lds<32, 2>(a.n))
                              : (ku == 1 ? hj_grad_lds<64, 1>(a.n) : hj_grad_lds<64, 2>(a.n));
   const void* k = D == 32 ? (ku == 1 ? (const void*)&hj_grad_kernel<32, 1> : (const void*)&hj_grad_kernel<32, 2>)

@@ -88,8 +88,19 @@ inline size_t record_elems(int op, int64_t D, size_t elem, bool frag) {
   return (n + q - 1) / q * q;
 }
 
-// development knobs read from the environment (enf_flow.hip)
+// Tuning and diagnostic knobs. The shipping library (libenf.so) is built with ENF_DIAG=0: every
+// knob is its compile-time default, nothing is read from the environment and the diagnostic kernel
+// variants (ENF_DEBUG_MODE: synthesized tiles / no stores) are not compiled in. The diagnostics
+// build (make diag -> libenf_diag.so, tools/ only) reads them from the environment.
+#ifndef ENF_DIAG
+#define ENF_DIAG 0
+#endif
+#if ENF_DIAG
 int env_int(const char* name, int dflt);
+#define ENF_KNOB(name, dflt) env_int(name, dflt)
+#else
+#define ENF_KNOB(name, dflt) (dflt)
+#endif
 
 size_t program_lds_bytes(const FlowArgs& a, size_t elem);
 bool frag_supported(const FlowArgs& a, size_t elem);

@@ -161,6 +161,7 @@ __device__ __forceinline__ void johnson_from_z(Tile<float, D, U>& x, Acc<float, 
               if (LADJ) acc[u][e / SEG] += r2.l;
             }
         } else {
+          const uint32_t csign = sign_mask_vgpr();
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             float prod[CPF];
@@ -170,8 +171,7 @@ __device__ __forceinline__ void johnson_from_z(Tile<float, D, U>& x, Acc<float, 
             for (int e = 0; e < V; ++e) {
               const float z = x[u][e];
               const float q = fmaf(z, z, 1.0f);
-              const float L = hw_log2(fabsf(z) + hw_sqrt(q));
-              x[u][e] = fmaf(pd[e], copysignf(L, z), pg[e]);
+              x[u][e] = fmaf(pd[e], asinh2_f32(z, q, hw_sqrt(q), csign), pg[e]);
               prod[e / SEG] *= q;
             }
             if (LADJ)

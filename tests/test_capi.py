@@ -37,6 +37,22 @@ def test_no_oracle_in_product(enf):
     assert "oracle" not in ldd
 
 
+def test_shipping_library_reads_no_environment(enf):
+    """The shipping libenf.so has no runtime tuning or diagnostic knobs: it
+    imports no getenv/secure_getenv and contains none of the ENF_* knob names, which exist only in
+    the ENF_DIAG=1 build (libenf_diag.so, tools/ only). The package binds libenf.so."""
+    import subprocess
+
+    path = os.path.join(os.path.dirname(enf._lib.DIAG_LIB_PATH), "libenf.so")
+    assert enf._lib.LIB_PATH == path
+    und = subprocess.run(["nm", "-D", "--undefined-only", path], capture_output=True, text=True).stdout
+    assert not re.search(r"\b(secure_)?getenv\b", und)
+    blob = open(path, "rb").read()
+    for knob in (b"ENF_DEBUG_MODE", b"ENF_HJ_R", b"ENF_FRAG_U", b"ENF_GRAD_REG", b"ENF_WY_MIN_K",
+                 b"ENF_BLOCKS_PER_CU", b"ENF_NO_SPECIALIZE", b"ENF_LDS_GENERIC_KB"):
+        assert knob not in blob, knob
+
+
 def test_version_and_errors(enf):
     L = enf._lib.lib()
     assert L.enf_version().decode().startswith("0.1.0")

@@ -1,0 +1,80 @@
+"""A/B timing of one flow configuration on the DIAGNOSTICS library (libenf_diag.so, ENF_DIAG=1):
+variants are selected by ENF_* environment knobs (enf_internal.h ENF_KNOB), one process per
+variant. Not the benchmark (bench.py times the shipping libenf.so).
+
+    ENF_HJ_FASTASINH=1 python tools/flow_time.py --D 32 --N 10000000 --pairs 4 --tag fast
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--D", type=int, default=32)
+    ap.add_argument("--N", type=int, default=10_000_000)
+    ap.add_argument("--pairs", type=int, default=4)
+    ap.add_argument("--pattern", default=None)
+    ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--tag", default="")
+    ap.add_argument("--product", action="store_true", help="time the shipping libenf.so instead")
+    args = ap.parse_args()
+    from enf_pkg import load
+    import bench
+
+    enf = load()
+    if not args.product:
+        enf._lib.use_diagnostics_library()
+    lib, L = enf._lib, enf._lib.lib()
+    dev = torch.device("cuda", 0)
+    npd = np.float32 if args.dtype == "f32" else np.float64
+    td = torch.float32 if args.dtype == "f32" else torch.float64
+    D, N = args.D, args.N
+    layers = bench.build_flow(D, args.pairs, npd, pattern=args.pattern)
+    g = torch.Generator(device=dev).manual_seed(0x5EED)
+    X = torch.randn((N, D), generator=g, device=dev, dtype=td)
+    Y = torch.empty_like(X)
+    ladj = torch.empty(N, device=dev, dtype=td)
+    dparams = [[torch.from_numpy(np.ascontiguousarray(p)).to(dev) for p in ps] for _, ps in layers]
+    arr = (lib.Layer * len(layers))()
+    for i, ((op, ps), dp) in enumerate(zip(layers, dparams)):
+        arr[i].op, arr[i].k = op, 1 if op == 5 else 0
+        for q, t in enumerate(dp):
+            arr[i].p[q] = t.data_ptr()
+    st = torch.cuda.current_stream(dev)
+    dt = lib.ENF_F32 if args.dtype == "f32" else lib.ENF_F64
+
+    def step():
+        lib.check(L.enf_flow_apply(dt, D, N, X.data_ptr(), D, Y.data_ptr(), D, ladj.data_ptr(), 0, arr, len(layers),
+                                   st.cuda_stream))
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(args.steps):
+        step()
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.steps
+    esz = 4 if args.dtype == "f32" else 8
+    knobs = {k: v for k, v in os.environ.items() if k.startswith("ENF_")}
+    print(json.dumps({"tag": args.tag, "lib": os.path.basename(lib.LIB_PATH), "knobs": knobs, "D": D, "N": N,
+                      "pairs": args.pairs, "pattern": args.pattern, "dtype": args.dtype, "kernel_ms": ms,
+                      "samples_per_s": N / (ms * 1e-3),
+                      "hbm_frac": N * (2 * D + 1) * esz / (ms * 1e-3) / 8e12}))
+
+
+if __name__ == "__main__":
+    main()
