@@ -4,31 +4,30 @@
 // (src/johnson_trafo.jl:29-32, ladj :39-42 / :76-80), fp32, D in {32, 64}, fused in one launch:
 // X is read once, Y and the per-sample ladj are written once.
 //
-// Folded layer constants. Inside the flow a Johnson output y = gamma + delta*asinh(z) is only ever
-// consumed by the next reflection and the next Johnson layer, both affine in y. With
-// L = sign(z) log2(|z| + sqrt(1 + z^2)) (= asinh(z)/ln2) and delta' = delta*ln2, y = gamma + delta' L,
-// so for pair p >= 1 (vh = v*sqrt(2/v'v), the reflection x - vh (vh'x) of householder_trafo!):
-//   dot = vh'y            = sum_d a_d L_d + c_p,              a_d = vh_d delta'_{p-1,d},
-//                                                            c_p = sum_d vh_d gamma_{p-1,d}
-//   z   = (y - dot vh - xi)/lambda
-//       = L P + Q - dotL R,   P = delta'_{p-1}/lambda, Q = (gamma_{p-1} - xi - c_p vh)/lambda,
-//                             R = vh/lambda                      (pair 0: a = vh, P = 1/lambda,
-//                                                                 Q = -xi/lambda, L := x)
-// and only the last pair forms y = gamma_n + delta'_n L. Per element and pair that is one FMA for
-// the dot product, two for z, then q = 1 + z^2, sqrt, |z| + s, log2, the sign (v_bfi), and for the
-// ladj -1/2 log2 of the product of the q of a lane's 8 rows of one column (one log per 8 elements).
-// The records are derived in double in each block's prologue from the raw device parameter vectors.
+// Per pair p (the register tile holds L_{p-1} = asinh(z_{p-1})/ln2 on entry, X itself for p = 0):
+//   y   = gamma_{p-1} + delta'_{p-1} L_{p-1}        the previous Johnson output (p = 0: y = X, i.e.
+//                                                    delta' = 1, gamma = 0), delta' = delta*ln2
+//   dot = vh'y,  vh = v sqrt(2/v'v)                 householder_trafo! (householder_trafo.jl:8-11)
+//   z   = y/lambda - xi/lambda - dot vh/lambda      (y - vh dot - xi)/lambda (johnson_trafo.jl:30)
+//   L_p = asinh(z)/ln2                              asinh2 (enf_frag.h): log2(|z| + sqrt(q)),
+//                                                    q = 1 + z^2, or the Taylor form for |z| < 1/8
+//   ladj += log|delta/lambda| - log(q)/2            johnson_trafo.jl:41; the constant part once per
+//                                                    column (ctot), -1/2 log2 of the product of the q
+//                                                    of a lane's 8 rows of one column
+// and the output y_n = gamma_n + delta'_n L_n. y is formed explicitly, as the reference rounds it,
+// before the reflection: folding gamma and delta' into the next pair's constants (round 1) saves one
+// FMA per element but adds terms that the reference has already cancelled, and gave up to 16x the
+// reference's error on elements where y cancels (tests/test_gpu_fp32_accuracy.py per-element test).
+// Per element and pair: 4 FMAs (y, dot, 2 for z), q, sqrt, |z| + s, log2, the small-|z| polynomial
+// (3) and its branch-free merge (4 full-rate ops), 7/8 multiply for the ladj product.
+//
+// Parameter records (LDS, built in double in each block's prologue): per pair and row
+// {delta', gamma, vh, 1/lambda, -xi/lambda, vh/lambda}; record n holds {delta'_n, gamma_n}.
 //
 // Fast-path guard: the product of 8 q stays finite unless |z| is large (about 2^8 on every row),
 // infinite or NaN; then the lanes of that column redo the whole program from X with the exact-range
 // elementwise form (johnson_fwd_f32_slow in enf_frag.h: asinh finite up to FLT_MAX, ladj -Inf where
 // the reference's fp32 1 + z^2 overflows).
-//
-// Loop structure: the pair loop is a runtime loop over one compact body (small code: the I-cache
-// holds it), with the next pair's parameter vectors read from LDS while the current one runs. Measured
-// alternatives that did not pay (profiles/r01_ab_*.txt): the pair loop unrolled for a compile-time
-// pair count, the next tile staged through LDS by global_load_lds (ENF_HJ_GLDS=1), 5 waves per SIMD
-// (spills), 4 or 16 rows per lane (ENF_HJ_R).
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -42,6 +41,7 @@
 namespace enf {
 
 constexpr int kHjMaxPairs = 8;
+constexpr int kHjW = 6;  // record parameters per row
 
 // Kernel arguments of the compiled program: the pair parameter vectors only (376 bytes; the
 // generic FlowArgs table is ~2 KB, and kernel arguments that large are staged with an extra
@@ -59,11 +59,11 @@ struct HJArgs {
   const float* xi[kHjMaxPairs];
   const float* lam[kHjMaxPairs];
 };
-// LDS: [per pair {hs, c, cl} + ctot: doubles][ladj staging: 4 waves x kStagePerWave floats][records]
-constexpr size_t kHjScratch = ((3 * kHjMaxPairs + 1) * sizeof(double) + 15) / 16 * 16;
+// LDS: [per pair {hs, cl} + ctot: doubles][ladj staging: 4 waves x kStagePerWave floats][records]
+constexpr size_t kHjScratch = ((2 * kHjMaxPairs + 1) * sizeof(double) + 15) / 16 * 16;
 constexpr size_t kHjHeader = kHjScratch + 4 * kStagePerWave * sizeof(float);
 
-static size_t hj_lds_bytes(int D, int n) { return kHjHeader + (size_t)(n + 1) * 4 * D * sizeof(float); }
+static size_t hj_lds_bytes(int D, int n) { return kHjHeader + (size_t)(n + 1) * kHjW * D * sizeof(float); }
 
 // Register layout of the compiled program: a lane owns R rows of ONE column as NF = R/4 16-byte
 // fragments; fragment h holds rows h*(D/NF) + 4*g .. +3 with g = lane % G the lane's row group and
@@ -90,16 +90,15 @@ struct HJLay {
   }
 };
 
-template <int D, int R, int U>
-using HJTile = float[U][R];
-
 // VGPR banks (register index mod 4): an FMA whose three source VGPRs sit in one bank issues at
-// half rate on gfx950 (tools/microbench5: 1.8 vs 1.0-1.2 ns per wave-instruction). The tile x and
-// the records arrive by 16-byte loads into 4-register tuples whose bases the compiler aligns to
-// even registers, so x[e], P[e], Q[e] would share a bank for every e. a, P and R are therefore
-// stored one slot rotated within each 16-byte vector: row e of the lane uses slot hj_rot(e), whose
-// register is an odd distance from x[e]'s -- no FMA of the pair loop has three sources in one bank.
+// half rate on gfx950 (tools/microbench5: 1.8 vs 1.0-1.2 ns per wave-instruction). The tile and the
+// records arrive by 16-byte loads into 4-register tuples whose bases the compiler aligns to even
+// registers, so x[e] and the e-th value of every record vector would share a bank. The multiplier
+// of each FMA (delta', vh, 1/lambda, vh/lambda) is therefore stored one slot rotated within its
+// 16-byte vector: row e uses slot hj_rot(e), an odd register distance from x[e]'s.
 __host__ __device__ constexpr int hj_rot(int e) { return (e & ~3) | ((e + 1) & 3); }
+enum : int { HJ_DP = 0, HJ_GP = 1, HJ_VH = 2, HJ_IL = 3, HJ_NXI = 4, HJ_RR = 5 };
+__host__ __device__ constexpr bool hj_rotated(int q) { return q == HJ_DP || q == HJ_VH || q == HJ_IL || q == HJ_RR; }
 
 // DBG (diagnostic builds, ENF_DEBUG_MODE): 1 = synthesize the tile instead of loading it, 2 = also
 // skip the stores (compute-only timing).
@@ -184,110 +183,90 @@ __device__ __forceinline__ void hj_store(const HJArgs& a, float ctot, int64_t co
   }
 }
 
-// Records, pair p < n: [group g][param q in (a, P, Q, R)][R values, value 4h+e = row h*D/NF+4g+e];
-// record n (final): same layout with (gamma_{n-1}, delta'_{n-1}, 0, 0). A lane reads each
-// parameter of its rows with NF 16-byte LDS reads.
+// Records, pair p < n: [group g][param q][R values, value 4h+e = row h*D/NF+4g+e, rotated slot for
+// the multipliers]; record n: {delta'_{n-1}, gamma_{n-1}} (the output). A lane reads each parameter
+// of its rows with NF 16-byte LDS reads.
 template <int D, int R>
 __device__ void build_hj_program(const HJArgs& a, int n, float* __restrict__ rec, double* __restrict__ scr,
                                  float* ctot) {
   constexpr int NF = R / 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  // pass 1 (one wave per pair): v'v, sum_d v_d gamma_{p-1,d}, and the constant ladj part
-  // sum_d log|delta/lambda| (johnson_trafo.jl:41) in double
+  // pass 1 (one wave per pair): v'v and the constant ladj part sum_d log|delta/lambda|
+  // (johnson_trafo.jl:41) in double
   for (int p = wave; p < n; p += nw) {
     const float* v = a.v[p];
-    const float* gprev = p > 0 ? a.g[p - 1] : nullptr;
-    double vv = 0.0, cg = 0.0, cl = 0.0;
+    double vv = 0.0, cl = 0.0;
     for (int d = lane; d < D; d += 64) {
       const double vd = v[d];
       vv += vd * vd;
-      if (gprev) cg += vd * (double)gprev[d];
       cl += log(fabs((double)a.d[p][d])) - log(fabs((double)a.lam[p][d]));
     }
     for (int m = 32; m >= 1; m >>= 1) {
       vv += __shfl_xor(vv, m);
-      cg += __shfl_xor(cg, m);
       cl += __shfl_xor(cl, m);
     }
     if (lane == 0) {
-      const double hs = sqrt(2.0 / vv);  // householder_trafo.jl:9-10: 2 v (v'x) / (v'v)
-      scr[3 * p] = hs;
-      scr[3 * p + 1] = hs * cg;
-      scr[3 * p + 2] = cl;
+      scr[2 * p] = sqrt(2.0 / vv);  // householder_trafo.jl:9-10: 2 v (v'x) / (v'v)
+      scr[2 * p + 1] = cl;
     }
   }
   __syncthreads();
-  // pass 2: folded records
+  // pass 2: records
   for (int i = threadIdx.x; i < (n + 1) * D; i += blockDim.x) {
     const int p = i / D, d = i % D;
     const int h = d / (D / NF), w = d % (D / NF), g = w / 4, e = w % 4;
-    float* r = rec + (size_t)p * 4 * D + g * 4 * R + 4 * h;
-    double q0, q1, q2, q3;
+    float* r = rec + (size_t)p * kHjW * D + g * kHjW * R + 4 * h;
+    double q[kHjW] = {0, 0, 0, 0, 0, 0};
+    q[HJ_DP] = p > 0 ? (double)a.d[p - 1][d] * kLn2 : 1.0;
+    q[HJ_GP] = p > 0 ? (double)a.g[p - 1][d] : 0.0;
     if (p < n) {
-      const double vh = (double)a.v[p][d] * scr[3 * p];
-      const double xi = a.xi[p][d];
+      const double vh = (double)a.v[p][d] * scr[2 * p];
       const double il = 1.0 / (double)a.lam[p][d];
-      if (p == 0) {
-        q0 = vh;
-        q1 = il;
-        q2 = -xi * il;
-      } else {
-        const double gp = a.g[p - 1][d];
-        const double dp = (double)a.d[p - 1][d] * kLn2;
-        q0 = vh * dp;
-        q1 = dp * il;
-        q2 = (gp - xi - scr[3 * p + 1] * vh) * il;
-      }
-      q3 = vh * il;
-    } else {
-      q0 = a.g[n - 1][d];
-      q1 = (double)a.d[n - 1][d] * kLn2;
-      q2 = q3 = 0.0;
+      q[HJ_VH] = vh;
+      q[HJ_IL] = il;
+      q[HJ_NXI] = -(double)a.xi[p][d] * il;
+      q[HJ_RR] = vh * il;
     }
-    // a, P, R at the rotated slot hj_rot(e) of the row's 16-byte vector, Q at slot e (see HJParams)
-    r[hj_rot(e)] = (float)q0;
-    r[R + hj_rot(e)] = (float)q1;
-    r[2 * R + e] = (float)q2;
-    r[3 * R + hj_rot(e)] = (float)q3;
+#pragma unroll
+    for (int k = 0; k < kHjW; ++k) r[k * R + (hj_rotated(k) ? hj_rot(e) : e)] = (float)q[k];
   }
   if (threadIdx.x == 0) {
     double c = 0.0;
-    for (int p = 0; p < n; ++p) c += scr[3 * p + 2];
+    for (int p = 0; p < n; ++p) c += scr[2 * p + 1];
     *ctot = (float)c;
   }
   __syncthreads();
 }
 
-
+// One pair's parameters of the lane's rows (6 x R values): the first three are read at the end of
+// the previous pair, the last three at the start of the pair (they are needed after the dot).
 template <int R>
 struct HJParams {
-  float a[R], P[R], Q[R], Rv[R];
+  float v[kHjW][R];
+  template <int Q0, int Q1>
   __device__ __forceinline__ void load(const float* r) {
 #pragma unroll
-    for (int h = 0; h < R / 4; ++h) {
-      lds_vec<float, 4>(r + 4 * h, *reinterpret_cast<float(*)[4]>(&a[4 * h]));
-      lds_vec<float, 4>(r + R + 4 * h, *reinterpret_cast<float(*)[4]>(&P[4 * h]));
-      lds_vec<float, 4>(r + 2 * R + 4 * h, *reinterpret_cast<float(*)[4]>(&Q[4 * h]));
-      lds_vec<float, 4>(r + 3 * R + 4 * h, *reinterpret_cast<float(*)[4]>(&Rv[4 * h]));
-    }
+    for (int k = Q0; k < Q1; ++k)
+#pragma unroll
+      for (int h = 0; h < R / 4; ++h) lds_vec<float, 4>(r + k * R + 4 * h, *reinterpret_cast<float(*)[4]>(&v[k][4 * h]));
   }
+  __device__ __forceinline__ float m(int k, int e) const { return v[k][hj_rotated(k) ? hj_rot(e) : e]; }
 };
 
-// Householder dot of every column of the tile: in-lane FMA chains over the lane's R rows, then
-// log2(G) DPP stages across the G lanes of the column.
+// Householder dot of every column of the tile: two independent partial chains per column (even
+// and odd rows) over the lane's R rows, then log2(G) DPP stages across the G lanes of the column.
 template <int D, int R, int U>
-__device__ __forceinline__ void hj_dots(const float (&x)[U][R], const float (&w)[R], float (&dot)[U]) {
+__device__ __forceinline__ void hj_dots(const float (&y)[U][R], const HJParams<R>& prm, float (&dot)[U]) {
   constexpr int G = HJLay<D, R, U>::G;
-  // two independent partial chains per column (even / odd rows): 2U chains of R/2 dependent FMAs
   float d2[U][2];
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int c = 0; c < 2; ++c) d2[u][c] = w[hj_rot(c)] * x[u][c];
+    for (int c = 0; c < 2; ++c) d2[u][c] = prm.m(HJ_VH, c) * y[u][c];
 #pragma unroll
   for (int e = 2; e < R; ++e)
 #pragma unroll
-    for (int u = 0; u < U; ++u) d2[u][e & 1] = fmaf(w[hj_rot(e)], x[u][e], d2[u][e & 1]);
+    for (int u = 0; u < U; ++u) d2[u][e & 1] = fmaf(prm.m(HJ_VH, e), y[u][e], d2[u][e & 1]);
 #pragma unroll
   for (int u = 0; u < U; ++u) dot[u] = d2[u][0] + d2[u][1];
   if constexpr (G >= 2) {
@@ -334,37 +313,42 @@ __device__ __forceinline__ float prod_tree(const float (&q)[R]) {
   }
 }
 
+// y = gamma' + delta' L, the dot and z of one pair, in place on the tile (x: L on entry, z on exit).
+template <int D, int R, int U>
+__device__ __forceinline__ void hj_pair_z(float (&x)[U][R], const float* r, HJParams<R>& prm) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_DP, e), prm.m(HJ_GP, e));
+  prm.template load<HJ_IL, kHjW>(r);
+  float dot[U];
+  hj_dots<D, R, U>(x, prm, dot);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_IL, e), prm.m(HJ_NXI, e));
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(-dot[u], prm.m(HJ_RR, e), x[u][e]);
+}
+
 // One pair (reflection + Johnson) on the register tile, fast form. x holds L (pair 0: the input x)
 // on entry and the new L on exit; r points at the lane's record group of this pair and is advanced
-// to the next record (prm is reloaded for it). Returns the largest product of q = 1 + z^2 over a
-// lane's R rows of one column (+Inf / NaN: the fast form is not valid for the tile).
+// to the next record (whose first three parameters are read at the end). Returns the largest
+// product of q = 1 + z^2 over a lane's R rows of one column (+Inf / NaN: the fast form is not valid
+// for the tile). ACC = false (diagnostics build only): round 1's absolute-error asinh form.
 template <int D, int R, int U, bool LADJ, bool ACC = true>
 __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U], const float*& r, HJParams<R>& prm,
                                               uint32_t csign) {
-  float dot[U];
-  hj_dots<D, R, U>(x, prm.a, dot);
-  // z = L P + Q - dotL R (in place; the first FMA does not wait for the dot reduction)
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.P[hj_rot(e)], prm.Q[e]);
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int e = 0; e < R; ++e) x[u][e] = fmaf(-dot[u], prm.Rv[hj_rot(e)], x[u][e]);
-  // next pair's records (record n holds gamma_n, delta'_n for the output): read here, during the
-  // Johnson part, or (ACC: 32 fewer VGPRs live across it, 4 waves per SIMD) at the end of the pair
-  if constexpr (!ACC) {
-    r += 4 * D;
-    prm.load(r);
-  }
+  hj_pair_z<D, R, U>(x, r, prm);
   // stage by stage over the whole tile (U*R independent chains per stage)
   float q[U][R], t[U][R], pr[U];
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) q[u][e] = fmaf(x[u][e], x[u][e], 1.0f);
-  if constexpr (R == 8 && ACC) {
+  if constexpr (R == 8) {
 #pragma unroll
     for (int u = 0; u < U; ++u) sqrt8(t[u], q[u]);
   } else {
@@ -375,8 +359,7 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) pr[u] = prod_tree<R>(q[u]);
-  // small |z|: the Taylor form of asinh2_small (enf_frag.h) in place of q
-  if constexpr (ACC) {
+  if constexpr (ACC) {  // small |z|: the Taylor form of asinh2_small (enf_frag.h) in place of q
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -386,14 +369,9 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) t[u][e] = fabsf(x[u][e]) + t[u][e];
-  if constexpr (R == 8 && ACC) {
+  if constexpr (R == 8) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      float w8[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) w8[e] = t[u][e];
-      log2_8(t[u], w8);
-    }
+    for (int u = 0; u < U; ++u) log2_8_inplace(t[u]);
   } else {
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -412,10 +390,8 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
       else
         x[u][e] = copysignf(t[u][e], x[u][e]);
     }
-  if constexpr (ACC) {
-    r += 4 * D;
-    prm.load(r);
-  }
+  r += kHjW * D;
+  prm.template load<0, HJ_IL>(r);
   float m = pr[0];
 #pragma unroll
   for (int u = 1; u < U; ++u) m = fmaxf(m, pr[u]);
@@ -426,23 +402,20 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
 // FLT_MAX, ladj -Inf where the reference's fp32 1 + z^2 overflows.
 template <int D, int R, int U, bool LADJ>
 __device__ __forceinline__ void hj_pair_exact(float (&x)[U][R], float (&acc)[U], const float*& r, HJParams<R>& prm) {
-  float dot[U];
-  hj_dots<D, R, U>(x, prm.a, dot);
+  hj_pair_z<D, R, U>(x, r, prm);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) {
-      const YL yl = johnson_fwd_f32_slow(fmaf(-dot[u], prm.Rv[hj_rot(e)], fmaf(x[u][e], prm.P[hj_rot(e)], prm.Q[e])), 0.f, 1.f);
+      const YL yl = johnson_fwd_f32_slow(x[u][e], 0.f, 1.f);
       x[u][e] = yl.y;
       if (LADJ) acc[u] += yl.l;
     }
-  r += 4 * D;
-  prm.load(r);
+  r += kHjW * D;
+  prm.template load<0, HJ_IL>(r);
 }
 
-// NP > 0: the pair loop unrolled for exactly NP pairs (no loop-carried register copies between
-// the pair loop and the tile loop); NP == 0: runtime pair count a.n.
-template <int D, int R, int U, int LM, int NP, bool ACC = true>
+template <int D, int R, int U, int LM, bool ACC = true>
 struct HJBody {
   const HJArgs& a;
   const float* rec;  // this lane's record group
@@ -456,21 +429,13 @@ struct HJBody {
     float acc[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) acc[u] = 0.f;
-    // No "+v" asm fence on x here (the interpreter uses one to pin the vmcnt wait): with a runtime
-    // pair loop it made hipcc 7.2's register allocator reuse live tile registers (wrong results).
-    // The compiler's own counted waits keep the next tile's loads in flight.
     const float* r = rec;
     HJParams<R> prm;
-    prm.load(r);
+    prm.template load<0, HJ_IL>(r);
     const uint32_t csign = sign_mask_vgpr();
     // branch-free pair loop; a tile with a product overflow (|z| large, Inf, NaN) is redone below
     float m = 0.f;
-    if constexpr (NP > 0) {
-#pragma unroll
-      for (int p = 0; p < NP; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ, ACC>(x, acc, r, prm, csign));
-    } else {
-      for (int p = 0; p < n; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ, ACC>(x, acc, r, prm, csign));
-    }
+    for (int p = 0; p < n; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ, ACC>(x, acc, r, prm, csign));
     // column-uniform: the exact form's dot products read every lane of a column (DPP)
     m = group_max<HJLay<D, R, U>::G>(m);
     if (__builtin_expect(!(m <= FLT_MAX), 0)) {
@@ -478,19 +443,21 @@ struct HJBody {
 #pragma unroll
       for (int u = 0; u < U; ++u) acc[u] = 0.f;
       r = rec;
-      prm.load(r);
+      prm.template load<0, HJ_IL>(r);
       for (int p = 0; p < n; ++p) hj_pair_exact<D, R, U, LADJ>(x, acc, r, prm);
     }
-    // y = gamma_n + delta'_n L
+    // y_n = gamma_n + delta'_n L_n (record n)
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.P[hj_rot(e)], prm.a[hj_rot(e)]);
+      for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_DP, e), prm.m(HJ_GP, e));
     hj_store<D, R, U, LM, TAIL, DBG>(a, ctot, col0, x, acc, old, stage);
   }
 };
 
-// Persistent, software-pipelined tile loop (as frag_stream in enf_frag.h, for the HJLay layout).
+// Persistent, software-pipelined tile loop (as frag_stream in enf_frag.h, for the HJLay layout):
+// wave w processes tiles w, w + nwaves, ...; the next tile's loads are in flight while this tile
+// computes; the ragged last tile (N not a multiple of the tile) is processed by one wave.
 template <int D, int R, int U, int LM, int DBG, typename Body>
 __device__ __forceinline__ void hj_stream(const HJArgs& a, Body& body) {
   using L = HJLay<D, R, U>;
@@ -528,95 +495,18 @@ __device__ __forceinline__ void hj_stream(const HJArgs& a, Body& body) {
   }
 }
 
-// The same loop with the next tile staged in LDS by the load-to-LDS DMA (global_load_lds_dwordx4)
-// instead of a second register tile: per wave a 64 x 16 B x U*NF image in the load order, read
-// back with one ds_read_b128 per fragment. The DMA of tile t+1 is issued after tile t has been
-// read into registers (lgkmcnt(0)), and waited for with a counted vmcnt that leaves tile t's
-// stores in flight (they are the only vector-memory operations issued after it).
-typedef __attribute__((address_space(3))) void* lds_vptr_t;
-typedef __attribute__((address_space(1))) void* gbl_vptr_t;
-// s_waitcnt immediates, gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]
-constexpr int waitcnt_vm(int n) { return (n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14); }
-constexpr int kWaitLgkm0 = 15 | (7 << 4) | (0 << 8) | (3 << 14);
-
-template <int D, int R, int U>
-__device__ __forceinline__ void hj_glds(const HJArgs& a, int64_t col0, float* xbuf) {
-  using L = HJLay<D, R, U>;
-  const int lane = threadIdx.x & 63;
-  const float* X = (const float*)a.X;
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int h = 0; h < L::NF; ++h)
-      __builtin_amdgcn_global_load_lds((gbl_vptr_t)(X + L::col(col0, u, lane) * D + L::row(h, lane)),
-                                       (lds_vptr_t)(xbuf + (u * L::NF + h) * 256), 16, 0, 0);
-}
-
-template <int D, int R, int U>
-__device__ __forceinline__ void hj_lds_tile(const float* xbuf, float (&x)[U][R]) {
-  constexpr int NF = R / 4;
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int h = 0; h < NF; ++h) {
-      const u32x4 v4 = reinterpret_cast<const u32x4*>(xbuf + (u * NF + h) * 256)[lane];
-      __builtin_memcpy(&x[u][4 * h], &v4, 16);
-    }
-}
-
-template <int D, int R, int U, int LM, typename Body>
-__device__ __forceinline__ void hj_stream_lds(const HJArgs& a, Body& body, float* xbuf) {
-  using L = HJLay<D, R, U>;
-  constexpr int64_t CT = L::TC;
-  constexpr int NST = U * L::NF + (LM > 0 ? L::NLS : 0);  // vector-memory ops a tile issues after the DMA
-  const int64_t ntiles_full = a.N / CT;
-  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) +
-                          __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  float x[U][R], old[L::NLS];
-  int64_t t = wave_id;
-  if (t < ntiles_full) {
-    hj_glds<D, R, U>(a, t * CT, xbuf);
-    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-    for (;;) {
-      hj_lds_tile<D, R, U>(xbuf, x);
-      __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // the image is in registers before it is refilled
-      const int64_t tn = t + nwaves;
-      if (tn < ntiles_full) hj_glds<D, R, U>(a, tn * CT, xbuf);
-      hj_load_old<D, R, U, LM>(a, t * CT, old, false);
-      body.template tile<false, 0>(t * CT, x, old);
-      if (tn >= ntiles_full) break;
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(NST));
-      t = tn;
-    }
-  }
-  if (ntiles_full * CT < a.N && wave_id == ntiles_full % nwaves) {
-    const int64_t c0 = ntiles_full * CT;
-    hj_load<D, R, U, true, 0>(a, c0, x);
-    hj_load_old<D, R, U, LM>(a, c0, old, true);
-    body.template tile<true, 0>(c0, x, old);
-  }
-}
-
-// GLDS: stage the next tile through LDS (hj_stream_lds) instead of a second register tile.
-template <int D, int R, int U, int LM, int OCC, int DBG, int NP, int GLDS = 0, bool ACC = true>
+template <int D, int R, int U, int LM, int OCC, int DBG, bool ACC = true>
 __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   const int n = a.n;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* scr = reinterpret_cast<double*>(smem);
-  float* ctotp = reinterpret_cast<float*>(scr + 3 * kHjMaxPairs);
+  float* ctotp = reinterpret_cast<float*>(scr + 2 * kHjMaxPairs);
   float* stage = reinterpret_cast<float*>(smem + kHjScratch) + (threadIdx.x >> 6) * kStagePerWave;
   float* rec = reinterpret_cast<float*>(smem + kHjHeader);
   build_hj_program<D, R>(a, n, rec, scr, ctotp);
   constexpr int G = HJLay<D, R, U>::G;
-  HJBody<D, R, U, LM, NP, ACC> body{a, rec + ((threadIdx.x & 63) % G) * 4 * R, *ctotp, stage, n};
-  if constexpr (GLDS && DBG == 0) {
-    float* xbuf = rec + (size_t)(n + 1) * 4 * D + (threadIdx.x >> 6) * (U * R * 64);
-    hj_stream_lds<D, R, U, LM>(a, body, xbuf);
-  } else {
-    hj_stream<D, R, U, LM, DBG>(a, body);
-  }
+  HJBody<D, R, U, LM, ACC> body{a, rec + ((threadIdx.x & 63) % G) * kHjW * R, *ctotp, stage, n};
+  hj_stream<D, R, U, LM, DBG>(a, body);
 }
 
 int hj_program_pairs(const FlowArgs& a) {
@@ -628,42 +518,34 @@ int hj_program_pairs(const FlowArgs& a) {
   return a.nsteps / 2;
 }
 
-template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, int NP = 0, int GLDS = 0, bool ACC = true>
+template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, bool ACC = true>
 static hipError_t launch_hj(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
-  const size_t lds = hj_lds_bytes(D, h.n) + (GLDS ? (size_t)4 * U * R * 64 * sizeof(float) : 0);
-  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, NP, GLDS, ACC>);
+  const size_t lds = hj_lds_bytes(D, h.n);
+  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, ACC>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)HJLay<D, R, U>::TC * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, NP, GLDS, ACC>), dim3((unsigned)blocks), dim3(256), lds, st,
-                     h);
+  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, ACC>), dim3((unsigned)blocks), dim3(256), lds, st, h);
   return hipGetLastError();
 }
 
-// Default R = 8 rows per lane, U = 2 slabs (16 values per lane). Tuning variants (development only,
-// fp32 D = 32 with ladj): ENF_HJ_R in {4, 8, 16} (U = 16 / R), ENF_HJ_U2 = 1 doubles U.
+// R = 8 rows per lane, U = 2 slabs (16 values per lane). Diagnostics build only (ENF_DIAG):
+// ENF_DEBUG_MODE 1/2 (synthesized tile / no stores), ENF_HJ_FASTASINH = 1 (round 1's asinh form).
 template <int LM>
 static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, const DeviceInfo& dev) {
   (void)dbg;
   if (D == 32) {
 #if ENF_DIAG
     if constexpr (LM == 1) {
-      static const int r = ENF_KNOB("ENF_HJ_R", 8);
-      static const int u2 = ENF_KNOB("ENF_HJ_U2", 0);
       static const int fast = ENF_KNOB("ENF_HJ_FASTASINH", 0);
-      if (dbg == 1) return fast ? launch_hj<32, 8, 2, 1, 4, 1, 0, 0, false>(a, st, dev) : launch_hj<32, 8, 2, 1, 4, 1>(a, st, dev);
-      if (dbg == 2) return fast ? launch_hj<32, 8, 2, 1, 4, 2, 0, 0, false>(a, st, dev) : launch_hj<32, 8, 2, 1, 4, 2>(a, st, dev);
-      if (fast) return launch_hj<32, 8, 2, 1, 4, 0, 0, 0, false>(a, st, dev);
-      if (r == 4) return u2 ? launch_hj<32, 4, 8, 1>(a, st, dev) : launch_hj<32, 4, 4, 1>(a, st, dev);
-      if (r == 16) return launch_hj<32, 16, 1, 1>(a, st, dev);
-      if (u2) return launch_hj<32, 8, 4, 1>(a, st, dev);
-      static const int glds = ENF_KNOB("ENF_HJ_GLDS", 0);
-      if (glds) return launch_hj<32, 8, 2, 1, 4, 0, 0, 1>(a, st, dev);
+      if (dbg == 1) return fast ? launch_hj<32, 8, 2, 1, 4, 1, false>(a, st, dev) : launch_hj<32, 8, 2, 1, 4, 1>(a, st, dev);
+      if (dbg == 2) return fast ? launch_hj<32, 8, 2, 1, 4, 2, false>(a, st, dev) : launch_hj<32, 8, 2, 1, 4, 2>(a, st, dev);
+      if (fast) return launch_hj<32, 8, 2, 1, 4, 0, false>(a, st, dev);
     }
 #endif
     return launch_hj<32, 8, 2, LM, 4>(a, st, dev);
   }
-  return launch_hj<64, 8, 2, LM>(a, st, dev);
+  return launch_hj<64, 8, 2, LM, 4>(a, st, dev);
 }
 
 hipError_t launch_hj_program(const FlowArgs& a, int lm, int dbg, hipStream_t st, const DeviceInfo& dev) {

@@ -15,8 +15,11 @@ elementwise, where tests/parity.py's column-normwise criterion would hide a smal
   with the per-element scale |gamma_n| + |delta_n*asinh(z_n)| = |gamma_n| + |y_hi - gamma_n|
   (SURVEY.md §7 "Parity criterion"); where z_n itself cancels (z_n = (u - xi)/lambda with u the
   last reflection's output, both O(1)) no fp32 evaluation, the reference's included, has that
-  accuracy, and the bound there is a few ulps of the last layer's input conditioning,
-  16 * 2^-24 * delta/(lambda sqrt(1+z^2)) * (|y_prev| + |vh| sum|vh y_prev| + |xi|), or 4x the
+  accuracy, and the bound there is the rounding bound of the last layer's inputs: the reflection's
+  D-term dot product alone carries up to D ulps of sum|vh y_prev| (Higham's gamma_D), the kernel
+  multiplies by the precomputed 1/lambda, xi/lambda, vh/lambda where the reference divides (three
+  more roundings), and y_prev carries the earlier layers' errors, so
+  2 (D + 8) * 2^-24 * delta/(lambda sqrt(1+z^2)) * (|y_prev| + |vh| sum|vh y_prev| + |xi|), or 4x the
   reference fp32 algorithm's own error on that element (it also exceeds the conditioning bound on a
   few elements: errors of the earlier layers enter y_prev); over all such elements the kernel's RMS
   error is within 2x the reference's.
@@ -121,8 +124,8 @@ def test_fp32_flow_homogeneous_tiny(enf, gpu, oracle, D, pairs):
 @pytest.mark.parametrize("D", [32, 64])
 def test_fp32_flow_per_element(enf, gpu, oracle, D):
     """Config-3 flow (J o H)^4, survey parameter distributions: every output element within
-    1e-5 * (|gamma_n| + |delta_n asinh z_n|) of the high-precision value, or within 16 ulps of the
-    last layer's input conditioning where z_n cancels (module docstring)."""
+    1e-5 * (|gamma_n| + |delta_n asinh z_n|) of the high-precision value, or within the rounding
+    bound of the last layer's inputs where z_n cancels (module docstring)."""
     rng = np.random.default_rng(3 * D)
     N = 100_003
     layers = hj_layers(rng, D, 4, homogeneous=False)
@@ -140,13 +143,17 @@ def test_fp32_flow_per_element(enf, gpu, oracle, D):
     Yr, _ = oracle.flow_apply(layers, X, nthreads=8)
     scale = np.abs(g) + np.abs(Yh - g)
     err, err_ref = np.abs(Y - Yh), np.abs(Yr.astype(np.float64) - Yh)
-    bound = np.maximum(np.maximum(RTOL32 * scale, 16 * 2.0 ** -24 * cond), 4 * err_ref)
+    bound = np.maximum(np.maximum(RTOL32 * scale, 2 * (D + 8) * 2.0 ** -24 * cond), 4 * err_ref)
     ok = err <= bound
     bad = np.argwhere(~ok)
-    assert ok.all(), f"{bad.shape[0]} elements fail, worst {np.max(err / bound):.2f} x bound; first {bad[:3].tolist()}"
+    info = [(tuple(b), f"err {err[tuple(b)]:.2e} ref {err_ref[tuple(b)]:.2e} scale {scale[tuple(b)]:.2e} "
+                       f"cond {cond[tuple(b)]:.2e} z {z[tuple(b)]:.2e} y {Yh[tuple(b)]:.2e}") for b in bad[:4]]
+    assert ok.all(), f"{bad.shape[0]} elements fail, worst {np.max(err / bound):.2f} x bound; {info}"
     hard = err_ref > RTOL32 * scale  # where the reference itself misses the elementwise bound
     if hard.any():
         rms, rms_ref = np.sqrt(np.mean(err[hard] ** 2)), np.sqrt(np.mean(err_ref[hard] ** 2))
+        print(f"D={D}: {hard.sum()} elements where the reference misses 1e-5*scale; RMS error {rms:.3e} vs the "
+              f"reference's {rms_ref:.3e}")
         assert rms <= 2 * rms_ref, f"RMS error {rms:.3e} vs reference {rms_ref:.3e} on {hard.sum()} elements"
     # the elementwise criterion proper holds wherever z_n does not cancel
     big = np.abs(z) > 0.25

@@ -7,6 +7,11 @@ import sys
 
 pat = sys.argv[1] if len(sys.argv) > 1 else "flow_frag"
 root = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out/pmc"
+# optional metadata k=v (D=32 N=10000000 dtype=f32 pairs=4 kernel=... git=...): bench.py matches D/N/dtype/pairs
+meta = {}
+for kv in sys.argv[3:]:
+    k, _, v = kv.partition("=")
+    meta[k] = int(v) if v.isdigit() else v
 per = collections.defaultdict(list)
 dur = []
 for p in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
@@ -35,4 +40,11 @@ if "SQ_WAVE_CYCLES" in out:
     for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
         if k in out:
             out[k + "_frac"] = out[k] / w
+if meta:
+    counters = {k: v for k, v in out.items() if k.isupper()}
+    derived = {k: v for k, v in out.items() if not k.isupper()}
+    algo = meta.get("N", 0) * (2 * meta.get("D", 0) + 1) * (4 if meta.get("dtype") == "f32" else 8)
+    out = dict(meta, source="rocprofv3 --kernel-trace --pmc, one counter group per pass (tools/pmc.sh); FETCH_SIZE "
+                            "doubled per MI355X_MICROARCH.md §HBM (gfx950 reports half of wide coalesced reads)",
+               algorithmic_bytes_per_launch=algo, counters=counters, **derived)
 print(json.dumps(out, indent=1))
