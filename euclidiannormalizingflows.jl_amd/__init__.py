@@ -5,6 +5,7 @@ installed in this image; the Julia ccall shim that binds the same C ABI is julia
 All compute goes through libenf.so (include/enf.h): hand-written HIP kernels for gfx950.
 """
 from ._lib import EnfError, version  # noqa: F401
+from .comm import EnfComm  # noqa: F401
 from .distributions import JohnsonSU  # noqa: F401
 from .trafos import (  # noqa: F401
     CenterContract,
@@ -40,5 +41,5 @@ __all__ = [
     "optimize_whitening",
     "ScaleShiftTrafo", "CenterStretch", "CenterContract", "JohnsonTrafo", "JohnsonTrafoInv",
     "HouseholderTrafo", "ComposedFunction", "compose", "inverse", "stream_with_logabsdet_jacobian", "with_logabsdet_jacobian",
-    "leaves", "Trafo", "MethodError", "DimensionMismatch", "EnfError", "version", "JohnsonSU",
+    "leaves", "Trafo", "MethodError", "DimensionMismatch", "EnfError", "version", "JohnsonSU", "EnfComm",
 ]

@@ -138,20 +138,46 @@ class Trafo:
     def __repr__(self):
         return f"{type(self).__name__}({', '.join(repr(p) for p in self.params())})"
 
-    # -- device parameter cache: list of length-D (H: D x k, column-major) contiguous tensors
-    def _device_params(self, device, dtype, D: int):
+    # -- device parameter cache: list of length-D (H: D x k, column-major) contiguous tensors. Julia's
+    # transforms are immutable; these Python objects are not, so an entry is valid only for the
+    # parameter values it was made from: reassigning a field drops the cache (__setattr__), and the
+    # key carries a fingerprint of every parameter (value bytes of host arrays, the version counter
+    # of tensors), so in-place changes are seen too.
+    def __setattr__(self, name, value):
+        if name in self.FIELDS:
+            self.__dict__.pop("_dev_cache", None)
+        object.__setattr__(self, name, value)
+
+    def _cached(self, device, dtype, D: int, make):
         key = (str(device), dtype, D)
+        fp = tuple(_fingerprint(p) for p in self.params())
         cache = self.__dict__.setdefault("_dev_cache", {})
-        if key not in cache:
-            cache[key] = [_param_to_device(p, device, dtype, D, name) for p, name in
-                          zip(self.params(), self.FIELDS)]
-        return cache[key]
+        hit = cache.get(key)
+        if hit is None or hit[0] != fp:
+            hit = (fp, make())
+            cache[key] = hit
+        return hit[1]
+
+    def _device_params(self, device, dtype, D: int):
+        return self._cached(device, dtype, D, lambda: [_param_to_device(p, device, dtype, D, name) for p, name in
+                                                       zip(self.params(), self.FIELDS)])
 
     def _k(self) -> int:
         return 0
 
     def _check_ladj_signature(self, is_vector_input: bool) -> None:
         """Raise MethodError where the reference defines no with_logabsdet_jacobian method."""
+
+
+def _fingerprint(p):
+    """Identity + content version of a parameter for the device cache key."""
+    if isinstance(p, torch.Tensor):
+        return ("t", id(p), p.data_ptr(), p._version, p.dtype, tuple(p.shape))
+    if isinstance(p, np.ndarray):
+        return ("a", p.dtype.str, p.shape, p.tobytes())
+    if isinstance(p, (list, tuple)):
+        return ("l", tuple(_fingerprint(q) for q in p))
+    return ("s", type(p).__name__, p)
 
 
 def _param_to_device(p, device, dtype, D, name):
@@ -301,9 +327,7 @@ class HouseholderTrafo(Trafo):
         return HouseholderTrafo(np.ascontiguousarray(np.asarray(V)[:, ::-1]))
 
     def _device_params(self, device, dtype, D):
-        key = (str(device), dtype, D)
-        cache = self.__dict__.setdefault("_dev_cache", {})
-        if key not in cache:
+        def make():
             V = self.V
             t = V.detach().to(device=device, dtype=dtype) if isinstance(V, torch.Tensor) else \
                 torch.as_tensor(np.asarray(V, dtype=np.float64 if dtype == torch.float64 else np.float32),
@@ -312,8 +336,8 @@ class HouseholderTrafo(Trafo):
                 t = t.reshape(-1, 1)
             if t.ndim != 2 or t.shape[0] != D:
                 raise DimensionMismatch(f"HouseholderTrafo V has {t.shape[0]} rows, data has {D}")
-            cache[key] = [t.t().contiguous()]  # column-major D x k == row-major k x D
-        return cache[key]
+            return [t.t().contiguous()]  # column-major D x k == row-major k x D
+        return self._cached(device, dtype, D, make)
 
 
 def _as_param_array(p):

@@ -19,12 +19,15 @@ negll is written to a device history buffer and copied to the host once at the e
 
 Samples ``smpls`` are the reference's VectorOfSimilarVectors flattened: a (D, N) column-major
 matrix (``flatview``). Minibatches are consecutive column ranges of
-``round(N / nbatches)`` samples (Iterators.partition, the last one possibly shorter). With a
-process group, each rank takes an equal contiguous share of every minibatch and the gradient is
+``round(N / nbatches)`` samples (Iterators.partition, the last one possibly shorter). Data-parallel
+training is opt-in (``process_group=``, ``comm=`` or ``data_parallel=True``): every rank must hold
+the SAME samples, takes an equal contiguous share of every minibatch, and the gradient is
 normalised by the GLOBAL minibatch size, so every rank applies the identical update.
 
 Trainable parameters are the array-valued fields (Optimisers/Functors treat scalar fields as
-constants). Known reference quirk: under Zygote the primal ladj of a
+constants; Zygote still returns their gradient, summed to a number). A length-1 vector field
+broadcast over the D rows is ONE trainable (its gradient is the sum over the rows; on the device
+its D copies receive that same summed gradient, so they stay equal). Known reference quirk: under Zygote the primal ladj of a
 ScaleShiftTrafo is 0 (rrule(similar_fill), src/abstract_trafo.jl:30-33), so the reference's
 recorded negll misses +sum(log|a|); ``mvnormal_negll_trafograd(..., similar_fill_quirk=True)``
 reproduces that value (the gradient is unaffected either way); optimize_whitening records the
@@ -66,6 +69,7 @@ class FlowState:
     def __init__(self, trafo, D: int, dtype, device, optimizer: Optional[ADAGrad] = None):
         self.trafos: List[Trafo] = leaves(trafo)
         self.D, self.dtype, self.device = D, dtype, device
+        self.optimizer = optimizer or ADAGrad()  # the rule Optimisers.setup stores in the state's leaves
         segs, self.trainable, self.shapes = [], [], []
         for t in self.trafos:
             for name, p in zip(t.FIELDS, t.params()):
@@ -82,9 +86,26 @@ class FlowState:
         self.offsets = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
         self.theta = torch.as_tensor(np.concatenate(segs), dtype=dtype, device=device)
         self.nparams = int(self.offsets[-1])
-        eps = (optimizer or ADAGrad()).epsilon
-        self.acc = torch.full_like(self.theta, eps)  # Optimisers.init(ADAGrad) = onevalue(epsilon, x)
+        self.acc = torch.full_like(self.theta, self.optimizer.epsilon)  # Optimisers.init(ADAGrad) = onevalue(epsilon, x)
         self._layers = self._make_layers()
+
+    def tied_segments(self):
+        """[start, end) of every trainable length-1 vector field expanded to D entries: one
+        trainable whose gradient is the sum over the D rows."""
+        return [(int(self.offsets[i]), int(self.offsets[i + 1])) for i, ((_, shape), tr) in
+                enumerate(zip(self.shapes, self.trainable)) if tr and shape == (1,) and self.D > 1]
+
+    def layout(self):
+        return (self.D, self.dtype, [type(t).__name__ for t in self.trafos], self.shapes, self.trainable)
+
+    def copy_optimizer_state_from(self, other: "FlowState") -> None:
+        """Continue from another state (optimize_whitening.jl:28-29: state = deepcopy(optstate)):
+        ADAGrad's accumulator and rule are copied, never aliased; the layouts must match."""
+        if other.layout() != self.layout():
+            raise ValueError("optstate does not match the flow: "
+                             f"{other.layout()} vs {self.layout()} (D, dtype, transforms, field shapes)")
+        self.acc = other.acc.detach().clone()
+        self.optimizer = ADAGrad(other.optimizer.eta, other.optimizer.epsilon)
 
     def _make_layers(self):
         arr = (_lib.Layer * len(self.trafos))()
@@ -127,7 +148,7 @@ class FlowState:
                         a = a[:, 0]
                     vals.append(a.copy())
                 elif self.trainable[seg]:
-                    vals.append(a.copy())
+                    vals.append(a[:1].copy() if shape == (1,) else a.copy())
                 else:
                     vals.append(getattr(t, name))
                 seg += 1
@@ -199,8 +220,13 @@ def mvnormal_negll_trafograd(trafo, X, similar_fill_quirk: bool = False):
         per = []
         for _ in t.FIELDS:
             a = g[state.offsets[seg]:state.offsets[seg + 1]]
+            _, shape = state.shapes[seg]
             if isinstance(t, HouseholderTrafo):
                 a = a.reshape(state.D, -1, order="F")
+            elif shape == ():  # a scalar field broadcast over the rows: Zygote's gradient is the sum
+                a = float(np.sum(a))
+            elif shape == (1,):
+                a = np.array([np.sum(a)])
             per.append(a)
             seg += 1
         grads.append(per)
@@ -266,33 +292,44 @@ def allreduce_sum_(buf: torch.Tensor, world: int, group=None) -> torch.Tensor:
 def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None, nbatches: int = 100,
                        nepochs: int = 100, optstate: Optional[FlowState] = None,
                        negll_history: Optional[List[float]] = None, process_group=None,
-                       similar_fill_quirk: bool = False, graph: bool = False,
+                       similar_fill_quirk: bool = False, graph: bool = False, comm=None,
+                       data_parallel: bool = False,
                        _dp_step: bool = False, _separate_update: bool = False) -> WhiteningResult:
     """src/optimize_whitening.jl:25-45 on the device (see module docstring). similar_fill_quirk=True
     records the negll the reference records under Zygote (ScaleShiftTrafo's primal ladj taken as 0,
     src/abstract_trafo.jl:30-33: + sum log|a| per sample); the updates are the same either way.
 
-    graph=True (one rank): the launches of one epoch are captured once into a HIP graph
-    (torch.cuda.CUDAGraph) and the graph is replayed per epoch, which removes the host launch gaps
-    between the ~3 launches of each minibatch step; the parameters, optimizer state and history are
-    bit-identical to the eager loop (same kernels in the same order). Multi-rank runs stay eager.
+    optstate continues a previous run as the reference does (state = deepcopy(optstate), trafo =
+    deepcopy(initial_trafo)): the parameters come from initial_trafo, the ADAGrad accumulator and rule
+    from a copy of optstate (never modified); a layout mismatch raises ValueError.
+
+    Data-parallel training is opt-in: process_group= (torch.distributed sum: RCCL on ROCm, gloo on
+    CPU), comm= (an EnfComm: RCCL through libenf on the kernels' own stream) or data_parallel=True
+    (the default group). All ranks must hold the same smpls.
+
+    graph=True: the launches of one epoch are captured once into a HIP graph (torch.cuda.CUDAGraph)
+    and the graph is replayed per epoch, which removes the host launch gaps between the launches of
+    each minibatch step; the parameters, optimizer state and history are bit-identical to the eager
+    loop (same kernels in the same order). With several ranks this needs comm= (the RCCL all-reduce
+    is captured into the graph); a torch.distributed group stays eager.
 
     Test hooks: _dp_step=True runs the data-parallel step (gradient, all-reduce, enf_whitening_apply)
     on one rank; _separate_update=True replaces enf_whitening_apply by the separate
     enf_adagrad_step / enf_householder_normalize_strided calls (identical arithmetic)."""
     import torch.distributed as dist
 
-    optimizer = optimizer or ADAGrad()
     M, _, _ = _to_device_matrix(smpls)
     D, N = M.shape
     dtype = _dtype_of(initial_trafo, M)
     M = _colmajor(M, dtype)
-    if optstate is None:
-        state = FlowState(initial_trafo, D, dtype, M.device, optimizer)
-    else:  # continue from a previous optimizer state (optimize_whitening.jl:28, 44)
-        state = optstate
+    state = FlowState(initial_trafo, D, dtype, M.device, optimizer)
+    if optstate is not None:  # continue from a previous optimizer state (optimize_whitening.jl:28-29, 44)
+        state.copy_optimizer_state_from(optstate)
+    optimizer = state.optimizer
     world, rank = 1, 0
-    if process_group is not None or (dist.is_available() and dist.is_initialized()):
+    if comm is not None:
+        world, rank = comm.nranks, comm.rank
+    elif process_group is not None or data_parallel:
         world = dist.get_world_size(process_group)
         rank = dist.get_rank(process_group)
     plan = minibatch_plan(N, nbatches, rank, world)
@@ -305,8 +342,9 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
     hbatches = householder_batches(state)
     segs = trainable_runs(state)
     ss_a = [(int(state.offsets[i]), int(state.offsets[i + 1])) for i, _ in _scaleshift_a_segments(state)]
+    tied = state.tied_segments()
     # one rank: the fused step (gradient, loss, ADAGrad and re-normalisation in three launches)
-    fused = world == 1
+    fused = world == 1 and not tied and comm is None
     runs = np.ascontiguousarray(np.array(segs, dtype=np.int64).reshape(-1))
     hbs = np.ascontiguousarray(np.array(hbatches, dtype=np.int64).reshape(-1))
     if len(segs) > 64 or len(hbatches) > 16:
@@ -340,7 +378,12 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
                 _lib.check(L.enf_flow_negll_grad(dt, D, hi - lo, Xb.data_ptr(), _ld(M), state.layers(),
                                                  len(state.trafos), out.data_ptr(), ws.data_ptr(),
                                                  ws.numel() * 8, stream))
-            allreduce_sum_(out, world, process_group)
+            if comm is not None:
+                comm.allreduce_sum_(out, stream)
+            else:
+                allreduce_sum_(out, world, process_group)
+            for s0, s1 in tied:  # one trainable broadcast over D rows: every copy gets the summed gradient
+                out[1 + s0:1 + s1] = out[1 + s0:1 + s1].sum()
             if apply_fused:  # loss, ADAGrad and re-normalisation in one launch (enf_whitening_apply)
                 _lib.check(L.enf_whitening_apply(dt, D, state.nparams, out.data_ptr(), B, state.theta.data_ptr(),
                                                  state.acc.data_ptr(), runs.ctypes.data, len(segs), hbs.ctypes.data,
@@ -361,7 +404,7 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
 
     P = len(plan)
     with torch.cuda.device(M.device):
-        if graph and world == 1 and nepochs > 0:
+        if graph and (world == 1 or comm is not None) and nepochs > 0:
             hep = torch.zeros(P, dtype=torch.float64, device=M.device)
             torch.cuda.synchronize(M.device)
             cg = torch.cuda.CUDAGraph()

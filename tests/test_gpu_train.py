@@ -256,7 +256,8 @@ def _dp_worker(rank, world, port, q):
     for _ in range(2):
         layers += [(5, rand_params(rng, 5, D, np.float64)), (3, rand_params(rng, 3, D, np.float64))]
     X = rng.standard_normal((D, 3001))
-    res = enf.optimize_whitening(colmajor_cuda(X), make_flow(enf, layers), enf.ADAGrad(), nbatches=3, nepochs=2)
+    res = enf.optimize_whitening(colmajor_cuda(X), make_flow(enf, layers), enf.ADAGrad(), nbatches=3, nepochs=2,
+                                 data_parallel=True)
     q.put((rank, res.optimizer_state.theta.cpu().numpy(), res.negll_history))
     dist.destroy_process_group()
 
