@@ -91,7 +91,7 @@ def pmc_evidence(D, N, args):
                     "issue_cycle_floor_per_simd": cyc, "pmc_effective_clock_ghz": clk,
                     "pmc_kernel_ms": dur / 1e6 if dur else None,
                     "issue_floor_frac": cyc / (clk * dur) if clk and dur else None,
-                    "wait_inst_any_frac": c.get("SQ_WAIT_INST_ANY_frac"),
+                    "wait_inst_any_frac": tr.get("SQ_WAIT_INST_ANY_frac"),
                     "lds_insts_per_launch": c.get("SQ_INSTS_LDS"),
                     "source": f"{rel} (not this run)"}
         return traffic, valu

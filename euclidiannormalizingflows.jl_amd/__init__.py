@@ -30,6 +30,7 @@ from .train import (  # noqa: F401
     FlowState,
     WhiteningResult,
     allreduce_sum_,
+    flow_vjp,
     minibatch_plan,
     mvnormal_negll_trafo,
     mvnormal_negll_trafograd,
@@ -37,7 +38,7 @@ from .train import (  # noqa: F401
 )
 
 __all__ = [
-    "ADAGrad", "FlowState", "WhiteningResult", "allreduce_sum_", "minibatch_plan", "mvnormal_negll_trafo", "mvnormal_negll_trafograd",
+    "ADAGrad", "FlowState", "WhiteningResult", "allreduce_sum_", "flow_vjp", "minibatch_plan", "mvnormal_negll_trafo", "mvnormal_negll_trafograd",
     "optimize_whitening",
     "ScaleShiftTrafo", "CenterStretch", "CenterContract", "JohnsonTrafo", "JohnsonTrafoInv",
     "HouseholderTrafo", "ComposedFunction", "compose", "inverse", "stream_with_logabsdet_jacobian", "with_logabsdet_jacobian",

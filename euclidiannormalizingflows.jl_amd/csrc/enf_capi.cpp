@@ -442,6 +442,25 @@ enf_status enf_flow_negll_grad(enf_dtype dtype, int64_t D, int64_t N, const void
   ENF_CATCH
 }
 
+enf_status enf_flow_vjp(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx, const void* dY,
+                        int64_t lddy, const void* dladj, const enf_layer* layers, int32_t nlayers, void* dX,
+                        int64_t lddx, void* dparams, void* workspace, size_t workspace_bytes, void* hip_stream) {
+  ENF_TRY
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
+  if (D < 0 || N < 0) return fail(ENF_ERR_INVALID, "D and N must be >= 0");
+  const int64_t d1 = D > 0 ? D : 1;
+  if (ldx < d1 || lddy < d1 || lddx < d1) return fail(ENF_ERR_INVALID, "ldx, lddy or lddx < D");
+  enf_status vs = validate_layers(D, layers, nlayers);
+  if (vs != ENF_OK) return vs;
+  if (N == 0 || D == 0) return ENF_OK;
+  if (!X || !dY || !dX) return fail(ENF_ERR_INVALID, "X, dY or dX is NULL");
+  if (dX == X) return fail(ENF_ERR_INVALID, "dX may not alias X");
+  if (dX == dY && lddx != lddy) return fail(ENF_ERR_INVALID, "dX aliases dY with a different leading dimension");
+  return enf::flow_vjp(dtype == ENF_F64, D, N, X, ldx, dY, lddy, dladj, layers, nlayers, dX, lddx, dparams, workspace,
+                       workspace_bytes, (hipStream_t)hip_stream);
+  ENF_CATCH
+}
+
 enf_status enf_whitening_step(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
                               const enf_layer* layers, int32_t nlayers, void* theta, void* acc, const int64_t* runs,
                               int32_t nruns, const int64_t* hbatches, int32_t nhb, double eta, double epsilon,

@@ -17,6 +17,13 @@
 //
 // The arithmetic here is the accurate library form (ocml asinh/log/exp/... in T); it is not the
 // headline path.
+//
+// enf_flow_vjp runs the same kernel with general cotangents (VJP = true): the backward pass starts
+// from g = dY and weights every step's ladj derivative by the sample's dladj (the negll loss is the
+// special case dY = Y, dladj = -1), writes the input cotangent dX = g after the last step, and the
+// block partials hold the parameter VJP summed over the samples (householder_trafo.jl:22-54,88-124:
+// the rrules of householder_trafo / chained_householder_trafo; Zygote's broadcast AD of the
+// elementwise maps).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -49,6 +56,13 @@ struct GradArgs {
   int32_t col[kMaxGradSteps];     // Householder column
   int32_t roff[kMaxGradSteps];    // record offset (elements of T) in LDS
   int32_t goff[kMaxGradSteps];    // gradient offset of the step's first parameter vector
+  // enf_flow_vjp only: the cotangents of Y (D x N, ld lddy) and of ladj (length N, may be NULL) and
+  // the output dX (D x N, ld lddx)
+  const void* dY;
+  int64_t lddy;
+  const void* dl;
+  void* dX;
+  int64_t lddx;
 };
 
 __host__ __device__ constexpr int grad_nparams(int op) {
@@ -133,13 +147,15 @@ __device__ __forceinline__ T fwd_elem(int op, T x, const T* p, T& lad) {
   }
 }
 
-// Backward of one elementwise step for one element: input x, output cotangent g (dS/dy).
-// Adds dS/dparam into dp[0..np) and returns dS/dx. S contains -ladj, hence the "- dl" terms.
+// Backward of one elementwise step for one element: input x, output cotangent g (dS/dy), ladj
+// cotangent cl (dS/dladj: -1 for the loss S, which contains -ladj). Adds dS/dparam into dp[0..np)
+// and returns dS/dx. The negll kernel passes the literal cl = -1, for which every "+ cl*t" /
+// "- cl*t" below is exactly the subtraction / addition of t.
 template <typename T>
-__device__ __forceinline__ T bwd_elem(int op, T x, T g, const T* p, T* dp) {
+__device__ __forceinline__ T bwd_elem(int op, T x, T g, const T* p, T* dp, T cl) {
   switch (op) {
     case OP_SCALESHIFT: {  // y = x a + b ; l = log|a|
-      dp[0] += g * x - (T)1 / p[0];
+      dp[0] += g * x + cl * ((T)1 / p[0]);
       dp[1] += g;
       return g * p[0];
     }
@@ -148,20 +164,20 @@ __device__ __forceinline__ T bwd_elem(int op, T x, T g, const T* p, T* dp) {
       const T z = (x - p[2]) / lm;
       const T s2 = (T)1 + z * z, s = sqrt(s2);
       dp[0] += g;
-      dp[1] += g * asinh(z) - (T)1 / dl;
-      dp[2] += -g * dl / (lm * s) - z / (lm * s2);
-      dp[3] += -g * dl * z / (lm * s) + (T)1 / lm - z * z / (lm * s2);
-      return g * dl / (lm * s) + z / (lm * s2);
+      dp[1] += g * asinh(z) + cl * ((T)1 / dl);
+      dp[2] += -g * dl / (lm * s) + cl * (z / (lm * s2));
+      dp[3] += (-g * dl * z / (lm * s) - cl * ((T)1 / lm)) + cl * (z * z / (lm * s2));
+      return g * dl / (lm * s) - cl * (z / (lm * s2));
     }
     case OP_JOHNSON_INV: {  // y = lm*sinh(w) + xi, w = (x - gm)/dl ; l = log|lm/dl| + log cosh w
       const T dl = p[1], lm = p[3];
       const T w = (x - p[0]) / dl;
       const T ch = cosh(w), th = tanh(w);
-      dp[0] += -g * lm * ch / dl + th / dl;
-      dp[1] += -g * lm * ch * w / dl + (T)1 / dl + th * w / dl;
+      dp[0] += -g * lm * ch / dl - cl * (th / dl);
+      dp[1] += (-g * lm * ch * w / dl - cl * ((T)1 / dl)) - cl * (th * w / dl);
       dp[2] += g;
-      dp[3] += g * sinh(w) - (T)1 / lm;
-      return g * lm * ch / dl - th / dl;
+      dp[3] += g * sinh(w) + cl * ((T)1 / lm);
+      return g * lm * ch / dl + cl * (th / dl);
     }
     case OP_CENTER_CONTRACT: {
       // y = (softplus(t1) - softplus(t2))/b, t1 = b(xu - a), t2 = -b(xu + a), xu = x - c
@@ -173,10 +189,10 @@ __device__ __forceinline__ T bwd_elem(int op, T x, T g, const T* p, T* dp) {
       const T q1 = s1 * ((T)1 - s1), q2 = s2 * ((T)1 - s2);
       const T dydx = ss, dyda = s2 - s1, dydb = (s1 * (xu - a) + s2 * (xu + a)) / b - y / b;
       const T dldx = (q1 * b - q2 * b) / ss, dlda = -(q1 + q2) * b / ss, dldb = (q1 * (xu - a) - q2 * (xu + a)) / ss;
-      dp[0] += g * dyda - dlda;
-      dp[1] += g * dydb - dldb;
-      dp[2] += -(g * dydx - dldx);  // d/dc = -d/dx
-      return g * dydx - dldx;
+      dp[0] += g * dyda + cl * dlda;
+      dp[1] += g * dydb + cl * dldb;
+      dp[2] += -(g * dydx + cl * dldx);  // d/dc = -d/dx
+      return g * dydx + cl * dldx;
     }
     case OP_CENTER_STRETCH: {
       // y = cs(x) with cc(y) = x: dy/dx = 1/cc'(y), dy/dth = -dcc/dth(y)/cc'(y);
@@ -196,16 +212,16 @@ __device__ __forceinline__ T bwd_elem(int op, T x, T g, const T* p, T* dp) {
       const T dyda = -cc_a / ss, dydb = -cc_b / ss, dydc = -cc_c / ss;
       const T dlda = -(lcc_y * dyda + lcc_a), dldb = -(lcc_y * dydb + lcc_b), dldc = -(lcc_y * dydc + lcc_c);
       const T dldx = -lcc_y * dydx;
-      dp[0] += g * dyda - dlda;
-      dp[1] += g * dydb - dldb;
-      dp[2] += g * dydc - dldc;
-      return g * dydx - dldx;
+      dp[0] += g * dyda + cl * dlda;
+      dp[1] += g * dydb + cl * dldb;
+      dp[2] += g * dydc + cl * dldc;
+      return g * dydx + cl * dldx;
     }
     default: return g;
   }
 }
 
-template <typename T, int D>
+template <typename T, int D, bool VJP>
 __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
   constexpr int V = 16 / (int)sizeof(T);
   constexpr int G = D >= V ? D / V : 1;
@@ -305,7 +321,7 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
       }
     }
     // ---- loss: sum_d (y^2 + log 2pi)/2 - ladj (only valid columns)
-    {
+    if constexpr (!VJP) {
       T part = 0;
 #pragma unroll
       for (int e = 0; e < V; ++e)
@@ -317,10 +333,21 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
       }
       lossp += (double)part;
     }
-    // ---- backward: g = dS/dy = y (invalid columns carry g = 0 and contribute nothing)
-    T g[V];
+    // ---- backward: g = dS/dy = y (invalid columns carry g = 0 and contribute nothing); VJP: g = dY,
+    // the ladj cotangent of each column dladj (0 when absent)
+    T g[V], cl[CPF];
+    if constexpr (VJP) {
 #pragma unroll
-    for (int e = 0; e < V; ++e) g[e] = valid[e] ? x[e] : (T)0;
+      for (int e = 0; e < V; ++e) {
+        const int64_t c = c0 + e / SEG;
+        g[e] = (valid[e] && r0 + e % SEG < a.D) ? ((const T*)a.dY)[c * a.lddy + r0 + e % SEG] : (T)0;
+      }
+#pragma unroll
+      for (int c = 0; c < CPF; ++c) cl[c] = (valid[c * SEG] && a.dl) ? ((const T*)a.dl)[c0 + c] : (T)0;
+    } else {
+#pragma unroll
+      for (int e = 0; e < V; ++e) g[e] = valid[e] ? x[e] : (T)0;
+    }
     for (int s = a.nsteps - 1; s >= 0; --s) {
       const T* as = act + s * 64 * V + lane * V;
       T xin[V];
@@ -355,7 +382,7 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
         for (int e = 0; e < V; ++e) {
           T p[4], dp[4] = {0, 0, 0, 0};
           for (int q = 0; q < np; ++q) p[q] = r[q * V + e];
-          const T gx = bwd_elem<T>(op, xin[e], g[e], p, dp);
+          const T gx = bwd_elem<T>(op, xin[e], g[e], p, dp, VJP ? cl[e / SEG] : (T)-1);
           const int row = r0 + e % SEG;
           for (int q = 0; q < np; ++q)
             wave_accumulate<G, CPF, SEG>(gacc + a.goff[s] + q * a.D, row, valid[e] ? dp[q] : (T)0, lane, a.D);
@@ -363,11 +390,19 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
         }
       }
     }
+    if constexpr (VJP) {  // dX = the cotangent after the first step
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const int64_t c = c0 + e / SEG;
+        if (valid[e] && r0 + e % SEG < a.D) ((T*)a.dX)[c * a.lddx + r0 + e % SEG] = g[e];
+      }
+    }
   }
   // ---- block partials
   for (int m = 32; m >= 1; m >>= 1) lossp += __shfl_xor(lossp, m);
   if (lane == 0) lossw[wave] = lossp;
   __syncthreads();
+  if (!a.partial) return;  // enf_flow_vjp without parameter cotangents
   double* out = (double*)a.partial + (int64_t)blockIdx.x * (1 + a.nparams);
   if (tid == 0) out[0] = lossw[0] + lossw[1] + lossw[2] + lossw[3];
   const double* g0 = reinterpret_cast<const double*>(smem);
@@ -384,6 +419,7 @@ struct ReduceArgs {
   int32_t nparams;
   int32_t D;
   int32_t nh;  // Householder columns
+  int32_t skip_loss;  // enf_flow_vjp: out has no loss slot (out[i - 1] += tot[i])
   void* out;
   double* tot;  // kSumSlices x (1 + nparams) slice totals (workspace tail); slice 0 = the total
   // per Householder column: offset of its gradient vector and its device column pointer
@@ -467,7 +503,11 @@ template <typename T>
 __global__ __launch_bounds__(256) void grad_finalize_kernel(ReduceArgs r) {
   finalize_totals<T>(r);
   T* out = (T*)r.out;
-  for (int i = threadIdx.x; i < 1 + r.nparams; i += blockDim.x) out[i] += (T)r.tot[i];
+  if (r.skip_loss) {
+    for (int i = threadIdx.x; i < r.nparams; i += blockDim.x) out[i] += (T)r.tot[1 + i];
+  } else {
+    for (int i = threadIdx.x; i < 1 + r.nparams; i += blockDim.x) out[i] += (T)r.tot[i];
+  }
 }
 
 // The rest of a single-rank optimize_whitening step in the same block (enf_whitening_step):
@@ -599,22 +639,22 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
   return ENF_OK;
 }
 
-template <typename T, int DD>
+template <typename T, int DD, bool VJP>
 hipError_t launch_grad_D(const Plan& P, hipStream_t st) {
   if (P.lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)negll_grad_kernel<T, DD>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)P.lds);
+    hipError_t e = hipFuncSetAttribute((const void*)negll_grad_kernel<T, DD, VJP>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((negll_grad_kernel<T, DD>), dim3(P.blocks), dim3(256), P.lds, st, P.ga);
+  hipLaunchKernelGGL((negll_grad_kernel<T, DD, VJP>), dim3(P.blocks), dim3(256), P.lds, st, P.ga);
   return hipGetLastError();
 }
 
-template <typename T>
+template <typename T, bool VJP = false>
 hipError_t launch_grad(const Plan& P, hipStream_t st) {
   hipError_t e0 = hipSuccess;
   switch (P.ga.Dp) {
-#define ENF_G(DD) case DD: e0 = launch_grad_D<T, DD>(P, st); break;
+#define ENF_G(DD) case DD: e0 = launch_grad_D<T, DD, VJP>(P, st); break;
     ENF_G(1) ENF_G(2) ENF_G(4) ENF_G(8) ENF_G(16) ENF_G(32) ENF_G(64)
 #undef ENF_G
     default: return hipErrorInvalidValue;
@@ -676,6 +716,41 @@ enf_status negll_grad(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx
   else hipLaunchKernelGGL((grad_finalize_kernel<float>), dim3(1), dim3(256), 0, st, P.ra);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? ENF_OK : set_error(ENF_ERR_HIP, hipGetErrorString(e));
+}
+
+enf_status flow_vjp(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const void* dY, int64_t lddy,
+                    const void* dladj, const enf_layer* layers, int32_t nlayers, void* dX, int64_t lddx, void* dparams,
+                    void* workspace, size_t workspace_bytes, hipStream_t st) {
+  Plan P;
+  enf_status s = make_plan(f64, D, N, layers, nlayers, P);
+  if (s != ENF_OK) return s;
+  if (P.lds > 160 * 1024) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_vjp: flow too large for LDS");
+  P.ga.X = X;
+  P.ga.ldx = ldx;
+  P.ga.dY = dY;
+  P.ga.lddy = lddy;
+  P.ga.dl = dladj;
+  P.ga.dX = dX;
+  P.ga.lddx = lddx;
+  if (dparams) {
+    const size_t need = ((size_t)P.blocks + kSumSlices) * (1 + (size_t)P.ga.nparams) * sizeof(double);
+    if (!workspace || workspace_bytes < need) return set_error(ENF_ERR_INVALID, "enf_flow_vjp: workspace too small");
+    P.ga.partial = workspace;
+    P.ra.partial = (const double*)workspace;
+    P.ra.tot = (double*)workspace + (size_t)P.blocks * (1 + (size_t)P.ga.nparams);
+  }
+  hipError_t e = f64 ? launch_grad<double, true>(P, st) : launch_grad<float, true>(P, st);
+  if (e == hipSuccess && dparams) {
+    hipLaunchKernelGGL(grad_sum_kernel, dim3((unsigned)((1 + P.ra.nparams + 63) / 64), kSumSlices), dim3(256), 0, st,
+                       P.ra);
+    P.ra.out = dparams;
+    P.ra.skip_loss = 1;
+    if (f64) hipLaunchKernelGGL((grad_finalize_kernel<double>), dim3(1), dim3(256), 0, st, P.ra);
+    else hipLaunchKernelGGL((grad_finalize_kernel<float>), dim3(1), dim3(256), 0, st, P.ra);
+    e = hipGetLastError();
+  }
+  if (e != hipSuccess) return set_error(ENF_ERR_HIP, hipGetErrorString(e));
+  return ENF_OK;
 }
 
 enf_status whitening_apply(bool f64, int64_t D, int64_t nparams, const void* g, int64_t B, void* theta, void* acc,

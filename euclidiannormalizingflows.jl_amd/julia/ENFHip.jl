@@ -307,6 +307,36 @@ function mvnormal_negll_trafograd(trafo::_Supported, X::HipMatrix{T}) where {T}
     g[1], d_trafo
 end
 
+# --- input / parameter VJP (enf_flow_vjp) ---------------------------------------------------------
+# The pullback of (Y, ladj) = with_logabsdet_jacobian(f, X) that Zygote builds from the reference's
+# rrules (householder_trafo_pullback_x, chained_householder_trafo_pullback_x, src/householder_trafo.jl:
+# 43-54,105-124) and broadcast AD: dX = J' dY + dladj .* grad_x(ladj) per sample, and with
+# params = true the parameter cotangent (Zygote-shaped, as mvnormal_negll_trafograd's) summed over the
+# samples. dladj = nothing is a zero ladj cotangent. All arguments share one element type.
+function flow_vjp(f::_Supported, X::HipMatrix{T}, dY::HipMatrix{T}, dladj::Union{Nothing,HipMatrix{T}} = nothing;
+                  params::Bool = false) where {T}
+    size(dY) == size(X) || throw(DimensionMismatch("dY must be $(size(X))"))
+    dladj === nothing || dladj.D * dladj.N == X.N || throw(DimensionMismatch("dladj must have N entries"))
+    fs = _leaves(f)
+    _flow_eltype(fs, T) === T || throw(ArgumentError("flow_vjp: parameters would promote the element type"))
+    layers, keep = _layers(fs, X.D, T)
+    dX = HipMatrix{T}(X.D, X.N)
+    np = params ? _param_count(layers, X.D) : 0
+    dp = params ? HipMatrix(zeros(T, np, 1)) : nothing
+    ws = params ? _grad_workspace(T, X.D, X.N, layers) : nothing
+    GC.@preserve X dY dladj layers keep dX dp ws begin
+        check(ccall((:enf_flow_vjp, libenf), Cint,
+                    (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Ptr{EnfLayer}, Int32,
+                     Ptr{Cvoid}, Int64, Ptr{Cvoid}, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
+                    _dt(T), X.D, X.N, X.buf.ptr, X.D, dY.buf.ptr, X.D, dladj === nothing ? C_NULL : dladj.buf.ptr,
+                    layers, length(layers), dX.buf.ptr, X.D, params ? dp.buf.ptr : C_NULL,
+                    params ? ws.ptr : C_NULL, params ? ws.bytes : 0, C_NULL))
+    end
+    params || return dX, nothing
+    g = vcat(zero(T), Array(dp)[:, 1])
+    dX, _tangent(f, g, 1, X.D)[1]
+end
+
 # --- RCCL communicator (enf_comm_*) for data-parallel optimize_whitening ------------------------
 mutable struct EnfComm
     h::Ptr{Cvoid}
@@ -503,6 +533,6 @@ function Random.rand(d::JohnsonSU, ::Type{HipMatrix{T}}, n::Integer; seed::UInt6
     out
 end
 
-export HipMatrix, EnfComm, comm_unique_id, allreduce_sum!, stream_with_logabsdet_jacobian
+export HipMatrix, EnfComm, comm_unique_id, allreduce_sum!, stream_with_logabsdet_jacobian, flow_vjp
 
 end # module

@@ -214,8 +214,14 @@ def mvnormal_negll_trafograd(trafo, X, similar_fill_quirk: bool = False):
     N = M.shape[1]
     res = (out / N).cpu().numpy()
     negll = float(res[0]) + (_scaleshift_ladj_const(state) if similar_fill_quirk else 0.0)
+    return negll, _tangent(state, res[1:])
+
+
+def _tangent(state: "FlowState", g: np.ndarray):
+    """Flat gradient (enf_flow_param_count layout) -> list per transform (application order) of
+    per-field arrays, shaped as Zygote returns them: a Householder field as its D x k matrix, a
+    scalar field broadcast over the rows as the sum, a length-1 vector field as a length-1 sum."""
     grads, seg = [], 0
-    g = res[1:]
     for t in state.trafos:
         per = []
         for _ in t.FIELDS:
@@ -223,14 +229,56 @@ def mvnormal_negll_trafograd(trafo, X, similar_fill_quirk: bool = False):
             _, shape = state.shapes[seg]
             if isinstance(t, HouseholderTrafo):
                 a = a.reshape(state.D, -1, order="F")
-            elif shape == ():  # a scalar field broadcast over the rows: Zygote's gradient is the sum
+            elif shape == ():
                 a = float(np.sum(a))
             elif shape == (1,):
                 a = np.array([np.sum(a)])
             per.append(a)
             seg += 1
         grads.append(per)
-    return negll, grads
+    return grads
+
+
+def flow_vjp(trafo, X, dY, dladj=None, param_grads: bool = False):
+    """Pullback of (Y, ladj) = with_logabsdet_jacobian(trafo, X) (enf_flow_vjp): returns
+    (dX, dparams) with dX[:, j] = J_j' dY[:, j] + dladj[j] * grad_x ladj_j, the cotangent Zygote's
+    pullback gives for X (src/householder_trafo.jl:43-54,105-124: the rrules' _pullback_x; broadcast
+    AD of the elementwise maps), and -- with param_grads -- the parameter cotangent summed over the
+    samples in mvnormal_negll_trafograd's per-transform layout (else None). dX has X's kind (device
+    tensor or numpy) and the promoted dtype. dladj=None is a zero ladj cotangent."""
+    M, restore, is_vec = _to_device_matrix(X)
+    if is_vec:
+        raise ValueError("flow_vjp: X must be a D x N matrix")
+    dtype = _dtype_of(trafo, M)
+    M = _colmajor(M, dtype)
+    D, N = M.shape
+    G, _, _ = _to_device_matrix(dY)
+    if tuple(G.shape) != (D, N):
+        raise ValueError(f"flow_vjp: dY has shape {tuple(G.shape)}, X is {(D, N)}")
+    G = _colmajor(G.to(M.device), dtype)
+    dl = None
+    if dladj is not None:
+        dl = torch.as_tensor(_as_cpu_array(dladj) if not isinstance(dladj, torch.Tensor) else dladj)
+        dl = dl.reshape(-1).to(device=M.device, dtype=dtype).contiguous()
+        if dl.numel() != N:
+            raise ValueError(f"flow_vjp: dladj has {dl.numel()} entries for N = {N}")
+    state = FlowState(trafo, D, dtype, M.device)
+    dX = torch.empty((N, D), dtype=dtype, device=M.device).t()  # column-major D x N
+    dp = torch.zeros(state.nparams, dtype=dtype, device=M.device) if param_grads else None
+    ws = _workspace(state, N) if param_grads else None
+    with torch.cuda.device(M.device):
+        _lib.check(_lib.lib().enf_flow_vjp(
+            _lib.ENF_F64 if dtype == torch.float64 else _lib.ENF_F32, D, N, M.data_ptr(), _ld(M), G.data_ptr(), _ld(G),
+            dl.data_ptr() if dl is not None else None, state.layers(), len(state.trafos), dX.data_ptr(), max(D, 1),
+            dp.data_ptr() if dp is not None else None, ws.data_ptr() if ws is not None else None,
+            ws.numel() * ws.element_size() if ws is not None else 0, torch.cuda.current_stream(M.device).cuda_stream))
+    grads = _tangent(state, dp.cpu().numpy()) if param_grads else None
+    orig_np, on_gpu, _ = restore
+    if not on_gpu:
+        dX = dX.cpu()
+        if orig_np:
+            dX = dX.numpy()
+    return dX, grads
 
 
 def mvnormal_negll_trafo(trafo, X) -> float:

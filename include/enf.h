@@ -24,6 +24,8 @@
  *   and stays in the host mirror; inverse flows run through enf_flow_apply with swapped ops.
  *   mvnormal_negll_trafo / mvnormal_negll_trafograd (src/optimize_whitening.jl:7-22)
  *                                                                -> enf_flow_negll_grad
+ *   Zygote.pullback of with_logabsdet_jacobian(f, X), incl. the Householder rrules
+ *     (src/householder_trafo.jl:43-54,105-124)                   -> enf_flow_vjp
  *   Optimisers.update(ADAGrad) + HouseholderTrafo functor re-normalisation
  *     (src/optimize_whitening.jl:40, src/householder_trafo.jl:134-146) -> enf_adagrad_step
  */
@@ -128,6 +130,20 @@ enf_status enf_flow_negll_grad_workspace(enf_dtype dtype, int64_t D, int64_t N,
 enf_status enf_flow_negll_grad(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
                                const enf_layer* layers, int32_t nlayers, void* out,
                                void* workspace, size_t workspace_bytes, void* hip_stream);
+/* Vector-Jacobian product of (Y, ladj) = with_logabsdet_jacobian(flow, X) (the Zygote pullback the
+ * reference's rrules build: householder_trafo_pullback_x / chained_householder_trafo_pullback_x,
+ * src/householder_trafo.jl:43-54,105-124, and broadcast AD of the elementwise maps). Given the
+ * cotangents dY (D x N, leading dim lddy) and dladj (length N; NULL = zero), writes
+ *   dX[:, j] = J_j' dY[:, j] + dladj[j] * grad_x ladj_j          (D x N, leading dim lddx)
+ * for every sample j (J_j = dY[:, j]/dX[:, j]). dX may alias dY exactly (lddx == lddy), not X.
+ * When dparams != NULL it also ACCUMULATES the parameter VJP summed over the samples into dparams
+ * (enf_flow_param_count entries, the layout of enf_flow_negll_grad's out[1:]); workspace is then
+ * required (enf_flow_negll_grad_workspace bytes), otherwise it may be NULL. The accurate library
+ * arithmetic of enf_flow_negll_grad's generic kernel; limits as enf_flow_negll_grad. */
+enf_status enf_flow_vjp(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx, const void* dY,
+                        int64_t lddy, const void* dladj, const enf_layer* layers, int32_t nlayers, void* dX,
+                        int64_t lddx, void* dparams, void* workspace, size_t workspace_bytes,
+                        void* hip_stream);
 /* In-place ADAGrad step of Optimisers.jl 0.2 (eta, epsilon) over `count` parameters:
  * acc += g.^2; theta -= eta * g ./ (sqrt.(acc) .+ epsilon), with g = grad * grad_scale.
  * params/acc/grad are device arrays of the dtype. */

@@ -170,10 +170,12 @@ def test_grad_rccl_single_rank_allreduce(enf, gpu):
     assert L.enf_comm_destroy(comm) == 0
 
 
-@pytest.mark.parametrize("D,pairs", [(32, 1), (32, 3), (32, 8), (64, 1), (64, 4)])
+@pytest.mark.parametrize("D,pairs", [(32, 1), (32, 3), (32, 4), (32, 8), (64, 1), (64, 4)])
 def test_hj_grad_kernel_vs_fp64(enf, gpu, oracle, D, pairs):
     """The fused (J∘H)^n fp32 training kernel (enf_grad_hj.hip) against the fp64 generic kernel,
-    whose gradients the finite-difference test pins; ragged N (tail tile), loss vs the oracle."""
+    whose gradients the finite-difference test pins; ragged N (tail tile), loss vs the oracle.
+    (32, 4) is config 5's flow (BASELINE.json): there both gradients are also checked against central
+    differences of the oracle's fp64 loss on 24 random coordinates."""
     rng = np.random.default_rng(50 + D + pairs)
     L64 = []
     for _ in range(pairs):
@@ -190,6 +192,19 @@ def test_hj_grad_kernel_vs_fp64(enf, gpu, oracle, D, pairs):
         for a, b in zip(p64, p32):
             a, b = np.ravel(a), np.ravel(b)
             assert np.max(np.abs(a - b)) < 1e-3 * (np.max(np.abs(a)) + 1e-3), (np.max(np.abs(a - b)), np.max(np.abs(a)))
+    if (D, pairs) == (32, 4):
+        flat_g = lambda g: np.concatenate([np.asarray(a, np.float64).reshape(-1, order="F") for per in g for a in per])
+        G64, G32 = flat_g(g64), flat_g(g32)
+        th0 = flat(L64, D)
+        scale = np.abs(G64).max()
+        for i in rng.choice(th0.size, 24, replace=False):
+            h = 1e-6 * max(1.0, abs(th0[i]))
+            tp, tm = th0.copy(), th0.copy()
+            tp[i] += h
+            tm[i] -= h
+            fd = (oracle_negll(oracle, unflat(L64, tp, D), X) - oracle_negll(oracle, unflat(L64, tm, D), X)) / (2 * h)
+            assert abs(G64[i] - fd) < 1e-6 * (abs(fd) + 1e-3 * scale), (i, G64[i], fd)
+            assert abs(G32[i] - fd) < 2e-3 * (abs(fd) + 1e-2 * scale), (i, G32[i], fd)
 
 
 def test_householder_normalize_strided(enf, gpu):

@@ -123,7 +123,7 @@ def julia_ccalls():
 def test_every_ccall_matches_the_header():
     protos = header_prototypes()
     calls = julia_ccalls()
-    assert len(calls) >= 18, len(calls)
+    assert len(calls) >= 19, len(calls)
     for sym, ret, types, args, line in calls:
         where = f"ENFHip.jl:{line} {sym}"
         assert sym in protos, f"{where}: not declared in include/enf.h"
@@ -141,7 +141,7 @@ def test_the_binding_covers_the_compute_entry_points():
     for sym in ("enf_flow_apply", "enf_flow_apply_host", "enf_flow_param_count", "enf_flow_negll_grad_workspace",
                 "enf_flow_negll_grad", "enf_whitening_step", "enf_whitening_apply", "enf_johnsonsu_eval",
                 "enf_johnsonsu_sample", "enf_comm_unique_id", "enf_comm_init", "enf_comm_destroy",
-                "enf_allreduce_sum", "enf_malloc", "enf_free", "enf_memcpy", "enf_last_error"):
+                "enf_allreduce_sum", "enf_malloc", "enf_free", "enf_memcpy", "enf_last_error", "enf_flow_vjp"):
         assert sym in bound, sym
 
 
