@@ -7,11 +7,18 @@ src/optimize_whitening.jl:37-41: the fused forward+backward negll gradient over 
 (enf_flow_negll_grad), the cross-rank sum (torch.distributed all-reduce = RCCL; none at world 1),
 ADAGrad on every trainable vector (enf_adagrad_step) and the Householder re-normalisation.
 
-    python bench_train.py [--steps 100 --warmup 5 --D 32 --N 10000000 --nbatches 100]
-    torchrun --nproc-per-node N bench_train.py ...       (one process per GPU)
+    python bench_train.py [--gpus N --steps 100 --warmup 5 --D 32 --N 10000000 --nbatches 100]
+
+--gpus N > 1 started by hand launches its N ranks itself (enf_launch.py), one process per GPU. At
+world > 1 the cross-rank sum is RCCL called through libenf (EnfComm, enf_allreduce_sum) on the
+kernels' own stream, so the whole data-parallel step -- gradient, all-reduce, update -- is captured
+into the HIP graph with the other timed steps (--graph 1, default). --selftest-cpu runs the rank
+plumbing (launch, minibatch shares, a gloo sum of a stand-in gradient, max-over-ranks) on the CPU for
+the tests; it measures nothing.
 
 Prints one JSON line (rank 0): steps/s, samples/s (global minibatch samples per second), the
-per-step time of the gradient kernel pair (HIP events) and the negll trajectory endpoints.
+per-step time of the gradient kernel pair (HIP events), every rank's time and the negll trajectory
+endpoints.
 """
 from __future__ import annotations
 
@@ -22,16 +29,50 @@ import sys
 import time
 
 import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from bench import build_flow, max_over_ranks  # noqa: E402
+import enf_launch  # noqa: E402
+from bench import build_flow, gather_ranks, max_over_ranks  # noqa: E402
+
+
+def selftest_cpu(args, world, rank):
+    """The harness on gloo without a GPU: each rank sums a stand-in gradient over its share of every
+    minibatch, the shares are summed across ranks, and every rank must end with the same update."""
+    import torch
+
+    if world > 1:
+        torch.distributed.init_process_group("gloo")
+    from enf_pkg import load
+
+    plan = load().minibatch_plan(args.N, args.nbatches, rank, world)
+    Xh = np.cos(np.arange(args.N, dtype=np.float64))
+    theta = torch.zeros(3, dtype=torch.float64)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        B, lo, hi = plan[i % len(plan)]
+        g = torch.tensor([float(Xh[lo:hi].sum()), float((Xh[lo:hi] ** 2).sum()), float(hi - lo)], dtype=torch.float64)
+        if world > 1:
+            torch.distributed.all_reduce(g)
+        assert g[2].item() == B  # the rank shares tile the minibatch exactly once
+        theta -= 0.1 * g / B
+    wall = time.perf_counter() - t0
+    per_rank = gather_ranks(wall, torch.device("cpu"), world, rank)
+    th = gather_ranks(float(theta.sum()), torch.device("cpu"), world, rank)
+    if rank == 0:
+        print(json.dumps({"metric": "optimize_whitening training steps/s (config 5)", "value": args.steps / max(per_rank),
+                          "unit": "steps/s", "n_gpus": world, "steps": args.steps, "selftest": "cpu (measures nothing)",
+                          "per_rank_s": per_rank, "ranks_agree": len(set(th)) == 1,
+                          "config": {"parallelism": f"dp{world}", "B": plan[0][0]}}))
+    if world > 1:
+        torch.distributed.destroy_process_group()
 
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--selftest-cpu", action="store_true", help="CPU tests only: rank plumbing on gloo")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--D", type=int, default=32)
@@ -40,12 +81,23 @@ def main():
     ap.add_argument("--pairs", type=int, default=4)
     ap.add_argument("--history", default="", help="write the per-step negll to this file (JSON list)")
     ap.add_argument("--graph", type=int, default=1,
-                    help="1 rank: capture the timed steps once into a HIP graph and replay it (0: eager launches)")
+                    help="capture the timed steps (incl. the RCCL all-reduce at world > 1) once into a HIP graph "
+                         "and replay it (0: eager launches)")
+    ap.add_argument("--comm", default="enf", choices=["enf", "torch"],
+                    help="world > 1: RCCL through libenf on the kernels' stream (enf; graph-capturable) or "
+                         "torch.distributed.all_reduce (torch; eager only)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # N > 1 started by hand: start the N ranks as child processes before anything touches a GPU
+    rc = enf_launch.spawn_ranks_if_needed(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
+    world, rank, local_rank = enf_launch.rank_env()
+    enf_launch.check_world(args.gpus, world)
+    if args.selftest_cpu:
+        return selftest_cpu(args, world, rank)
+    import torch
+
     if world > 1:
         import torch.distributed as dist
 
@@ -91,6 +143,9 @@ def main():
     hist = []
 
     fused = world == 1 and os.environ.get("BENCH_UNFUSED", "0") != "1"
+    comm = None
+    if not fused and args.comm == "enf":
+        comm = enf.EnfComm.from_process_group() if world > 1 else enf.EnfComm.single()
     runs = np.ascontiguousarray(np.array(segs, dtype=np.int64).reshape(-1))
     hbs = np.ascontiguousarray(np.array(hbatches, dtype=np.int64).reshape(-1))
     hdev = torch.zeros(args.warmup + args.steps, dtype=torch.float64, device=dev)
@@ -115,7 +170,10 @@ def main():
                                             len(state.trafos), out.data_ptr(), ws.data_ptr(), ws.numel() * 8, sh))
         if ev is not None:
             ev[1].record(stream)
-        enf.allreduce_sum_(out, world)
+        if comm is not None:
+            comm.allreduce_sum_(out, sh)  # RCCL on the kernels' stream
+        else:
+            enf.allreduce_sum_(out, world)
         # loss, ADAGrad and re-normalisation on every rank in one launch
         lib.check(L.enf_whitening_apply(lib.ENF_F32, D, state.nparams, out.data_ptr(), B, state.theta.data_ptr(),
                                         state.acc.data_ptr(), runs.ctypes.data, len(segs), hbs.ctypes.data,
@@ -128,7 +186,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    graph = bool(args.graph) and fused
+    graph = bool(args.graph) and (fused or comm is not None)
     if graph:
         # the timed steps as one HIP graph: captured (nothing runs), replayed once untimed (this
         # advances the optimizer by args.steps more steps), then replayed once timed
@@ -158,6 +216,7 @@ def main():
     grad_ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
     if graph:
         grad_ms /= args.steps  # the replay's event pair brackets all steps
+    per_rank_ms = gather_ranks(wall / args.steps * 1e3, dev, world, rank)
     wall, grad_ms_max = max_over_ranks([wall, grad_ms], dev, world)
     samples = sum(plan[(args.warmup + i) % len(plan)][0] for i in range(args.steps))
     negll = [float(h) for h in torch.cat(hist).cpu()]
@@ -172,13 +231,18 @@ def main():
             "grad_kernel_ms_median" if not fused else "fused_step_ms_median": grad_ms,
             "grad_kernel_ms_max_rank" if not fused else "fused_step_ms_max_rank": grad_ms_max, "dtype": "f32",
             "launch": "HIP graph of the timed steps (torch.cuda.CUDAGraph), replayed" if graph else "eager",
-            "step": "enf_whitening_step (fused, 1 rank)" if fused else "enf_flow_negll_grad + RCCL sum + enf_whitening_apply",
+            "step": "enf_whitening_step (fused, 1 rank)" if fused else
+                    "enf_flow_negll_grad + RCCL sum (" + ("libenf EnfComm" if comm is not None else "torch.distributed")
+                    + ") + enf_whitening_apply",
+            "per_rank_ms_per_step": per_rank_ms,
             "data": "synthetic: X = f_true^-1(Z), Z ~ N(0,1) (torch Philox 0x5EED), f_true seed 7, init seed 42",
             "config": {"workload": f"optimize_whitening D={D}, N={N}, nbatches={args.nbatches} "
                                    f"(B={plan[0][0]}), {args.pairs}x(J∘H), ADAGrad(0.1)",
                        "per_rank_share": plan[0][2] - plan[0][1], "parallelism": f"dp{world}"},
             "negll_first": negll[0], "negll_last": negll[-1],
         }))
+    if comm is not None:
+        comm.close()
     if world > 1:
         torch.distributed.destroy_process_group()
 

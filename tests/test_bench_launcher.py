@@ -49,3 +49,24 @@ def test_bench_world_mismatch_is_an_error():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--selftest-cpu", "--gpus", "2", "--no-cpu"],
                        capture_output=True, text=True, timeout=120, env={**os.environ, **env}, cwd=ROOT)
     assert p.returncode != 0 and "WORLD_SIZE=1" in (p.stderr + p.stdout)
+
+
+def run_bench_train(*args):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench_train.py"), "--selftest-cpu", "--steps", "7",
+                        "--N", "1003", "--nbatches", "4", *args], capture_output=True, text=True, timeout=240, env=env,
+                       cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("gpus", [1, 2, 3])
+def test_bench_train_launches_ranks(gpus):
+    """bench_train.py --gpus N starts N ranks itself; the ranks' minibatch shares tile every batch
+    (asserted inside each rank) and all ranks apply the same update."""
+    out = run_bench_train("--gpus", str(gpus))
+    assert out["n_gpus"] == gpus and len(out["per_rank_s"]) == gpus
+    assert out["ranks_agree"] and out["config"]["parallelism"] == f"dp{gpus}"
