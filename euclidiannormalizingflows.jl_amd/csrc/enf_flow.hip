@@ -39,8 +39,14 @@
 
 namespace enf {
 
+// Op sets of the interpreter instantiations: every op, or only reflections and Johnson layers (the
+// flows of configs 2-5). The step dispatch compiles only the ops of OPS, so a narrower set needs
+// fewer registers (fp64 D = 2: 208 VGPRs -> fewer, i.e. more waves per SIMD to hide fp64 latency).
+constexpr int kOpsAll = 0x3F;
+constexpr int kOpsHJ = (1 << OP_HOUSEHOLDER) | (1 << OP_JOHNSON);
+
 // Interpreter: runs the step table of the kernel arguments on one register tile, then stores it.
-template <typename T, int D, int U, int LM, bool TAIL, int DBG>
+template <typename T, int D, int U, int LM, bool TAIL, int DBG, int OPS = kOpsAll>
 __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict__ rec, T ctot,
                                           int64_t col0, Tile<T, D, U>& x,
                                           const T (&old)[LadjOut<T, D, U>::NLS][LadjOut<T, D, U>::W],
@@ -67,17 +73,24 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
     const int op = desc & 15;
     const T* __restrict__ r = rec + (desc >> 4) + grp * record_width(op) * V;
     desc = next;
-    if (op == OP_HOUSEHOLDER) step_householder<T, D, U>(x, r);
-    else if (op == OP_JOHNSON) step_johnson<T, D, U, LADJ>(x, acc, r);
-    else if (op == OP_JOHNSON_INV) step_johnson_inv<T, D, U, LADJ>(x, acc, r);
-    else if (op == OP_SCALESHIFT) step_scaleshift<T, D, U>(x, r);
-    else if (op == OP_CENTER_STRETCH) step_center_stretch<T, D, U, LADJ>(x, acc, r);
-    else step_center_contract<T, D, U, LADJ>(x, acc, r);
+    if (op == OP_HOUSEHOLDER) {
+      if constexpr ((OPS >> OP_HOUSEHOLDER) & 1) step_householder<T, D, U>(x, r);
+    } else if (op == OP_JOHNSON) {
+      if constexpr ((OPS >> OP_JOHNSON) & 1) step_johnson<T, D, U, LADJ>(x, acc, r);
+    } else if (op == OP_JOHNSON_INV) {
+      if constexpr ((OPS >> OP_JOHNSON_INV) & 1) step_johnson_inv<T, D, U, LADJ>(x, acc, r);
+    } else if (op == OP_SCALESHIFT) {
+      if constexpr ((OPS >> OP_SCALESHIFT) & 1) step_scaleshift<T, D, U>(x, r);
+    } else if (op == OP_CENTER_STRETCH) {
+      if constexpr ((OPS >> OP_CENTER_STRETCH) & 1) step_center_stretch<T, D, U, LADJ>(x, acc, r);
+    } else {
+      if constexpr ((OPS >> OP_CENTER_CONTRACT) & 1) step_center_contract<T, D, U, LADJ>(x, acc, r);
+    }
   }
   store_tile<T, D, U, LM, TAIL, DBG>(a, ctot, col0, x, acc, old, stage);
 }
 
-template <typename T, int D, int U, int LM>
+template <typename T, int D, int U, int LM, int OPS = kOpsAll>
 struct InterpBody {
   const FlowArgs& a;
   const T* rec;
@@ -86,12 +99,12 @@ struct InterpBody {
   template <bool TAIL, int DBG>
   __device__ __forceinline__ void tile(int64_t col0, Tile<T, D, U>& x,
                                        const T (&old)[LadjOut<T, D, U>::NLS][LadjOut<T, D, U>::W]) {
-    flow_tile<T, D, U, LM, TAIL, DBG>(a, rec, ctot, col0, x, old, stage);
+    flow_tile<T, D, U, LM, TAIL, DBG, OPS>(a, rec, ctot, col0, x, old, stage);
   }
 };
 
 // OCC: minimum waves per SIMD the register allocation must allow (launch-bounds occupancy hint)
-template <typename T, int D, int U, int LM, int OCC, int DBG = 0>
+template <typename T, int D, int U, int LM, int OCC, int DBG = 0, int OPS = kOpsAll>
 __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* stepc = reinterpret_cast<double*>(smem);
@@ -99,8 +112,12 @@ __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
   T* stage = reinterpret_cast<T*>(smem + kLdsScalars) + (threadIdx.x >> 6) * kStagePerWave;
   T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
   build_program<T, D, Frag<T, D>::V>(a, rec, stepc, ctotp);
-  InterpBody<T, D, U, LM> body{a, rec, (T)*ctotp, stage};
-  frag_stream<T, D, U, LM, DBG>(a, body);
+  if constexpr (DBG == 4) {  // diagnostics: the prologue alone
+    if (threadIdx.x == 0 && *ctotp == 1234.5) ((T*)a.Y)[blockIdx.x] = rec[0];
+    return;
+  }
+  InterpBody<T, D, U, LM, OPS> body{a, rec, (T)*ctotp, stage};
+  frag_stream<T, D, U, LM, DBG == 4 ? 0 : DBG>(a, body);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -299,15 +316,22 @@ hipError_t frag_grid(const void* kernel, int64_t N, int64_t cols_per_block, size
   return hipSuccess;
 }
 
-template <typename T, int D, int U, int LM, int OCC = 1, int DBG = 0>
+template <typename T, int D, int U, int LM, int OCC = 1, int DBG = 0, int OPS = kOpsAll>
 static hipError_t launch_frag(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
   using F = Frag<T, D>;
-  const void* k = reinterpret_cast<const void*>(&flow_frag_kernel<T, D, U, LM, OCC, DBG>);
+  const void* k = reinterpret_cast<const void*>(&flow_frag_kernel<T, D, U, LM, OCC, DBG, OPS>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, a.N, (int64_t)F::COLS_PER_INSTR * U * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_frag_kernel<T, D, U, LM, OCC, DBG>), dim3((unsigned)blocks), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((flow_frag_kernel<T, D, U, LM, OCC, DBG, OPS>), dim3((unsigned)blocks), dim3(256), lds, st, a);
   return hipGetLastError();
+}
+
+// the op set of a flow (bit op per step)
+static int flow_ops(const FlowArgs& a) {
+  int m = 0;
+  for (int s = 0; s < a.nsteps; ++s) m |= 1 << a.steps[s].op;
+  return m;
 }
 
 template <typename T, int LADJ>
@@ -329,6 +353,29 @@ static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, cons
       if (u == 4 && occ == 5) return launch_frag<T, 32, 4, LADJ, 5>(a, lds, st, dev);
     }
 #endif
+  }
+#if ENF_DIAG
+  if (a.D == 2) {  // C2 diagnostics: 1 = synthesized tile, 2 = also no stores, 4 = prologue only
+    static const int fdbg = ENF_KNOB("ENF_FRAG_DBG", 0);
+    if (fdbg == 1) return launch_frag<T, 2, 4, LADJ, 1, 1>(a, lds, st, dev);
+    if (fdbg == 2) return launch_frag<T, 2, 4, LADJ, 1, 2>(a, lds, st, dev);
+    if (fdbg == 4) return launch_frag<T, 2, 4, LADJ, 1, 4>(a, lds, st, dev);
+  }
+#endif
+  if ((flow_ops(a) & ~kOpsHJ) == 0) {  // reflections and Johnson layers only (configs 2-5)
+#if ENF_DIAG
+    static const int hju = ENF_KNOB("ENF_FRAG_HJU", 4);
+    if (a.D == 2 && hju == 2) return launch_frag<T, 2, 2, LADJ, 1, 0, kOpsHJ>(a, lds, st, dev);
+    if (a.D == 2 && hju == 1) return launch_frag<T, 2, 1, LADJ, 1, 0, kOpsHJ>(a, lds, st, dev);
+#endif
+    switch (a.D) {
+      case 1: return launch_frag<T, 1, 4, LADJ, 1, 0, kOpsHJ>(a, lds, st, dev);
+      case 2: return launch_frag<T, 2, 4, LADJ, 1, 0, kOpsHJ>(a, lds, st, dev);
+      case 4: return launch_frag<T, 4, 4, LADJ, 1, 0, kOpsHJ>(a, lds, st, dev);
+      case 8: return launch_frag<T, 8, 4, LADJ, 1, 0, kOpsHJ>(a, lds, st, dev);
+      case 16: return launch_frag<T, 16, 4, LADJ, 1, 0, kOpsHJ>(a, lds, st, dev);
+      default: break;
+    }
   }
   switch (a.D) {
     case 1: return launch_frag<T, 1, 4, LADJ>(a, lds, st, dev);
