@@ -88,6 +88,9 @@ enf_status validate_layers(int64_t D, const enf_layer* layers, int32_t nlayers) 
 }  // namespace
 
 namespace enf {
+// enf_cpu.cpp (host-only translation unit)
+enf_status flow_apply_cpu(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, void* Y, int64_t ldy,
+                          void* ladj, int32_t accumulate, const enf_layer* layers, int32_t nlayers, int32_t nthreads);
 // shared with enf_train.hip
 enf_status set_error(enf_status st, const char* msg) { return fail(st, msg); }
 enf_status current_device_info(DeviceInfo* out) { return device_info(out); }
@@ -410,6 +413,32 @@ enf_status enf_flow_param_count(int64_t D, const enf_layer* layers, int32_t nlay
     n += D * (layers[l].op == ENF_OP_HOUSEHOLDER ? layers[l].k : nparams_of(layers[l].op));
   *count = n;
   return ENF_OK;
+  ENF_CATCH
+}
+
+enf_status enf_flow_apply_cpu(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx, void* Y, int64_t ldy,
+                              void* ladj, int32_t accumulate_ladj, const enf_layer* layers, int32_t nlayers,
+                              int32_t nthreads) {
+  ENF_TRY
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
+  if (D < 0 || N < 0) return fail(ENF_ERR_INVALID, "D and N must be >= 0");
+  if (ldx < (D > 0 ? D : 1) || ldy < (D > 0 ? D : 1)) return fail(ENF_ERR_INVALID, "ldx or ldy < D");
+  enf_status vs = validate_layers(D, layers, nlayers);
+  if (vs != ENF_OK) return vs;
+  if (N == 0) return ENF_OK;
+  if (D > 0 && (!X || !Y)) return fail(ENF_ERR_INVALID, "X or Y is NULL");
+  const size_t elem = dtype == ENF_F64 ? 8 : 4;
+  if (D > 0 && X != Y) {
+    const char* xb = (const char*)X;
+    const char* yb = (const char*)Y;
+    const char* xe = xb + ((N - 1) * ldx + D) * elem;
+    const char* ye = yb + ((N - 1) * ldy + D) * elem;
+    if (xb < ye && yb < xe) return fail(ENF_ERR_INVALID, "X and Y overlap without being identical");
+  } else if (D > 0 && ldx != ldy) {
+    return fail(ENF_ERR_INVALID, "in-place call (X == Y) needs ldx == ldy");
+  }
+  return enf::flow_apply_cpu(dtype == ENF_F64, D, N, X, ldx, Y, ldy, ladj, accumulate_ladj, layers, D > 0 ? nlayers : 0,
+                             nthreads);
   ENF_CATCH
 }
 

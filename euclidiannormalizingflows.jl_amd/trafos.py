@@ -21,8 +21,15 @@ Adjoint row, src/abstract_trafo.jl:9); a single sample x of shape (D,) gives a 0
 Numeric types follow Julia's promotion (src/johnson_trafo.jl:30): Python ``int`` parameters do
 not promote, Python ``float`` parameters are Float64, arrays/tensors carry their own dtype.
 A composition runs as ONE fused enf_flow_apply launch per run of equal promoted type.
-Inputs that are not CUDA tensors (numpy arrays, CPU tensors) are copied to the current GPU and
-the results copied back; there is no CPU compute path.
+
+Where the data lives selects where it is computed, as in Julia (an Array runs the reference's CPU
+methods): CUDA tensors run the HIP kernels (enf_flow_apply); host data -- numpy arrays, CPU tensors
+and Python / numpy scalars -- runs libenf's host implementation (enf_flow_apply_cpu, SURVEY.md §8
+config 1 "on CPU, no GPU"). Neither is a fallback for the other: a CUDA tensor without a usable GPU
+fails, and host data never touches the GPU (stream_with_logabsdet_jacobian streams a host batch
+through the GPU explicitly). A scalar x follows Julia's broadcasting (src/johnson_trafo.jl:74-76,
+src/center_stretch.jl:37-39): with scalar parameters y and ladj are scalars; with vector parameters
+y is the length-D vector of x broadcast against them and ladj their sum.
 """
 from __future__ import annotations
 
@@ -375,8 +382,25 @@ def leaves(f) -> List[Trafo]:
 
 
 # ----------------------------------------------------------------------------- execution
+def _to_matrix(X):
+    """-> ((D, N) tensor where X lives -- CUDA or host --, restore info, is_vector)."""
+    orig_np = isinstance(X, np.ndarray)
+    if orig_np:
+        Xt = torch.from_numpy(np.asarray(X))
+    elif isinstance(X, torch.Tensor):
+        Xt = X
+    else:
+        raise TypeError(f"unsupported input type {type(X)}")
+    is_vec = Xt.ndim == 1
+    if Xt.ndim not in (1, 2):
+        raise DimensionMismatch("input must be a vector (D,) or a matrix (D, N)")
+    M = Xt.reshape(-1, 1) if is_vec else Xt
+    return M, (orig_np, Xt.is_cuda, X.device if isinstance(X, torch.Tensor) else None), is_vec
+
+
 def _to_device_matrix(X):
-    """-> (column-major (D, N) CUDA tensor, restore(Y, ladj) callable, is_vector)."""
+    """-> (column-major (D, N) CUDA tensor, restore(Y, ladj) callable, is_vector). The training and VJP
+    entry points run on the GPU only: host data is copied to the current GPU."""
     orig_np = isinstance(X, np.ndarray)
     if orig_np:
         Xt = torch.from_numpy(np.asarray(X))
@@ -392,7 +416,7 @@ def _to_device_matrix(X):
         raise DimensionMismatch("input must be a vector (D,) or a matrix (D, N)")
     if not on_gpu:
         if not torch.cuda.is_available():
-            raise RuntimeError("enf needs a ROCm GPU (torch.cuda.is_available() is False); no CPU path exists")
+            raise RuntimeError("this entry point runs on a ROCm GPU only (torch.cuda.is_available() is False)")
         Xt = Xt.to("cuda")
     M = Xt.reshape(-1, 1) if is_vec else Xt
     return M, (orig_np, on_gpu, X.device if isinstance(X, torch.Tensor) else None), is_vec
@@ -417,10 +441,26 @@ def _ld(M: torch.Tensor) -> int:
 
 
 def _run_segment(trafos, M, dtype, ladj, accumulate):
-    """One enf_flow_apply over consecutive transforms of one promoted dtype."""
+    """One enf_flow_apply (device data) or enf_flow_apply_cpu (host data) over consecutive transforms
+    of one promoted dtype."""
     D, N = M.shape
     dev = M.device
     Y = _new_colmajor(D, N, dtype, dev)
+    if not M.is_cuda:
+        keep = []
+        arr = (_lib.Layer * max(1, len(trafos)))()
+        for i, t in enumerate(trafos):
+            ps = t._device_params(dev, dtype, D)
+            keep.extend(ps)
+            arr[i].op = t.OP
+            arr[i].k = t._k()
+            for q, p in enumerate(ps):
+                arr[i].p[q] = p.data_ptr()
+        _lib.check(_lib.lib().enf_flow_apply_cpu(
+            _lib.ENF_F64 if dtype == torch.float64 else _lib.ENF_F32, D, N, M.data_ptr(), _ld(M), Y.data_ptr(),
+            _ld(Y), ladj.data_ptr() if ladj is not None else None, 1 if accumulate else 0, arr, len(trafos), 0))
+        del keep
+        return Y
     keep = []
     arr = (_lib.Layer * max(1, len(trafos)))()
     for i, t in enumerate(trafos):
@@ -440,9 +480,39 @@ def _run_segment(trafos, M, dtype, ladj, accumulate):
     return Y
 
 
-def _apply(f, X, want_ladj: bool):
+def _apply_scalar(f, x, want_ladj: bool):
+    """A scalar x (Julia's x::Real methods): a 1 x 1 batch when every parameter is a scalar, else x
+    broadcast to the length-D vector of the parameters (D from the vector parameters)."""
     ts = leaves(f)
-    M, restore, is_vec = _to_device_matrix(X)
+    for t in ts:
+        if isinstance(t, HouseholderTrafo):
+            raise MethodError("HouseholderTrafo is defined for vectors and matrices only (src/householder_trafo.jl:156-160)")
+    lens = {np.size(_as_cpu_array(p)) for t in ts for p in t.params() if _is_vector(p)}
+    lens.discard(1)
+    if len(lens) > 1:
+        raise DimensionMismatch(f"parameter vectors of lengths {sorted(lens)}")
+    kx = _kind(x)
+    dt = _promote(kx, *[_kind(p) for t in ts for p in t.params()])
+    np_dt = np.float64 if dt == torch.float64 else np.float32
+    if not lens and not any(_is_vector(p) for t in ts for p in t.params()):
+        if want_ladj:
+            for t in ts:
+                t._check_ladj_signature(True)
+        Y, L = _apply(f, np.full((1, 1), x, dtype=np_dt), want_ladj)
+        y = np_dt(Y[0, 0]).item() if np_dt is np.float64 else np_dt(Y[0, 0])
+        if not want_ladj:
+            return y, None
+        return y, (np_dt(L[0, 0]).item() if np_dt is np.float64 else np_dt(L[0, 0]))
+    D = lens.pop() if lens else 1
+    return _apply(f, np.full(D, x, dtype=np_dt), want_ladj)
+
+
+def _apply(f, X, want_ladj: bool):
+    if isinstance(X, (numbers.Real, np.generic)) and not isinstance(X, bool) or \
+            (isinstance(X, np.ndarray) and X.ndim == 0):
+        return _apply_scalar(f, X.item() if isinstance(X, np.ndarray) else X, want_ladj)
+    ts = leaves(f)
+    M, restore, is_vec = _to_matrix(X)
     if want_ladj:
         for t in ts:
             t._check_ladj_signature(is_vec)
@@ -516,7 +586,7 @@ def stream_with_logabsdet_jacobian(f, X: np.ndarray, chunk_cols: int = 0, out=No
     if _promote(dt, *[_kind(p) for t in ts for p in t.params()]) != dt:
         raise MethodError("stream_with_logabsdet_jacobian: parameters would promote X's dtype")
     if not torch.cuda.is_available():
-        raise RuntimeError("enf needs a ROCm GPU (torch.cuda.is_available() is False); no CPU path exists")
+        raise RuntimeError("stream_with_logabsdet_jacobian streams through a ROCm GPU (torch.cuda.is_available() is False)")
     D, N = X.shape
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     Y = np.empty_like(X, order="F") if out is None else out

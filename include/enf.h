@@ -19,6 +19,7 @@
  *   and their Base.ComposedFunction (ChangesOfVariables 0.1: inner first, ladj_inner+ladj_outer)
  *   -> enf_flow_apply (one fused launch for the whole composition).
  *   (f)(X)  (the same call sites without ladj)                    -> enf_flow_apply, ladj = NULL.
+ *   the same calls on host Arrays (config 1, no GPU)               -> enf_flow_apply_cpu
  *   InverseFunctions.inverse(f)  is host-side parameter algebra (src/scale_shift_trafo.jl:26-30,
  *   src/center_stretch.jl:45,69, src/johnson_trafo.jl:82,107, src/householder_trafo.jl:153-154)
  *   and stays in the host mirror; inverse flows run through enf_flow_apply with swapped ops.
@@ -110,6 +111,16 @@ enf_status enf_flow_apply_host(enf_dtype dtype, int64_t D, int64_t N, const void
                                void* Y, int64_t ldy, void* ladj, int32_t accumulate_ladj,
                                const enf_layer* layers, int32_t nlayers, int64_t chunk_cols,
                                void* hip_stream);
+
+/* Host (CPU) execution, SURVEY.md §8 config 1 ("on CPU, no GPU"): the same flow with X, Y, ladj AND
+ * the layer parameter pointers in HOST memory, computed on the host cores with the reference's
+ * formulas in the data type (host libm asinh / log / exp / sinh; muladd as fma, nothing else fused),
+ * per-layer ladj summed per column and combined as ChangesOfVariables combines a left-associated
+ * f_n o ... o f_1: l_1 + (l_2 + (... + l_n)). nthreads <= 0: all hardware threads. Synchronous;
+ * needs no GPU. Y may alias X exactly (ldx == ldy). */
+enf_status enf_flow_apply_cpu(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
+                              void* Y, int64_t ldy, void* ladj, int32_t accumulate_ladj,
+                              const enf_layer* layers, int32_t nlayers, int32_t nthreads);
 
 /* ---------------------------------------------------------------- training (config 5) -- */
 /* Number of gradient entries of the flow: sum over layers of D*nparams (Householder D*k).

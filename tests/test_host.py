@@ -76,11 +76,20 @@ def test_scaleshift_method_errors(enf):
 
 
 def test_no_cpu_fallback(enf):
-    """Without a GPU the product path raises: there is no CPU compute path."""
+    """Placement selects the path, nothing falls back: host data runs libenf's host implementation
+    (enf_flow_apply_cpu) with or without a GPU; the device-only entry points (training, VJP, host
+    streaming through the GPU) raise without one instead of computing elsewhere."""
     if torch.cuda.is_available():
         pytest.skip("GPU present")
-    with pytest.raises(RuntimeError, match="GPU"):
-        enf.JohnsonTrafo(1, 2, 3, 4)(np.zeros((2, 3), np.float32))
+    Y = enf.JohnsonTrafo(1, 2, 3, 4)(np.zeros((2, 3), np.float32))
+    assert isinstance(Y, np.ndarray) and Y.shape == (2, 3)
+    X = np.zeros((2, 3), np.float32)
+    f = enf.JohnsonTrafo(np.ones(2, np.float32), 2, 3, 4)
+    for call in (lambda: enf.mvnormal_negll_trafograd(f, X), lambda: enf.flow_vjp(f, X, X),
+                 lambda: enf.optimize_whitening(X, f, enf.ADAGrad(), nbatches=1, nepochs=1),
+                 lambda: enf.stream_with_logabsdet_jacobian(f, np.asfortranarray(X))):
+        with pytest.raises(RuntimeError, match="GPU"):
+            call()
 
 
 def test_package_does_not_import_oracle(enf):
