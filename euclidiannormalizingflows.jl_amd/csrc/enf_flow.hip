@@ -111,13 +111,18 @@ __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
   double* ctotp = stepc + kMaxSteps;
   T* stage = reinterpret_cast<T*>(smem + kLdsScalars) + (threadIdx.x >> 6) * kStagePerWave;
   T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
-  build_program<T, D, Frag<T, D>::V>(a, rec, stepc, ctotp);
+  (void)ctotp;
   if constexpr (DBG == 4) {  // diagnostics: the prologue alone
-    if (threadIdx.x == 0 && *ctotp == 1234.5) ((T*)a.Y)[blockIdx.x] = rec[0];
+    const double c = build_program<T, D, Frag<T, D>::V>(a, rec, stepc);
+    if (threadIdx.x == 0 && c == 1234.5) ((T*)a.Y)[blockIdx.x] = rec[0];
     return;
   }
-  InterpBody<T, D, U, LM, OPS> body{a, rec, (T)*ctotp, stage};
-  frag_stream<T, D, U, LM, DBG == 4 ? 0 : DBG>(a, body);
+  InterpBody<T, D, U, LM, OPS> body{a, rec, (T)0, stage};
+  // the prologue runs after the wave's first tile loads are issued (frag_stream), so the HBM latency
+  // of the first tile overlaps the parameter loads and record construction
+  frag_stream<T, D, U, LM, DBG == 4 ? 0 : DBG>(a, body, [&]() {
+    body.ctot = (T)build_program<T, D, Frag<T, D>::V>(a, rec, stepc);
+  });
 }
 
 // ------------------------------------------------------------------------------------------
@@ -201,8 +206,8 @@ __global__ __launch_bounds__(256) void flow_generic_kernel(FlowArgs a) {
   double* stepc = reinterpret_cast<double*>(smem);
   double* ctotp = stepc + kMaxSteps;
   T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
-  build_program<T, 0, 1>(a, rec, stepc, ctotp);
-  const double ctot = *ctotp;
+  (void)ctotp;
+  const double ctot = build_program<T, 0, 1>(a, rec, stepc);
   const int D = a.D;
   const T* __restrict__ X = (const T*)a.X;
   T* __restrict__ Y = (T*)a.Y;
@@ -233,8 +238,8 @@ __global__ __launch_bounds__(256) void flow_lds_kernel(FlowArgs a, int ct, int d
   double* stepc = reinterpret_cast<double*>(smem);
   double* ctotp = stepc + kMaxSteps;
   T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
-  build_program<T, 0, 1>(a, rec, stepc, ctotp);
-  const double ctot = *ctotp;
+  (void)ctotp;
+  const double ctot = build_program<T, 0, 1>(a, rec, stepc);
   const int D = a.D;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   T* img = reinterpret_cast<T*>(smem + a.img_off) + (size_t)wave * ct * dp;

@@ -311,13 +311,14 @@ __global__ __launch_bounds__(256) void flow_wy_kernel(FlowArgs a) {
   double* ctotp = stepc + kMaxSteps;
   double* hs = reinterpret_cast<double*>(smem + kLdsScalars);  // dense-prologue scratch (the stage area)
   T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
-  build_program<T, D, Frag<T, D>::V>(a, rec, stepc, ctotp);
+  (void)ctotp;
+  const double ctot_d = build_program<T, D, Frag<T, D>::V>(a, rec, stepc);
   for (int s = 0; s < a.nsteps; ++s)
     if (a.steps[s].op == OP_DENSE) {
       build_dense<T, D>(a, a.steps[s], rec + a.steps[s].off, hs);
       __syncthreads();
     }
-  const T ctot = (T)*ctotp;
+  const T ctot = (T)ctot_d;
   // the waves' transpose images follow the records (program_lds_bytes, 16-byte aligned)
   u32x4* img = reinterpret_cast<u32x4*>(smem + a.img_off + (threadIdx.x >> 6) * Tt::kBytesPerWave);
   const int64_t ntiles = (a.N + W::COLS - 1) / W::COLS;

@@ -364,9 +364,11 @@ __device__ __forceinline__ void store_tile(const FlowArgs& a, T ctot, int64_t co
 // entry and from the back edge with the same outstanding memory operations (the previous tile's
 // stores behind the current tile's loads). The ragged last tile (N not a multiple of the tile) is
 // processed by one wave with masked loads and stores.
-// Body::tile<TAIL, DBG>(col0, x, old) runs the flow on one register tile and stores it.
-template <typename T, int D, int U, int LM, int DBG, typename Body>
-__device__ __forceinline__ void frag_stream(const FlowArgs& a, Body& body) {
+// Body::tile<TAIL, DBG>(col0, x, old) runs the flow on one register tile and stores it. pro() -- the
+// block prologue, with its barrier -- runs exactly once per wave, after the wave's first tile loads
+// are issued, so their HBM latency overlaps it.
+template <typename T, int D, int U, int LM, int DBG, typename Body, typename Pro>
+__device__ __forceinline__ void frag_stream(const FlowArgs& a, Body& body, Pro&& pro) {
   using F = Frag<T, D>;
   using LO = LadjOut<T, D, U>;
   static_assert(F::G == 1 || LO::TC <= kStagePerWave, "ladj staging area too small");
@@ -386,6 +388,7 @@ __device__ __forceinline__ void frag_stream(const FlowArgs& a, Body& body) {
     int64_t t1 = t + nwaves;
     load_ladj_old<T, D, U, LM>(a, t * COLS_PER_TILE, old);
     load_tile<T, D, U, false, DBG>(a, (t1 < ntiles_full ? t1 : t) * COLS_PER_TILE, xb);
+    pro();
     body.template tile<false, DBG>(t * COLS_PER_TILE, xa, old);
     while (t1 < ntiles_full) {
       const int64_t t2 = t1 + nwaves;
@@ -399,6 +402,8 @@ __device__ __forceinline__ void frag_stream(const FlowArgs& a, Body& body) {
       body.template tile<false, DBG>(t2 * COLS_PER_TILE, xa, old);
       t1 = t3;
     }
+  } else {
+    pro();
   }
   if (ntiles_full * COLS_PER_TILE < a.N && wave_id == ntiles_full % nwaves) {
     const int64_t c0 = ntiles_full * COLS_PER_TILE;

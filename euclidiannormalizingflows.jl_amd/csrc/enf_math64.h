@@ -24,6 +24,8 @@
 
 #include <cstdint>
 
+#include "enf_logtab.h"
+
 namespace enf {
 
 // n / d for d > 0 normal: v_rcp_f64 seed (relative error < 2^-22), one Newton step, and one
@@ -101,7 +103,89 @@ __device__ __forceinline__ double log1p64_ge0(double t) {
   return u < __builtin_huge_val() ? r : u;
 }
 
-// sinh(w) over the whole double range (johnson_trafo.jl:36), odd, +-Inf -> +-Inf, NaN -> NaN:
+// ---------------------------------------------------------------------------------------------
+// Table logarithm and asinh for the fused flow kernels (frag interpreter, fp64 JohnsonTrafo): no
+// division, no reciprocal, one hardware seed (v_rsq_f64) per asinh. On gfx950 every fp64 VALU
+// instruction issues at half the fp32 rate and v_rcp/v_rsq/v_sqrt_f64 cost ~3.6 of them
+// (profiles/r02_microbench15_fp64_costs.txt); msun's reduction above needs a division per log
+// (rcp + 4 FMAs) and asinh64 three reciprocals, the forms below none.
+//
+// log64_tab(u, kadd) = log(u * 2^kadd) for u >= 1 finite: u = 2^k m, m in [1, 2); j = the top B
+// fraction bits of m rounded (0..2^B), c_j = 1 + j/2^B; r = fma(m, 1/c_j, -1) (|r| <= ~2^-(B+1), one
+// rounding); log m = -log(1/c_j) + log1p(r) with the table's -log(1/c_j) in hi + lo (enf_logtab.h,
+// exact to 2^-106 for the stored 1/c_j) and log1p(r) = r + r^2 P(r) (truncation < 2^-53 r). B = 5
+// (33 entries): few distinct LDS addresses per wave, so the per-lane lookups mostly broadcast
+// instead of conflicting in the LDS banks, at two FMAs more than B = 7;
+// j = 0 has 1/c = 1 exactly, so log(1 + tiny) keeps full relative accuracy. tab: the table in LDS
+// (3 doubles per entry), filled by the kernel prologue.
+__device__ __forceinline__ double log64_tab(double u, int kadd, const double* __restrict__ tab) {
+  constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const uint64_t b = __builtin_bit_cast(uint64_t, u);
+  const uint32_t hi = (uint32_t)(b >> 32), frac = hi & 0xFFFFFu;
+  const int k = (int)(hi >> 20) - 1023 + kadd;
+  const uint32_t j = (frac + (1u << (19 - kLogTabBits))) >> (20 - kLogTabBits);
+  const double m = __builtin_bit_cast(double, ((uint64_t)(frac | 0x3FF00000u) << 32) | (uint32_t)b);
+  const double* t = tab + 3 * j;
+  const double r = fma(m, t[0], -1.0);
+  const double kd = (double)k;
+  const double lhi = fma(kd, ln2_hi, t[1]);
+  const double llo = fma(kd, ln2_lo, t[2]);
+  // log1p(r) = r + r^2 P(r), P to r^(NP-2): |r| <= 2^-(B+1), truncation r^NP/NP < 2^-53 r
+  constexpr int NP = kLogTabBits >= 7 ? 8 : kLogTabBits >= 5 ? 10 : 12;
+  double p = ((NP - 1) & 1 ? 1.0 : -1.0) / (NP - 1);
+#pragma unroll
+  for (int n = NP - 2; n >= 2; --n) p = fma(p, r, (n & 1 ? 1.0 : -1.0) / n);
+  return lhi + (r + fma(r * r, p, llo));
+}
+
+// asinh(x) over the whole double range, odd, +-Inf -> +-Inf, NaN -> NaN, with the table log:
+//   a = |x| < 2^26: s = sqrt(1 + a^2) as s1 + corr (rsq seed, one Goldschmidt step; corr carries
+//     the residual q - s1^2 AND the rounding of q = fl(1 + a^2), e_q = fma(a, a, 1 - q) exactly);
+//     u = fl(a + s1) and c its exact error (Fast2Sum) plus corr: a + sqrt(1 + a^2) = u + c, so
+//     asinh a = log(u) + c/u, and 1/u = s - a exactly (math), computed as (s1 - a) + corr (s1 - a
+//     is exact; c itself carries the Goldschmidt step's error of s1, up to 2^-44 s). For small a this is
+//     msun's log1p form without the log1p: u = 1 + (the rounded part) and c the rest.
+//   a >= 2^26: asinh a = log(2a) + 1/(4a^2) - ... = log(a) + ln2 within 2^-54 (kadd = 1).
+__device__ __forceinline__ double asinh64_tab(double x, const double* __restrict__ tab) {
+  const double a = __builtin_fabs(x);
+  const bool big = a >= 67108864.0;
+  const double q = fma(a, a, 1.0);
+  const double y = __builtin_amdgcn_rsq(q);
+  double g = q * y, h = 0.5 * y;
+  const double rr = fma(-g, h, 0.5);
+  g = fma(g, rr, g);
+  h = fma(h, rr, h);
+  const double eq = fma(a, a, 1.0 - q);
+  const double corr = (fma(-g, g, q) + eq) * h;
+  const double u0 = a + g;
+  const double c0 = (a - (u0 - g)) + corr;
+  const double cu = c0 * ((g - a) + corr);  // 1/u = s - a: g - a is exact (Sterbenz), corr completes s
+  double r = log64_tab(big ? a : u0, big ? 1 : 0, tab);
+  r += big ? 0.0 : cu;
+  r = a < __builtin_huge_val() ? r : a;  // Inf stays Inf, NaN stays NaN
+  return __builtin_copysign(r, x);
+}
+
+// log(q_1 q_2 ... q_n) for n values q_i >= 1 (a fragment column segment's 1 + z^2): the exponents
+// are summed as integers and the mantissas multiplied (< 2^n), so no product overflows; +Inf if a
+// factor is +Inf, NaN if one is NaN (the reference's log(1/sqrt(Inf)) = -Inf, NaN propagation).
+template <int NQ>
+__device__ __forceinline__ double logprod64_tab(const double (&q)[NQ], const double* __restrict__ tab) {
+  int ks = 0;
+  double mp = 1.0, qs = 0.0;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, q[i]);
+    const uint32_t hi = (uint32_t)(b >> 32);
+    ks += (int)(hi >> 20) - 1023;
+    mp *= __builtin_bit_cast(double, ((uint64_t)((hi & 0xFFFFFu) | 0x3FF00000u) << 32) | (uint32_t)b);
+    qs += q[i];
+  }
+  const double l = log64_tab(mp, ks, tab);
+  return qs < __builtin_huge_val() ? l : qs;
+}
+
+// sinh(w) over the whole double range// sinh(w) over the whole double range (johnson_trafo.jl:36), odd, +-Inf -> +-Inf, NaN -> NaN:
 //   |w| < 1: the odd Taylor series to w^17 (truncation < 1e-17 relative);
 //   else e^|w|/2 - e^-|w|/2 with e^|w| = 2^k e^r (msun e_exp.c reduction, |r| <= ln2/2, e^r by its
 //   Taylor series to r^13, truncation < 2^-57) and both halves scaled by ldexp, so sinh stays finite

@@ -12,8 +12,13 @@
 #include "enf_frag.h"
 #include "enf_math64.h"
 #include "enf_internal.h"
+#include "enf_logtab.h"
 
 namespace enf {
+
+// The fp64 log reduction table (enf_math64.h log64_tab) in LDS: copied from constant memory by
+// build_program in every fp64 kernel that runs the fragment steps (3 KB).
+static __shared__ double g_logtab[3 * kLogTabN];
 
 // ------------------------------------------------------------------------------------------
 // parameter records in LDS
@@ -78,13 +83,18 @@ __device__ __forceinline__ void param_values(int op, const LayerDesc& L, int col
 
 // Block prologue: one wave per step. Pass 1 reduces over the D distinct rows (v'v for a
 // reflection; the constant ladj part sum log|delta/lambda|, sum log|a| in double); pass 2 writes
-// the records in the layout above. ctot = sum of the per-step constants (natural log).
+// the records in the layout above. Returns ctot = sum of the per-step constants (natural log) to
+// every thread. One barrier, LDS only (lds_barrier): the caller may have global loads in flight
+// (the frag kernels issue their first tile before the prologue) and they are not waited for here.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 template <typename T, int DC, int RV>
-__device__ void build_program(const FlowArgs& a, T* __restrict__ rec, double* __restrict__ stepc,
-                              double* __restrict__ ctot) {
+__device__ double build_program(const FlowArgs& a, T* __restrict__ rec, double* __restrict__ stepc) {
   const int D = DC > 0 ? DC : a.D;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int nent = D > RV ? D : RV;  // record entries per parameter
+  if constexpr (std::is_same_v<T, double>)
+    for (int i = threadIdx.x; i < 3 * kLogTabN; i += blockDim.x) g_logtab[i] = kLogTab[i];
   for (int s = wave; s < a.nsteps; s += nw) {
     const Step st = a.steps[s];
     if (st.op == OP_DENSE) {  // built by the dense kernel's own prologue; no ladj constant
@@ -107,7 +117,14 @@ __device__ void build_program(const FlowArgs& a, T* __restrict__ rec, double* __
         part += st.op == OP_JOHNSON ? c : -c;
       }
     }
-    for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m);
+    // lanes >= D hold 0: log2(D) butterfly stages put the total in lane 0 (D = 2: one stage), then
+    // lane 0's value is made wave-uniform
+    for (int m = 1; m < D && m < 64; m <<= 1) part += __shfl_xor(part, m);
+    {
+      const uint64_t pb = __builtin_bit_cast(uint64_t, part);
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pb), hi = __builtin_amdgcn_readfirstlane((uint32_t)(pb >> 32));
+      part = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+    }
     // normalised reflection: H x = x - vh (vh'x), vh = v*sqrt(2/v'v) (householder_trafo.jl:9-10)
     const double hscale = st.op == OP_HOUSEHOLDER ? sqrt(2.0 / part) : 0.0;
     for (int i = lane; i < nent; i += 64) {
@@ -120,13 +137,10 @@ __device__ void build_program(const FlowArgs& a, T* __restrict__ rec, double* __
     if (lane == 0)
       stepc[s] = (st.op == OP_HOUSEHOLDER || st.op == OP_CENTER_STRETCH || st.op == OP_CENTER_CONTRACT) ? 0.0 : part;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double c = 0.0;
-    for (int s = 0; s < a.nsteps; ++s) c += stepc[s];
-    *ctot = c;
-  }
-  __syncthreads();
+  lds_barrier();
+  double c = 0.0;  // every thread sums the (broadcast) LDS values: no second barrier
+  for (int s = 0; s < a.nsteps; ++s) c += stepc[s];
+  return c;
 }
 
 
@@ -208,35 +222,26 @@ __device__ __forceinline__ void step_johnson(Tile<T, D, U>& x, Acc<T, D, U>& acc
           }
         johnson_from_z<D, U, LADJ>(x, acc, pg, pd, zmax);
       } else {
-        // y = gamma + delta*asinh(z) (asinh64: msun's algorithm on hardware seeds, enf_math64.h);
-        // ladj: -log(prod of the fragment column's q = 1 + z^2)/2, one log per column segment
-        // (absolute error ~1e-16). A product that overflows while its factors do not (|z| ~ 1e77
-        // and up) is summed as logs instead; an infinite q gives -Inf as the reference's
-        // log(1/sqrt(Inf)) does.
+        // y = gamma + delta*asinh(z) (asinh64_tab: enf_math64.h, the table log, no reciprocal);
+        // ladj: -log(prod of the fragment column segment's q = 1 + z^2)/2, one table log per segment
+        // (exponents summed as integers, so no product overflows; q = +Inf gives -Inf as the
+        // reference's log(1/sqrt(Inf)) does)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          double prod[CPF], q[V];
-#pragma unroll
-          for (int c = 0; c < CPF; ++c) prod[c] = 1.0;
+          double q[V];
 #pragma unroll
           for (int e = 0; e < V; ++e) {
             const double z = (x[u][e] - px[e]) * pl[e];
-            x[u][e] = fma(pd[e], asinh64(z), pg[e]);
+            x[u][e] = fma(pd[e], asinh64_tab(z, g_logtab), pg[e]);
             q[e] = fma(z, z, 1.0);
-            prod[e / SEG] *= q[e];
           }
           if (LADJ)
 #pragma unroll
             for (int c = 0; c < CPF; ++c) {
-              double l;
-              if (__builtin_expect(prod[c] == __builtin_huge_val(), 0)) {
-                l = 0.0;
+              double qs[SEG];
 #pragma unroll
-                for (int e = c * SEG; e < (c + 1) * SEG; ++e) l += log64_ge1(q[e]);
-              } else {
-                l = log64_ge1(prod[c]);
-              }
-              acc[u][c] -= 0.5 * l;
+              for (int e = 0; e < SEG; ++e) qs[e] = q[c * SEG + e];
+              acc[u][c] -= 0.5 * logprod64_tab<SEG>(qs, g_logtab);
             }
         }
       }
