@@ -210,9 +210,15 @@ enf_status flow_apply_cpu(bool f64, int64_t D, int64_t N, const void* X, int64_t
     for (int q = 0; q < 4; ++q) hl[l].p[q] = layers[l].p[q];
   }
   int nt = nthreads;
-  if (nt <= 0) {
+  if (nt <= 0) {  // all hardware threads, but at least ~2^16 element-steps per thread (a thread's start
+                  // costs tens of microseconds: config 1's 1000 x 1 batch runs on the calling thread)
     const unsigned h = std::thread::hardware_concurrency();
+    int64_t steps = 0;
+    for (int l = 0; l < nlayers; ++l) steps += layers[l].op == ENF_OP_HOUSEHOLDER ? 2 * (int64_t)layers[l].k : 1;
+    const int64_t work = N * (D > 0 ? D : 1) * (steps > 0 ? steps : 1);
+    const int64_t want = 1 + work / (1 << 16);
     nt = h > 0 ? (int)h : 1;
+    if (want < nt) nt = (int)want;
   }
   const int64_t nblocks = (N + kBlock - 1) / kBlock;
   if (nt > nblocks) nt = (int)(nblocks > 0 ? nblocks : 1);

@@ -19,6 +19,9 @@ done
 for v in ${DBGS:-}; do
   run dbg$v ENF_FRAG_DBG=$v --D 2 --N 1000000 --pairs 1 --dtype f64 --steps 50
 done
+for b in ${BPCS:-}; do
+  run bpc$b ENF_BLOCKS_PER_CU=$b --D 2 --N 1000000 --pairs 1 --dtype f64 --steps 50
+done
 for u in ${US:-2 1}; do
   run u$u ENF_FRAG_HJU=$u --D 2 --N 1000000 --pairs 1 --dtype f64 --steps 50
 done
