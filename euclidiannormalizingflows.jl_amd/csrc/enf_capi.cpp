@@ -378,8 +378,11 @@ enf_status enf_flow_apply_host(enf_dtype dtype, int64_t D, int64_t N, const void
     // slot reuse: wait until its previous results have left the device
     if (i >= Ring::kSlots && (e = hipStreamWaitEvent(r.up, r.d2h[s], 0)) != hipSuccess)
       return hip_fail(e, "hipStreamWaitEvent");
-    e = hipMemcpy2DAsync(dX, D * elem, Xc + (size_t)c0 * ldx * elem, ldx * elem, D * elem, cols,
-                         hipMemcpyHostToDevice, r.up);
+    // a dense chunk (ld == D) is one linear copy: the 2D path is a different, slower copy engine
+    // program for the same bytes (tools/ingest_bench.py)
+    e = ldx == D ? hipMemcpyAsync(dX, Xc + (size_t)c0 * ldx * elem, (size_t)D * cols * elem, hipMemcpyHostToDevice, r.up)
+                 : hipMemcpy2DAsync(dX, D * elem, Xc + (size_t)c0 * ldx * elem, ldx * elem, D * elem, cols,
+                                    hipMemcpyHostToDevice, r.up);
     if (e == hipSuccess && ladj && accumulate_ladj)
       e = hipMemcpyAsync(dL, Lc + (size_t)c0 * elem, cols * elem, hipMemcpyHostToDevice, r.up);
     if (e == hipSuccess) e = hipEventRecord(r.h2d[s], r.up);
@@ -390,8 +393,9 @@ enf_status enf_flow_apply_host(enf_dtype dtype, int64_t D, int64_t N, const void
     if (fs != ENF_OK) return fs;
     if ((e = hipEventRecord(r.comp[s], st)) != hipSuccess || (e = hipStreamWaitEvent(r.down, r.comp[s], 0)) != hipSuccess)
       return hip_fail(e, "ingest compute event");
-    e = hipMemcpy2DAsync(Yc + (size_t)c0 * ldy * elem, ldy * elem, dX, D * elem, D * elem, cols,
-                         hipMemcpyDeviceToHost, r.down);
+    e = ldy == D ? hipMemcpyAsync(Yc + (size_t)c0 * ldy * elem, dX, (size_t)D * cols * elem, hipMemcpyDeviceToHost, r.down)
+                 : hipMemcpy2DAsync(Yc + (size_t)c0 * ldy * elem, ldy * elem, dX, D * elem, D * elem, cols,
+                                    hipMemcpyDeviceToHost, r.down);
     if (e == hipSuccess && ladj) e = hipMemcpyAsync(Lc + (size_t)c0 * elem, dL, cols * elem, hipMemcpyDeviceToHost, r.down);
     if (e == hipSuccess) e = hipEventRecord(r.d2h[s], r.down);
     if (e != hipSuccess) return hip_fail(e, "ingest D2H");

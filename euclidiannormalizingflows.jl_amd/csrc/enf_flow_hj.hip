@@ -186,9 +186,11 @@ __device__ __forceinline__ void hj_store(const HJArgs& a, float ctot, int64_t co
 // Records, pair p < n: [group g][param q][R values, value 4h+e = row h*D/NF+4g+e, rotated slot for
 // the multipliers]; record n: {delta'_{n-1}, gamma_{n-1}} (the output). A lane reads each parameter
 // of its rows with NF 16-byte LDS reads.
-template <int D, int R>
+template <int D, int R, int AS>
 __device__ void build_hj_program(const HJArgs& a, int n, float* __restrict__ rec, double* __restrict__ scr,
                                  float* ctot) {
+  // AS == 2 (asinh2_med3): z is carried as sqrt(K) z, so the three z records are scaled by sqrt(K)
+  const double zs = AS == 2 ? kAsinhSqrtK : 1.0;
   constexpr int NF = R / 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   // pass 1 (one wave per pair): v'v and the constant ladj part sum_d log|delta/lambda|
@@ -221,11 +223,11 @@ __device__ void build_hj_program(const HJArgs& a, int n, float* __restrict__ rec
     q[HJ_GP] = p > 0 ? (double)a.g[p - 1][d] : 0.0;
     if (p < n) {
       const double vh = (double)a.v[p][d] * scr[2 * p];
-      const double il = 1.0 / (double)a.lam[p][d];
+      const double il = zs / (double)a.lam[p][d];
       q[HJ_VH] = vh;
       q[HJ_IL] = il;
       q[HJ_NXI] = -(double)a.xi[p][d] * il;
-      q[HJ_RR] = vh * il;
+      q[HJ_RR] = vh * il;  // sqrt(K) vh / lambda
     }
 #pragma unroll
     for (int k = 0; k < kHjW; ++k) r[k * R + (hj_rotated(k) ? hj_rot(e) : e)] = (float)q[k];
@@ -233,6 +235,8 @@ __device__ void build_hj_program(const HJArgs& a, int n, float* __restrict__ rec
   if (threadIdx.x == 0) {
     double c = 0.0;
     for (int p = 0; p < n; ++p) c += scr[2 * p + 1];
+    // AS == 2: the fast form sums -log2(q')/2 = -log2(q)/2 - log2(K)/2 per element (ln2 * acc)
+    if (AS == 2) c += 0.5 * D * n * log(kAsinhK);
     *ctot = (float)c;
   }
   __syncthreads();
@@ -337,8 +341,10 @@ __device__ __forceinline__ void hj_pair_z(float (&x)[U][R], const float* r, HJPa
 // on entry and the new L on exit; r points at the lane's record group of this pair and is advanced
 // to the next record (whose first three parameters are read at the end). Returns the largest
 // product of q = 1 + z^2 over a lane's R rows of one column (+Inf / NaN: the fast form is not valid
-// for the tile). ACC = false (diagnostics build only): round 1's absolute-error asinh form.
-template <int D, int R, int U, bool LADJ, bool ACC = true>
+// for the tile). AS selects the asinh form: 1 = the four-op merge asinh2_merge (the product), and in
+// the diagnostics build only 2 = asinh2_med3 (z' = sqrt(K) z, enf_frag.h) and 0 = round 1's
+// absolute-error form.
+template <int D, int R, int U, bool LADJ, int AS = 1>
 __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U], const float*& r, HJParams<R>& prm,
                                               uint32_t csign) {
   hj_pair_z<D, R, U>(x, r, prm);
@@ -347,7 +353,7 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < R; ++e) q[u][e] = fmaf(x[u][e], x[u][e], 1.0f);
+    for (int e = 0; e < R; ++e) q[u][e] = fmaf(x[u][e], x[u][e], AS == 2 ? (float)kAsinhK : 1.0f);
   if constexpr (R == 8) {
 #pragma unroll
     for (int u = 0; u < U; ++u) sqrt8(t[u], q[u]);
@@ -359,11 +365,12 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) pr[u] = prod_tree<R>(q[u]);
-  if constexpr (ACC) {  // small |z|: the Taylor form of asinh2_small (enf_frag.h) in place of q
+  if constexpr (AS > 0) {  // small |z|: the Taylor form (enf_frag.h) in place of q
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int e = 0; e < R; ++e) q[u][e] = asinh2_small(x[u][e], q[u][e]);
+      for (int e = 0; e < R; ++e)
+        q[u][e] = AS == 2 ? asinh2_small_k(x[u][e], q[u][e]) : asinh2_small(x[u][e], q[u][e]);
   }
 #pragma unroll
   for (int u = 0; u < U; ++u)
@@ -385,7 +392,9 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) {
-      if constexpr (ACC)
+      if constexpr (AS == 2)
+        x[u][e] = asinh2_med3(q[u][e], t[u][e]);
+      else if constexpr (AS == 1)
         x[u][e] = asinh2_merge(x[u][e], q[u][e], t[u][e], csign);
       else
         x[u][e] = copysignf(t[u][e], x[u][e]);
@@ -400,22 +409,25 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
 
 // The same pair in the exact-range elementwise form (johnson_fwd_f32_slow): asinh finite up to
 // FLT_MAX, ladj -Inf where the reference's fp32 1 + z^2 overflows.
-template <int D, int R, int U, bool LADJ>
+// (AS == 2: the records give sqrt(K) z; z is unscaled here, and the ladj carries the fast form's
+// -log2(K)/2 per element that the column constant cancels.)
+template <int D, int R, int U, bool LADJ, int AS>
 __device__ __forceinline__ void hj_pair_exact(float (&x)[U][R], float (&acc)[U], const float*& r, HJParams<R>& prm) {
   hj_pair_z<D, R, U>(x, r, prm);
+  constexpr float halflog2k = 3.4396521971792485e-07f;  // log2(K)/2
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) {
-      const YL yl = johnson_fwd_f32_slow(x[u][e], 0.f, 1.f);
+      const YL yl = johnson_fwd_f32_slow(AS == 2 ? x[u][e] * (float)kAsinhRSqrtK : x[u][e], 0.f, 1.f);
       x[u][e] = yl.y;
-      if (LADJ) acc[u] += yl.l;
+      if (LADJ) acc[u] += AS == 2 ? yl.l - halflog2k : yl.l;
     }
   r += kHjW * D;
   prm.template load<0, HJ_IL>(r);
 }
 
-template <int D, int R, int U, int LM, bool ACC = true>
+template <int D, int R, int U, int LM, int AS = 1>
 struct HJBody {
   const HJArgs& a;
   const float* rec;  // this lane's record group
@@ -435,7 +447,7 @@ struct HJBody {
     const uint32_t csign = sign_mask_vgpr();
     // branch-free pair loop; a tile with a product overflow (|z| large, Inf, NaN) is redone below
     float m = 0.f;
-    for (int p = 0; p < n; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ, ACC>(x, acc, r, prm, csign));
+    for (int p = 0; p < n; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ, AS>(x, acc, r, prm, csign));
     // column-uniform: the exact form's dot products read every lane of a column (DPP)
     m = group_max<HJLay<D, R, U>::G>(m);
     if (__builtin_expect(!(m <= FLT_MAX), 0)) {
@@ -444,7 +456,7 @@ struct HJBody {
       for (int u = 0; u < U; ++u) acc[u] = 0.f;
       r = rec;
       prm.template load<0, HJ_IL>(r);
-      for (int p = 0; p < n; ++p) hj_pair_exact<D, R, U, LADJ>(x, acc, r, prm);
+      for (int p = 0; p < n; ++p) hj_pair_exact<D, R, U, LADJ, AS>(x, acc, r, prm);
     }
     // y_n = gamma_n + delta'_n L_n (record n)
 #pragma unroll
@@ -495,7 +507,7 @@ __device__ __forceinline__ void hj_stream(const HJArgs& a, Body& body) {
   }
 }
 
-template <int D, int R, int U, int LM, int OCC, int DBG, bool ACC = true>
+template <int D, int R, int U, int LM, int OCC, int DBG, int AS = 1>
 __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   const int n = a.n;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -503,9 +515,9 @@ __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   float* ctotp = reinterpret_cast<float*>(scr + 2 * kHjMaxPairs);
   float* stage = reinterpret_cast<float*>(smem + kHjScratch) + (threadIdx.x >> 6) * kStagePerWave;
   float* rec = reinterpret_cast<float*>(smem + kHjHeader);
-  build_hj_program<D, R>(a, n, rec, scr, ctotp);
+  build_hj_program<D, R, AS>(a, n, rec, scr, ctotp);
   constexpr int G = HJLay<D, R, U>::G;
-  HJBody<D, R, U, LM, ACC> body{a, rec + ((threadIdx.x & 63) % G) * kHjW * R, *ctotp, stage, n};
+  HJBody<D, R, U, LM, AS> body{a, rec + ((threadIdx.x & 63) % G) * kHjW * R, *ctotp, stage, n};
   hj_stream<D, R, U, LM, DBG>(a, body);
 }
 
@@ -518,29 +530,37 @@ int hj_program_pairs(const FlowArgs& a) {
   return a.nsteps / 2;
 }
 
-template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, bool ACC = true>
+template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, int AS = 1>
 static hipError_t launch_hj(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
   const size_t lds = hj_lds_bytes(D, h.n);
-  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, ACC>);
+  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, AS>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)HJLay<D, R, U>::TC * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, ACC>), dim3((unsigned)blocks), dim3(256), lds, st, h);
+  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, AS>), dim3((unsigned)blocks), dim3(256), lds, st, h);
   return hipGetLastError();
 }
 
 // R = 8 rows per lane, U = 2 slabs (16 values per lane). Diagnostics build only (ENF_DIAG):
-// ENF_DEBUG_MODE 1/2 (synthesized tile / no stores), ENF_HJ_FASTASINH = 1 (round 1's asinh form).
+// ENF_DEBUG_MODE 1/2 (synthesized tile / no stores), ENF_HJ_ASINH = 0/2 (round 1's asinh form / the
+// one-med3 clamp asinh2_med3 in place of the four-op merge: 9% faster, rejected for its coherent bias,
+// DESIGN.md §3).
+template <int DBG, int LM>
+static hipError_t launch_hj_as(int as, const HJArgs& a, hipStream_t st, const DeviceInfo& dev) {
+  if (as == 0) return launch_hj<32, 8, 2, LM, 4, DBG, 0>(a, st, dev);
+  if (as == 2) return launch_hj<32, 8, 2, LM, 4, DBG, 2>(a, st, dev);
+  return launch_hj<32, 8, 2, LM, 4, DBG, 1>(a, st, dev);
+}
 template <int LM>
 static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, const DeviceInfo& dev) {
   (void)dbg;
   if (D == 32) {
 #if ENF_DIAG
     if constexpr (LM == 1) {
-      static const int fast = ENF_KNOB("ENF_HJ_FASTASINH", 0);
-      if (dbg == 1) return fast ? launch_hj<32, 8, 2, 1, 4, 1, false>(a, st, dev) : launch_hj<32, 8, 2, 1, 4, 1>(a, st, dev);
-      if (dbg == 2) return fast ? launch_hj<32, 8, 2, 1, 4, 2, false>(a, st, dev) : launch_hj<32, 8, 2, 1, 4, 2>(a, st, dev);
-      if (fast) return launch_hj<32, 8, 2, 1, 4, 0, false>(a, st, dev);
+      static const int as = ENF_KNOB("ENF_HJ_ASINH", 1);
+      if (dbg == 1) return launch_hj_as<1, 1>(as, a, st, dev);
+      if (dbg == 2) return launch_hj_as<2, 1>(as, a, st, dev);
+      return launch_hj_as<0, 1>(as, a, st, dev);
     }
 #endif
     return launch_hj<32, 8, 2, LM, 4>(a, st, dev);

@@ -140,6 +140,35 @@ __device__ __forceinline__ float asinh2_f32(float z, float q, float s, uint32_t 
   return asinh2_merge(z, asinh2_small(z, q), hw_log2(fabsf(z) + s), csign);
 }
 
+// The same two forms merged by one clamp -- a measured and REJECTED alternative, kept in the
+// diagnostics build of the compiled (J o H)^n program only (enf_flow_hj.hip AS = 2, ENF_HJ_ASINH=2):
+// 0.743 vs 0.818 ms on the headline flow, but the bias b below is coherent (the same sign as z on
+// every element that takes the log side), so through four pairs and the reflections' dot products it
+// accumulates to up to 2.6x the per-element bound of tests/test_gpu_fp32_accuracy.py (errors ~2e-5 of
+// the element's scale, where the merge form stays within it; profiles/r02_asinh_med3_ab.txt).
+//   asinh(z)/ln2 = med3(S, -t', t'),  t' = t + b
+// The Taylor form S truncated after its positive z^5 term lies above asinh|z| for every z > 0 (odd:
+// below for z < 0) and grows like z^5, while the log form t carries an absolute error below ~2.2e-7
+// (log2 units; w = |z| + sqrt(q) rounds near 1 for small |z|). With the bias b above that error the
+// clamp returns S exactly where S < t' -- the accurate small-|z| side -- and +-t' elsewhere: S is chosen
+// for |z| < ~0.17, where its truncation error (~5 z^7/112) is below b. One v_med3_f32 (half rate) in
+// place of the merge's four full-rate operations; the price is the bias b on the log side, a relative
+// error below 2e-6 near the crossover and below 4e-7 for |z| > 1 (tools/asinh32_err.py, 4M z over
+// 1e-30..1e3). The bias costs no instruction: the program carries z' = sqrt(K) z (its records for z
+// are scaled), so q' = z'^2 + K = K q, sqrt(q') = sqrt(K) s and log2(|z'| + sqrt(q')) = t + log2(K)/2,
+// i.e. b = log2(K)/2 with K = 1 + 2^-21 (b = 3.44e-7); the Taylor coefficients absorb sqrt(K) and K,
+// and the ladj's log2 q' = log2 q + log2 K is corrected in the column constant.
+constexpr double kAsinhK = 1.0 + 1.0 / 2097152.0;   // 1 + 2^-21, exact in fp32
+constexpr double kAsinhSqrtK = 1.0000002384185507;  // sqrt(K)
+constexpr double kAsinhRSqrtK = 0.9999997615815062; // 1/sqrt(K)
+__device__ __forceinline__ float asinh2_small_k(float zk, float qk) {
+  // z (A0 + A1 q + A2 q^2) / ln2 with z = zk / sqrt(K), q = qk / K
+  constexpr double rk = kAsinhRSqrtK * kLog2e;
+  return zk * fmaf(qk, fmaf(qk, (float)(kAsinhA2 * rk / (kAsinhK * kAsinhK)), (float)(kAsinhA1 * rk / kAsinhK)),
+                   (float)(kAsinhA0 * rk));
+}
+__device__ __forceinline__ float asinh2_med3(float small, float tb) { return __builtin_amdgcn_fmed3f(small, -tb, tb); }
+
 // fp32 robust Johnson element (huge |z|, Inf, NaN): the rare path of the fragment kernel and the
 // generic kernel's form. asinh stays finite for |z| up to FLT_MAX; log(1+z^2) overflows to +Inf
 // exactly where the reference's fp32 `1 + ((x-xi)/lambda)^2` does (johnson_trafo.jl:41), so

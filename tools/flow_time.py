@@ -2,7 +2,7 @@
 variants are selected by ENF_* environment knobs (enf_internal.h ENF_KNOB), one process per
 variant. Not the benchmark (bench.py times the shipping libenf.so).
 
-    ENF_HJ_FASTASINH=1 python tools/flow_time.py --D 32 --N 10000000 --pairs 4 --tag fast
+    ENF_HJ_ASINH=1 python tools/flow_time.py --D 32 --N 10000000 --pairs 4 --tag fast
 """
 from __future__ import annotations
 

@@ -14,8 +14,9 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   rc=$?; grep -E "passed|failed|FAILED|Error" $OUT/${TAG}_pytest.txt | tail -30; ok $rc || { echo "pytest crashed rc=$rc"; exit $rc; }
 fi
 echo "== A/B flow time"
-for v in ${VARIANTS:-"acc:" "fast:ENF_HJ_FASTASINH=1" "acc_compute:ENF_DEBUG_MODE=2" "acc_synth:ENF_DEBUG_MODE=1"}; do
-  tag=${v%%:*}; kv=${v#*:}
+# variants "tag:KNOB=v,KNOB=v" (comma-separated knobs)
+for v in ${VARIANTS:-merge: med3:ENF_HJ_ASINH=2 fast:ENF_HJ_ASINH=0 merge_compute:ENF_DEBUG_MODE=2 med3_compute:ENF_HJ_ASINH=2,ENF_DEBUG_MODE=2}; do
+  tag=${v%%:*}; kv=${v#*:}; kv=${kv//,/ }
   env $kv timeout -k 10 120 python tools/flow_time.py --tag $tag ${FLOW_ARGS:-} >> $OUT/${TAG}_ab.jsonl 2>> $OUT/${TAG}_ab.err
   rc=$?; [ $rc -eq 0 ] || { echo "flow_time failed rc=$rc"; tail $OUT/${TAG}_ab.err; exit $rc; }
 done

@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest -v --timeout 120 --timeout-method thread -
   tests/test_gpu_fp32_accuracy.py tests/test_gpu_parity.py ${PYTEST_ARGS:-} > $OUT/r2_pytest_acc.txt 2>&1
 rc=$?; grep -E "passed|failed|FAILED|Error" $OUT/r2_pytest_acc.txt | tail -30; ok $rc || { echo "pytest crashed rc=$rc"; exit $rc; }
 echo "== A/B flow time"
-for v in "acc:" "fast:ENF_HJ_FASTASINH=1"; do
+for v in "acc:" "fast:ENF_HJ_ASINH=0"; do
   tag=${v%%:*}; kv=${v#*:}
   env $kv timeout -k 10 120 python tools/flow_time.py --tag $tag >> $OUT/r2_ab_asinh.jsonl 2>> $OUT/r2_ab.err
   rc=$?; [ $rc -eq 0 ] || { echo "flow_time failed rc=$rc"; tail $OUT/r2_ab.err; exit $rc; }
