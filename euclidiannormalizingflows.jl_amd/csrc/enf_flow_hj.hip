@@ -341,19 +341,26 @@ __device__ __forceinline__ void hj_pair_z(float (&x)[U][R], const float* r, HJPa
 // on entry and the new L on exit; r points at the lane's record group of this pair and is advanced
 // to the next record (whose first three parameters are read at the end). Returns the largest
 // product of q = 1 + z^2 over a lane's R rows of one column (+Inf / NaN: the fast form is not valid
-// for the tile). AS selects the asinh form: 1 = the four-op merge asinh2_merge (the product), and in
-// the diagnostics build only 2 = asinh2_med3 (z' = sqrt(K) z, enf_frag.h) and 0 = round 1's
-// absolute-error form.
+// for the tile). AS selects the asinh form: 1 = the mask-first merge asinh2_mask / asinh2_pick (the
+// product), and in the diagnostics build only 3 = the same merge with its mask taken from the log2
+// (asinh2_merge), 2 = asinh2_med3 (z' = sqrt(K) z, enf_frag.h) and 0 = round 1's absolute-error form.
 template <int D, int R, int U, bool LADJ, int AS = 1>
 __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U], const float*& r, HJParams<R>& prm,
                                               uint32_t csign) {
   hj_pair_z<D, R, U>(x, r, prm);
   // stage by stage over the whole tile (U*R independent chains per stage)
   float q[U][R], t[U][R], pr[U];
+  uint32_t msel[U][R];  // AS == 1: the select mask of asinh2_pick, from q (before the transcendentals)
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) q[u][e] = fmaf(x[u][e], x[u][e], AS == 2 ? (float)kAsinhK : 1.0f);
+  if constexpr (AS == 1) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < R; ++e) msel[u][e] = asinh2_mask(q[u][e], csign);
+  }
   if constexpr (R == 8) {
 #pragma unroll
     for (int u = 0; u < U; ++u) sqrt8(t[u], q[u]);
@@ -395,6 +402,8 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
       if constexpr (AS == 2)
         x[u][e] = asinh2_med3(q[u][e], t[u][e]);
       else if constexpr (AS == 1)
+        x[u][e] = asinh2_pick(q[u][e], t[u][e], msel[u][e]);
+      else if constexpr (AS == 3)
         x[u][e] = asinh2_merge(x[u][e], q[u][e], t[u][e], csign);
       else
         x[u][e] = copysignf(t[u][e], x[u][e]);
@@ -549,6 +558,7 @@ template <int DBG, int LM>
 static hipError_t launch_hj_as(int as, const HJArgs& a, hipStream_t st, const DeviceInfo& dev) {
   if (as == 0) return launch_hj<32, 8, 2, LM, 4, DBG, 0>(a, st, dev);
   if (as == 2) return launch_hj<32, 8, 2, LM, 4, DBG, 2>(a, st, dev);
+  if (as == 3) return launch_hj<32, 8, 2, LM, 4, DBG, 3>(a, st, dev);
   return launch_hj<32, 8, 2, LM, 4, DBG, 1>(a, st, dev);
 }
 template <int LM>

@@ -135,9 +135,26 @@ __device__ __forceinline__ float asinh2_merge(float z, float small, float t, uin
   const uint32_t m = (uint32_t)(__builtin_bit_cast(int32_t, t - kAsinhSmallL2) >> 31);
   return __builtin_bit_cast(float, __builtin_amdgcn_bitop3_b32(__builtin_bit_cast(uint32_t, small), ts, m, 0xE4));
 }
+// Mask-first form of the same merge (round 2): the select mask is taken from q, not from t, so it
+// issues while the sqrt / log2 of the tile are in flight and ONE instruction follows the log2:
+//   M = ((bits(q) - bits(1 + 1/64)) >> 31) | 0x80000000    v_sub_u32 + v_ashrrev_i32 + v_or_b32
+//   L = M ? S : t  (bitwise)                                v_bitop3_b32 0xE4
+// q >= 1, so the integer difference is negative exactly when q < 1 + 1/64, i.e. |z| < 1/8 (up to the
+// rounding of q, where both forms are accurate). M's sign bit is always set, so the sign bit comes
+// from S = z * p (p > 0), which is z's sign: the log side needs no separate copysign. NaN q (NaN z)
+// leaves M's low bits clear (+NaN) or set (-NaN) and either way returns a NaN.
+constexpr uint32_t kAsinhSmallQBits = 0x3F820000u;  // 1 + 1/64 = q at |z| = 1/8
+__device__ __forceinline__ uint32_t asinh2_mask(float q, uint32_t csign) {
+  const int32_t d = (int32_t)(__builtin_bit_cast(uint32_t, q) - kAsinhSmallQBits);
+  return (uint32_t)(d >> 31) | csign;
+}
+__device__ __forceinline__ float asinh2_pick(float small, float t, uint32_t M) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_bitop3_b32(__builtin_bit_cast(uint32_t, small),
+                                                               __builtin_bit_cast(uint32_t, t), M, 0xE4));
+}
 // the full fp32 form given q = fma(z, z, 1) and s = sqrt(q): asinh(z)/ln2
 __device__ __forceinline__ float asinh2_f32(float z, float q, float s, uint32_t csign) {
-  return asinh2_merge(z, asinh2_small(z, q), hw_log2(fabsf(z) + s), csign);
+  return asinh2_pick(asinh2_small(z, q), hw_log2(fabsf(z) + s), asinh2_mask(q, csign));
 }
 
 // The same two forms merged by one clamp -- a measured and REJECTED alternative, kept in the
