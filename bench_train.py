@@ -106,6 +106,20 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    res = train_leg(dev, world, rank, D=args.D, N=args.N, nbatches=args.nbatches, pairs=args.pairs, steps=args.steps,
+                    warmup=args.warmup, graph=bool(args.graph), comm_kind=args.comm, history=args.history)
+    if rank == 0:
+        print(json.dumps(res))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps=100, warmup=5, graph=True,
+              comm_kind="enf", history=""):
+    """Config 5 on this process's GPU as one rank of `world` (torch.distributed initialised by the
+    caller when world > 1): returns the result record (the same on every rank; rank 0 prints it).
+    Also run by bench.py after its headline measurement (`train` object of its JSON line)."""
+    import torch
 
     from enf_pkg import load
 
@@ -113,23 +127,22 @@ def main():
     lib = enf._lib
     from euclidiannormalizingflows_jl_amd.train import FlowState, _workspace, householder_batches, trainable_runs  # noqa: E402,E501
 
-    D, N = args.D, args.N
     mk = lambda layers: enf.compose(*[enf.HouseholderTrafo(ps[0]) if op == 5 else enf.JohnsonTrafo(*ps)
                                       for op, ps in reversed(layers)])
     # the data-generating flow's inverse (sinh layers) must stay finite over 4 layers: delta in [3, 5]
-    ltrue = build_flow(D, args.pairs, np.float32, seed=7)
+    ltrue = build_flow(D, pairs, np.float32, seed=7)
     rs = np.random.default_rng(7)
     for op, ps in ltrue:
         if op == 3:
             ps[1] = rs.uniform(3, 5, D).astype(np.float32)
     f_true = mk(ltrue)
-    f0 = mk(build_flow(D, args.pairs, np.float32, seed=42))
+    f0 = mk(build_flow(D, pairs, np.float32, seed=42))
     # every rank holds the whole sample set (columns are read by rank shares of each minibatch)
     g = torch.Generator(device=dev).manual_seed(0x5EED)
     Z = torch.randn((N, D), generator=g, device=dev, dtype=torch.float32).t()
     X = enf.inverse(f_true)(Z)
     del Z
-    plan = enf.minibatch_plan(N, args.nbatches, rank, world)
+    plan = enf.minibatch_plan(N, nbatches, rank, world)
     state = FlowState(f0, D, torch.float32, dev, enf.ADAGrad())
     out = torch.zeros(1 + state.nparams, dtype=torch.float32, device=dev)
     ws = _workspace(state, max(B for B, _, _ in plan))
@@ -144,11 +157,11 @@ def main():
 
     fused = world == 1 and os.environ.get("BENCH_UNFUSED", "0") != "1"
     comm = None
-    if not fused and args.comm == "enf":
+    if not fused and comm_kind == "enf":
         comm = enf.EnfComm.from_process_group() if world > 1 else enf.EnfComm.single()
     runs = np.ascontiguousarray(np.array(segs, dtype=np.int64).reshape(-1))
     hbs = np.ascontiguousarray(np.array(hbatches, dtype=np.int64).reshape(-1))
-    hdev = torch.zeros(args.warmup + args.steps, dtype=torch.float64, device=dev)
+    hdev = torch.zeros(warmup + steps, dtype=torch.float64, device=dev)
 
     def step(i, ev=None, sh=sh):
         B, lo, hi = plan[i % len(plan)]
@@ -180,34 +193,34 @@ def main():
                                         len(hbatches), opt.eta, opt.epsilon, hdev[i:].data_ptr(), sh))
         return hdev[i:i + 1]
 
-    for i in range(args.warmup):
+    for i in range(warmup):
         hist.append(step(i))
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    graph = bool(args.graph) and (fused or comm is not None)
+    graph = graph and (fused or comm is not None)
     if graph:
         # the timed steps as one HIP graph: captured (nothing runs), replayed once untimed (this
-        # advances the optimizer by args.steps more steps), then replayed once timed
+        # advances the optimizer by steps more steps), then replayed once timed
         cg = torch.cuda.CUDAGraph()
         with torch.cuda.graph(cg):
             cs = torch.cuda.current_stream().cuda_stream
-            for i in range(args.steps):
-                step(args.warmup + i, None, cs)
+            for i in range(steps):
+                step(warmup + i, None, cs)
         cg.replay()
         torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     t0 = time.perf_counter()
     if graph:
         evs = evs[:1]
         evs[0][0].record(stream)
         cg.replay()
         evs[0][1].record(stream)
-        hist.append(hdev[args.warmup:args.warmup + args.steps])
+        hist.append(hdev[warmup:warmup + steps])
     else:
-        for i in range(args.steps):
-            hist.append(step(args.warmup + i, evs[i]))
+        for i in range(steps):
+            hist.append(step(warmup + i, evs[i]))
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -215,36 +228,34 @@ def main():
     wall = time.perf_counter() - t0
     grad_ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
     if graph:
-        grad_ms /= args.steps  # the replay's event pair brackets all steps
-    per_rank_ms = gather_ranks(wall / args.steps * 1e3, dev, world, rank)
+        grad_ms /= steps  # the replay's event pair brackets all steps
+    per_rank_ms = gather_ranks(wall / steps * 1e3, dev, world, rank)
     wall, grad_ms_max = max_over_ranks([wall, grad_ms], dev, world)
-    samples = sum(plan[(args.warmup + i) % len(plan)][0] for i in range(args.steps))
+    samples = sum(plan[(warmup + i) % len(plan)][0] for i in range(steps))
     negll = [float(h) for h in torch.cat(hist).cpu()]
-    if args.history and rank == 0:
-        with open(args.history, "w") as f:
+    if history and rank == 0:
+        with open(history, "w") as f:
             json.dump(negll, f)
-    if rank == 0:
-        print(json.dumps({
-            "metric": "optimize_whitening training steps/s (config 5)",
-            "value": args.steps / wall, "unit": "steps/s", "samples_per_s": samples / wall,
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
-            "grad_kernel_ms_median" if not fused else "fused_step_ms_median": grad_ms,
-            "grad_kernel_ms_max_rank" if not fused else "fused_step_ms_max_rank": grad_ms_max, "dtype": "f32",
-            "launch": "HIP graph of the timed steps (torch.cuda.CUDAGraph), replayed" if graph else "eager",
-            "step": "enf_whitening_step (fused, 1 rank)" if fused else
-                    "enf_flow_negll_grad + RCCL sum (" + ("libenf EnfComm" if comm is not None else "torch.distributed")
-                    + ") + enf_whitening_apply",
-            "per_rank_ms_per_step": per_rank_ms,
-            "data": "synthetic: X = f_true^-1(Z), Z ~ N(0,1) (torch Philox 0x5EED), f_true seed 7, init seed 42",
-            "config": {"workload": f"optimize_whitening D={D}, N={N}, nbatches={args.nbatches} "
-                                   f"(B={plan[0][0]}), {args.pairs}x(J∘H), ADAGrad(0.1)",
-                       "per_rank_share": plan[0][2] - plan[0][1], "parallelism": f"dp{world}"},
-            "negll_first": negll[0], "negll_last": negll[-1],
-        }))
+    res = {
+        "metric": "optimize_whitening training steps/s (config 5)",
+        "value": steps / wall, "unit": "steps/s", "samples_per_s": samples / wall,
+        "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": wall / steps * 1e3,
+        "grad_kernel_ms_median" if not fused else "fused_step_ms_median": grad_ms,
+        "grad_kernel_ms_max_rank" if not fused else "fused_step_ms_max_rank": grad_ms_max, "dtype": "f32",
+        "launch": "HIP graph of the timed steps (torch.cuda.CUDAGraph), replayed" if graph else "eager",
+        "step": "enf_whitening_step (fused, 1 rank)" if fused else
+                "enf_flow_negll_grad + RCCL sum (" + ("libenf EnfComm" if comm is not None else "torch.distributed")
+                + ") + enf_whitening_apply",
+        "per_rank_ms_per_step": per_rank_ms,
+        "data": "synthetic: X = f_true^-1(Z), Z ~ N(0,1) (torch Philox 0x5EED), f_true seed 7, init seed 42",
+        "config": {"workload": f"optimize_whitening D={D}, N={N}, nbatches={nbatches} "
+                               f"(B={plan[0][0]}), {pairs}x(J∘H), ADAGrad(0.1)",
+                   "per_rank_share": plan[0][2] - plan[0][1], "parallelism": f"dp{world}"},
+        "negll_first": negll[0], "negll_last": negll[-1],
+    }
     if comm is not None:
         comm.close()
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    return res
 
 
 if __name__ == "__main__":

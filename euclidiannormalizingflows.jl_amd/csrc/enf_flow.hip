@@ -112,6 +112,10 @@ __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
   T* stage = reinterpret_cast<T*>(smem + kLdsScalars) + (threadIdx.x >> 6) * kStagePerWave;
   T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
   (void)ctotp;
+  if constexpr (DBG == 5) {  // diagnostics: nothing (the launch floor of the grid)
+    if (threadIdx.x == 0 && a.N == -1) ((T*)a.Y)[blockIdx.x] = (T)0;
+    return;
+  }
   if constexpr (DBG == 4) {  // diagnostics: the prologue alone
     const double c = build_program<T, D, Frag<T, D>::V>(a, rec, stepc);
     if (threadIdx.x == 0 && c == 1234.5) ((T*)a.Y)[blockIdx.x] = rec[0];
@@ -120,7 +124,7 @@ __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
   InterpBody<T, D, U, LM, OPS> body{a, rec, (T)0, stage};
   // the prologue runs after the wave's first tile loads are issued (frag_stream), so the HBM latency
   // of the first tile overlaps the parameter loads and record construction
-  frag_stream<T, D, U, LM, DBG == 4 ? 0 : DBG>(a, body, [&]() {
+  frag_stream<T, D, U, LM, DBG >= 4 ? 0 : DBG>(a, body, [&]() {
     body.ctot = (T)build_program<T, D, Frag<T, D>::V>(a, rec, stepc);
   });
 }
@@ -362,9 +366,11 @@ static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, cons
 #if ENF_DIAG
   if (a.D == 2) {  // C2 diagnostics: 1 = synthesized tile, 2 = also no stores, 4 = prologue only
     static const int fdbg = ENF_KNOB("ENF_FRAG_DBG", 0);
-    if (fdbg == 1) return launch_frag<T, 2, 4, LADJ, 1, 1>(a, lds, st, dev);
-    if (fdbg == 2) return launch_frag<T, 2, 4, LADJ, 1, 2>(a, lds, st, dev);
-    if (fdbg == 4) return launch_frag<T, 2, 4, LADJ, 1, 4>(a, lds, st, dev);
+    // the product's op set (kOpsHJ, 118 VGPRs); 5 = an empty kernel of the same grid (launch floor)
+    if (fdbg == 1) return launch_frag<T, 2, 4, LADJ, 1, 1, kOpsHJ>(a, lds, st, dev);
+    if (fdbg == 2) return launch_frag<T, 2, 4, LADJ, 1, 2, kOpsHJ>(a, lds, st, dev);
+    if (fdbg == 4) return launch_frag<T, 2, 4, LADJ, 1, 4, kOpsHJ>(a, lds, st, dev);
+    if (fdbg == 5) return launch_frag<T, 2, 4, LADJ, 1, 5, kOpsHJ>(a, lds, st, dev);
   }
 #endif
   if ((flow_ops(a) & ~kOpsHJ) == 0) {  // reflections and Johnson layers only (configs 2-5)
