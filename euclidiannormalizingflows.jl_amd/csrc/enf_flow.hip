@@ -363,6 +363,11 @@ static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, cons
     }
 #endif
   }
+  if constexpr (std::is_same_v<T, double>) {
+    // config 2: the compiled J o H program at D = 2 (ENF_NO_D2=1 in the diagnostics build: the interpreter)
+    static const int no_d2 = ENF_KNOB("ENF_NO_D2", 0);
+    if (!no_d2 && d2_program(a)) return launch_d2_program(a, LADJ, st, dev);
+  }
 #if ENF_DIAG
   if (a.D == 2) {  // C2 diagnostics: 1 = synthesized tile, 2 = also no stores, 4 = prologue only
     static const int fdbg = ENF_KNOB("ENF_FRAG_DBG", 0);

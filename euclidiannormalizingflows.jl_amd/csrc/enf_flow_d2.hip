@@ -1,0 +1,254 @@
+// enf_flow_d2.hip -- compiled program for config 2: JohnsonTrafo ∘ HouseholderTrafo
+// at D = 2 in fp64 (src/johnson_trafo.jl:29-32,39-42; src/householder_trafo.jl:8-11, one reflection),
+// X read once, Y and the per-sample ladj written once (40 algorithmic bytes per sample).
+//
+// Why a kernel of its own: at N = 1e6 the interpreter (flow_frag_kernel) spends ~3 us of its ~15 us in a
+// block prologue (parameter loads, double log / sqrt / division, the LDS log table, a block barrier)
+// that no wave can overlap, and walks its step table per tile (profiles/r02_c2_*: launch floor 2.3 us,
+// prologue 5.4, compute-only 12.4, full 14.9). Here every wave builds what it needs itself, with no
+// block barrier, while its first tile's loads are in flight:
+//  * the parameters are wave-uniform: rows 0 and 1 are computed by lanes 0 and 1 (v_d^2 and
+//    log|delta_d| - log|lambda_d|, summed by one lane swap, then sqrt(2/v'v), v_d sqrt(2/v'v), 1/lambda_d)
+//    and read back into scalar registers; gamma, delta, xi arrive by scalar loads;
+//  * the 33-entry fp64 log table (enf_logtab.h, used by asinh64_tab / logprod64_tab) is copied into
+//    the wave's own LDS slice by lanes 0..32 (one wave barrier, no block barrier);
+//  * a lane owns whole columns (one 16-byte fragment = one column), U = 2 columns per tile at a stride
+//    of 64, so every load / store instruction moves 1 KiB of contiguous HBM and the ladj store 512 B.
+// The arithmetic is the interpreter's, operation for operation (enf_steps.h step_householder /
+// step_johnson fp64 and build_program's constants, same ocml functions in the prologue), so the
+// results are bit-identical to it: dot = vh0 x0 + vh1 x1 (fma), x' = fma(-dot, vh, x),
+// z = (x' - xi) * (1/lambda), y = fma(delta, asinh64_tab(z), gamma), q = fma(z, z, 1),
+// ladj = fma(1, -log(q0 q1)/2, ctot) (+ the old ladj when accumulating).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+
+#include "enf_frag.h"
+#include "enf_internal.h"
+#include "enf_logtab.h"
+#include "enf_math64.h"
+
+namespace enf {
+
+struct D2Args {
+  const double* X;
+  double* Y;
+  double* ladj;
+  int64_t N;
+  const double* v;    // reflection vector (column of V)
+  const double* g;    // Johnson gamma, delta, xi, lambda
+  const double* d;
+  const double* xi;
+  const double* lam;
+};
+
+constexpr int kD2Tab = 3 * kLogTabN;  // doubles of one wave's table copy
+
+__device__ __forceinline__ double d2_readlane(double v, int l) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// DBG (diagnostics build only): 1 = synthesize the tile instead of loading it, 2 = also skip the stores
+template <int U, bool TAIL, int DBG>
+__device__ __forceinline__ void d2_load(const D2Args& a, int64_t col0, int lane, double (&x)[U][2]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t c = col0 + (int64_t)u * 64 + lane;
+    if (DBG >= 1) {
+      x[u][0] = (double)(lane + 3 * u) * 0.03125 - 1.0;
+      x[u][1] = (double)(lane - 5 * u) * 0.0625 + 0.5;
+    } else if (!TAIL) {
+      const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.X + 2 * c));
+      __builtin_memcpy(&x[u][0], &v4, 16);
+    } else {
+      x[u][0] = c < a.N ? a.X[2 * c] : 0.0;
+      x[u][1] = c < a.N ? a.X[2 * c + 1] : 0.0;
+    }
+  }
+}
+
+struct D2Prog {
+  double vh0, vh1, g0, g1, d0, d1, xi0, xi1, il0, il1, ctot;
+};
+
+template <int U, int LM, bool TAIL, int DBG>
+__device__ __forceinline__ void d2_tile(const D2Args& a, const D2Prog& P, const double* __restrict__ tab, int64_t col0,
+                                        int lane, double (&x)[U][2]) {
+  double old[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t c = col0 + (int64_t)u * 64 + lane;
+    old[u] = (LM == 2 && (!TAIL || c < a.N)) ? a.ladj[c] : 0.0;
+  }
+  double lad[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    // HouseholderTrafo: x - vh (vh'x)
+    double dot = P.vh0 * x[u][0];
+    dot = fma(P.vh1, x[u][1], dot);
+    const double x0 = fma(-dot, P.vh0, x[u][0]);
+    const double x1 = fma(-dot, P.vh1, x[u][1]);
+    // JohnsonTrafo
+    const double z0 = (x0 - P.xi0) * P.il0;
+    const double z1 = (x1 - P.xi1) * P.il1;
+    x[u][0] = fma(P.d0, asinh64_tab(z0, tab), P.g0);
+    x[u][1] = fma(P.d1, asinh64_tab(z1, tab), P.g1);
+    if (LM > 0) {
+      const double q[2] = {fma(z0, z0, 1.0), fma(z1, z1, 1.0)};
+      lad[u] = 0.0 - 0.5 * logprod64_tab<2>(q, tab);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t c = col0 + (int64_t)u * 64 + lane;
+    if (DBG == 2) {
+      if (x[u][0] == 1234.5) a.Y[2 * c] = x[u][1];  // keeps the compute alive, never true in practice
+    } else if (!TAIL) {
+      u32x4 v4;
+      __builtin_memcpy(&v4, &x[u][0], 16);
+      __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(a.Y + 2 * c));
+    } else if (c < a.N) {
+      a.Y[2 * c] = x[u][0];
+      a.Y[2 * c + 1] = x[u][1];
+    }
+    if (LM > 0 && DBG != 2) {
+      const double v = fma(1.0, lad[u], P.ctot) + old[u];
+      if (!TAIL || c < a.N) a.ladj[c] = v;
+    }
+  }
+}
+
+template <int U, int LM, int DBG>
+__global__ __launch_bounds__(256, U == 1 ? 8 : 4) void flow_d2_kernel(D2Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  double* tab = reinterpret_cast<double*>(smem) + wave * kD2Tab;
+  constexpr int64_t CT = 64 * U;
+  const int64_t ntiles_full = a.N / CT;
+  const int64_t wave_id = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  double xa[U][2], xb[U][2];
+  // the first tile's loads go out before the prologue, which then overlaps their latency
+  const bool full0 = wave_id < ntiles_full;
+  if (full0) d2_load<U, false, DBG>(a, wave_id * CT, lane, xa);
+  // the wave's copy of the log table
+  if (lane < kLogTabN) {
+    tab[3 * lane] = kLogTab[3 * lane];
+    tab[3 * lane + 1] = kLogTab[3 * lane + 1];
+    tab[3 * lane + 2] = kLogTab[3 * lane + 2];
+  }
+  // parameters (build_program / param_values in enf_steps.h, same operations and ocml functions, so the
+  // same values). A VALU instruction costs the whole wave whatever its active lanes, so the four logs and
+  // the three divisions run as one log and one division over lanes: lanes 0, 1 take log|delta_d| and
+  // 1/lambda_d, lanes 2, 3 log|lambda_{d-2}|, lane 2 also 2/v'v.
+  double vr = lane < 2 ? a.v[lane] : 0.0;
+  double pv = vr * vr;
+  pv += __shfl_xor(pv, 1);  // lanes 0, 1: v0^2 + v1^2 (build_program's one butterfly stage)
+  const double lg = log(fabs(lane < 2 ? a.d[lane & 1] : a.lam[lane & 1]));  // lanes 0..3
+  const double pvb = __shfl(pv, 0);
+  const double qt = (lane < 2 ? 1.0 : 2.0) / (lane < 2 ? a.lam[lane & 1] : pvb);  // 1/lambda_d; lane 2: 2/v'v
+  double pc = lg - __shfl_down(lg, 2);  // lanes 0, 1: log|delta_d| - log|lambda_d|
+  pc += __shfl_xor(pc, 1);
+  const double hscale = sqrt(d2_readlane(qt, 2));
+  const double vh = vr * hscale;
+  D2Prog P;
+  P.vh0 = d2_readlane(vh, 0);
+  P.vh1 = d2_readlane(vh, 1);
+  P.il0 = d2_readlane(qt, 0);
+  P.il1 = d2_readlane(qt, 1);
+  P.ctot = (0.0 + 0.0) + d2_readlane(pc, 0);  // the step constants summed in step order (H: 0)
+  P.g0 = a.g[0];
+  P.g1 = a.g[1];
+  P.d0 = a.d[0];
+  P.d1 = a.d[1];
+  P.xi0 = a.xi[0];
+  P.xi1 = a.xi[1];
+  // the table writes are complete before any lane of this wave reads it (LDS is in order per wave)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  // persistent loop with the next tile's loads in flight (as frag_stream)
+  if (full0) {
+    int64_t t = wave_id, t1 = t + nwaves;
+    d2_load<U, false, DBG>(a, (t1 < ntiles_full ? t1 : t) * CT, lane, xb);
+    d2_tile<U, LM, false, DBG>(a, P, tab, t * CT, lane, xa);
+    while (t1 < ntiles_full) {
+      const int64_t t2 = t1 + nwaves;
+      d2_load<U, false, DBG>(a, (t2 < ntiles_full ? t2 : t1) * CT, lane, xa);
+      d2_tile<U, LM, false, DBG>(a, P, tab, t1 * CT, lane, xb);
+      if (t2 >= ntiles_full) break;
+      const int64_t t3 = t2 + nwaves;
+      d2_load<U, false, DBG>(a, (t3 < ntiles_full ? t3 : t2) * CT, lane, xb);
+      d2_tile<U, LM, false, DBG>(a, P, tab, t2 * CT, lane, xa);
+      t1 = t3;
+    }
+  }
+  if (ntiles_full * CT < a.N && wave_id == ntiles_full % nwaves) {
+    const int64_t c0 = ntiles_full * CT;
+    d2_load<U, true, 0>(a, c0, lane, xa);
+    d2_tile<U, LM, true, 0>(a, P, tab, c0, lane, xa);
+  }
+}
+
+// Eligible: fp64, D = 2, fragment layout (contiguous, 16-byte aligned columns), exactly one single-column
+// reflection followed by one Johnson layer.
+bool d2_program(const FlowArgs& a) {
+  return a.frag && a.D == 2 && a.nsteps == 2 && a.steps[0].op == OP_HOUSEHOLDER && a.steps[1].op == OP_JOHNSON;
+}
+
+template <int U, int LM, int DBG>
+static hipError_t launch_d2_u(const D2Args& h, hipStream_t st, const DeviceInfo& dev) {
+  const size_t lds = 4 * kD2Tab * sizeof(double);
+  const void* k = reinterpret_cast<const void*>(&flow_d2_kernel<U, LM, DBG>);
+  int64_t blocks = 0;
+  hipError_t e = frag_grid(k, h.N, (int64_t)64 * U * 4, lds, dev, &blocks);
+  if (e != hipSuccess) return e;
+  // two blocks per CU (2 waves per SIMD, ~4 tiles per wave at N = 1e6): every wave pays the prologue,
+  // so fewer, longer waves beat full occupancy (11.2 vs 11.9 us; 1 block per CU: 12.6 us,
+  // profiles/r02_c2_d2_ab.txt; ENF_BLOCKS_PER_CU overrides in the diagnostics build)
+  static const int bpc_env = ENF_KNOB("ENF_BLOCKS_PER_CU", 0);
+  const int64_t cap = (int64_t)dev.num_cu * 2;
+  if (bpc_env == 0 && blocks > cap) blocks = cap;
+  hipLaunchKernelGGL((flow_d2_kernel<U, LM, DBG>), dim3((unsigned)blocks), dim3(256), lds, st, h);
+  return hipGetLastError();
+}
+
+template <int LM>
+static hipError_t launch_d2_lm(const D2Args& h, hipStream_t st, const DeviceInfo& dev) {
+#if ENF_DIAG
+  // ENF_D2_U: columns per lane per tile (2 default; 1: 49 VGPRs, 8 waves per SIMD); ENF_D2_DBG 1 / 2:
+  // synthesized tile / also no stores
+  static const int u = ENF_KNOB("ENF_D2_U", 2);
+  static const int dbg = ENF_KNOB("ENF_D2_DBG", 0);
+  if (dbg == 1) return launch_d2_u<2, LM, 1>(h, st, dev);
+  if (dbg == 2) return launch_d2_u<2, LM, 2>(h, st, dev);
+  if (u == 1) return launch_d2_u<1, LM, 0>(h, st, dev);
+#endif
+  // U = 2: 103 VGPRs (4 waves per SIMD); U = 4 interleaves 8 asinh chains and spills at 128 VGPRs
+  return launch_d2_u<2, LM, 0>(h, st, dev);
+}
+
+hipError_t launch_d2_program(const FlowArgs& a, int lm, hipStream_t st, const DeviceInfo& dev) {
+  D2Args h;
+  std::memset(&h, 0, sizeof h);
+  h.X = (const double*)a.X;
+  h.Y = (double*)a.Y;
+  h.ladj = (double*)a.ladj;
+  h.N = a.N;
+  const Step& sh = a.steps[0];
+  const LayerDesc& J = a.layers[a.steps[1].layer];
+  h.v = (const double*)a.layers[sh.layer].p[0] + (int64_t)sh.col * 2;
+  h.g = (const double*)J.p[0];
+  h.d = (const double*)J.p[1];
+  h.xi = (const double*)J.p[2];
+  h.lam = (const double*)J.p[3];
+  if (lm == 0) return launch_d2_lm<0>(h, st, dev);
+  if (lm == 1) return launch_d2_lm<1>(h, st, dev);
+  return launch_d2_lm<2>(h, st, dev);
+}
+
+}  // namespace enf
