@@ -54,6 +54,7 @@ template <int D, int KU, bool TAIL>
 __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int lane, const float* __restrict__ rec,
                                           float* __restrict__ zst, float* __restrict__ dst, float* __restrict__ acc,
                                           double& lossp, int& nvalid, float ctot) {
+  const uint32_t csign = sign_mask_vgpr();  // asinh2_f32: the accurate fp32 asinh (enf_frag.h)
   using L = GL<D, KU>;
   constexpr int V = 4, G = L::G, S = L::S;
   const int grp = lane % G;
@@ -106,7 +107,7 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
     for (int u = 0; u < KU; ++u) {
 #pragma unroll
       for (int e = 0; e < V; ++e) {
-        const float Lz = copysignf(hw_log2(fabsf(z[u][e]) + hw_sqrt(q[u][e])), z[u][e]);
+        const float Lz = asinh2_f32(z[u][e], q[u][e], hw_sqrt(q[u][e]), csign);
         x[u][e] = fmaf(dl2[e], Lz, gam[e]);
       }
       lad[u] = fmaf(-0.5f, hw_log2((q[u][0] * q[u][1]) * (q[u][2] * q[u][3])), lad[u]);
@@ -151,7 +152,7 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
         const float q = fmaf(z[e], z[e], 1.f);
         const float s = hw_sqrt(q);
         const float rs = hw_rcp(s);
-        const float Lz = copysignf(hw_log2(fabsf(z[e]) + s), z[e]);
+        const float Lz = asinh2_f32(z[e], q, s, csign);
         aG[e] += g[u][e];
         aD[e] = fmaf(g[u][e], Lz, aD[e]);
         const float dz = fmaf(g[u][e] * del[e], rs, z[e] * (rs * rs) * vm[u]);
@@ -330,6 +331,7 @@ template <int D, int KU, int NP, bool TAIL>
 __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0, int lane, const float* __restrict__ rec,
                                               const float (&xin)[KU][4], float (&acc)[NP][5][4], double& lossp,
                                               int& nvalid, float ctot) {
+  const uint32_t csign = sign_mask_vgpr();  // asinh2_f32: the accurate fp32 asinh (enf_frag.h)
   using L = GL<D, KU>;
   constexpr int V = 4, G = L::G, S = L::S;
   const int grp = lane % G;
@@ -368,7 +370,7 @@ __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0,
         zs[p][u][e] = fmaf(fmaf(-ds[p][u], vh[e], x[u][e]), il[e], nxil[e]);
         q[e] = fmaf(zs[p][u][e], zs[p][u][e], 1.f);
         ss[p][u][e] = hw_sqrt(q[e]);
-        ls[p][u][e] = copysignf(hw_log2(fabsf(zs[p][u][e]) + ss[p][u][e]), zs[p][u][e]);
+        ls[p][u][e] = asinh2_f32(zs[p][u][e], q[e], ss[p][u][e], csign);
         x[u][e] = fmaf(dl2[e], ls[p][u][e], gam[e]);
       }
       lad[u] = fmaf(-0.5f, hw_log2((q[0] * q[1]) * (q[2] * q[3])), lad[u]);
