@@ -83,6 +83,8 @@ def main():
     ap.add_argument("--graph", type=int, default=1,
                     help="capture the timed steps (incl. the RCCL all-reduce at world > 1) once into a HIP graph "
                          "and replay it (0: eager launches)")
+    ap.add_argument("--diag", action="store_true",
+                    help="tools only: run on the diagnostics library (libenf_diag.so, ENF_* knobs) instead of libenf.so")
     ap.add_argument("--comm", default="enf", choices=["enf", "torch"],
                     help="world > 1: RCCL through libenf on the kernels' stream (enf; graph-capturable) or "
                          "torch.distributed.all_reduce (torch; eager only)")
@@ -106,6 +108,10 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    if args.diag:
+        from enf_pkg import load
+
+        load()._lib.use_diagnostics_library()
     res = train_leg(dev, world, rank, D=args.D, N=args.N, nbatches=args.nbatches, pairs=args.pairs, steps=args.steps,
                     warmup=args.warmup, graph=bool(args.graph), comm_kind=args.comm, history=args.history)
     if rank == 0:
