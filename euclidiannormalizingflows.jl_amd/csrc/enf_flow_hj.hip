@@ -101,7 +101,9 @@ enum : int { HJ_DP = 0, HJ_GP = 1, HJ_VH = 2, HJ_IL = 3, HJ_NXI = 4, HJ_RR = 5 }
 __host__ __device__ constexpr bool hj_rotated(int q) { return q == HJ_DP || q == HJ_VH || q == HJ_IL || q == HJ_RR; }
 
 // DBG (diagnostic builds, ENF_DEBUG_MODE): 1 = synthesize the tile instead of loading it, 2 = also
-// skip the stores (compute-only timing).
+// skip the stores (compute-only timing); cache policy A/B: 8 = nontemporal loads, 9 = plain stores.
+// The product loads X with plain loads (0.800 / 0.798 vs 0.808 / 0.805 ms with nontemporal loads,
+// profiles/r02_cache_policy_ab.jsonl) and writes Y with nontemporal stores (plain: 0.810 / 0.822).
 template <int D, int R, int U, bool TAIL, int DBG>
 __device__ __forceinline__ void hj_load(const HJArgs& a, int64_t col0, float (&x)[U][R]) {
   using L = HJLay<D, R, U>;
@@ -113,11 +115,12 @@ __device__ __forceinline__ void hj_load(const HJArgs& a, int64_t col0, float (&x
 #pragma unroll
     for (int h = 0; h < L::NF; ++h) {
       const int64_t off = c * D + L::row(h, lane);
-      if (DBG >= 1) {
+      if (DBG == 1 || DBG == 2) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) x[u][4 * h + e] = (float)(lane + 3 * u + 5 * h + e) * 0.03125f - 1.f;
       } else if (!TAIL) {
-        const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X + off));
+        const u32x4 v4 = DBG == 8 ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X + off))
+                                  : *reinterpret_cast<const u32x4*>(X + off);
         __builtin_memcpy(&x[u][4 * h], &v4, 16);
       } else {
 #pragma unroll
@@ -159,7 +162,8 @@ __device__ __forceinline__ void hj_store(const HJArgs& a, float ctot, int64_t co
       } else if (!TAIL) {
         u32x4 v4;
         __builtin_memcpy(&v4, &x[u][4 * h], 16);
-        __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(Y + off));
+        if (DBG == 9) *reinterpret_cast<u32x4*>(Y + off) = v4;
+        else __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(Y + off));
       } else if (c < a.N) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) Y[off + e] = x[u][4 * h + e];
@@ -570,6 +574,8 @@ static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, c
       static const int as = ENF_KNOB("ENF_HJ_ASINH", 1);
       if (dbg == 1) return launch_hj_as<1, 1>(as, a, st, dev);
       if (dbg == 2) return launch_hj_as<2, 1>(as, a, st, dev);
+      if (dbg == 8) return launch_hj_as<8, 1>(as, a, st, dev);
+      if (dbg == 9) return launch_hj_as<9, 1>(as, a, st, dev);
       return launch_hj_as<0, 1>(as, a, st, dev);
     }
 #endif
