@@ -4,9 +4,7 @@
 // (src/johnson_trafo.jl:29-32, ladj :39-42 / :76-80), fp32, D in {32, 64}, fused in one launch:
 // X is read once, Y and the per-sample ladj are written once.
 //
-// Per pair p (the register tile holds L_{p-1} = asinh(z_{p-1})/ln2 on entry, X itself for p = 0):
-//   y   = gamma_{p-1} + delta'_{p-1} L_{p-1}        the previous Johnson output (p = 0: y = X, i.e.
-//                                                    delta' = 1, gamma = 0), delta' = delta*ln2
+// Per pair p (the register tile holds y, the previous Johnson output, on entry -- X itself for p = 0):
 //   dot = vh'y,  vh = v sqrt(2/v'v)                 householder_trafo! (householder_trafo.jl:8-11)
 //   z   = y/lambda - xi/lambda - dot vh/lambda      (y - vh dot - xi)/lambda (johnson_trafo.jl:30)
 //   L_p = asinh(z)/ln2                              asinh2 (enf_frag.h): log2(|z| + sqrt(q)),
@@ -14,15 +12,18 @@
 //   ladj += log|delta/lambda| - log(q)/2            johnson_trafo.jl:41; the constant part once per
 //                                                    column (ctot), -1/2 log2 of the product of the q
 //                                                    of a lane's 8 rows of one column
-// and the output y_n = gamma_n + delta'_n L_n. y is formed explicitly, as the reference rounds it,
-// before the reflection: folding gamma and delta' into the next pair's constants (round 1) saves one
+//   y   = gamma_p + delta'_p L_p                    at the end of the pair, delta' = delta*ln2
+// so the last pair leaves the output in the tile. y is formed explicitly, as the reference rounds it,
+// before the next reflection: folding gamma and delta' into the next pair's constants (round 1) saves one
 // FMA per element but adds terms that the reference has already cancelled, and gave up to 16x the
 // reference's error on elements where y cancels (tests/test_gpu_fp32_accuracy.py per-element test).
-// Per element and pair: 4 FMAs (y, dot, 2 for z), q, sqrt, |z| + s, log2, the small-|z| polynomial
+// Per element and pair: 4 FMAs (dot, 2 for z, y), q, sqrt, |z| + s, log2, the small-|z| polynomial
 // (3) and its branch-free merge (4 full-rate ops), 7/8 multiply for the ladj product.
 //
 // Parameter records (LDS, built in double in each block's prologue): per pair and row
-// {delta', gamma, vh, 1/lambda, -xi/lambda, vh/lambda}; record n holds {delta'_n, gamma_n}.
+// {delta', gamma, vh, 1/lambda, -xi/lambda, vh/lambda}; record p's {delta', gamma} slots hold pair p-1's
+// (read at the end of pair p-1, which applies them; record 0's {1, 0} is not used), record n holds
+// {delta'_n, gamma_n}.
 //
 // Fast-path guard: the product of 8 q stays finite unless |z| is large (about 2^8 on every row),
 // infinite or NaN; then the lanes of that column redo the whole program from X with the exact-range
@@ -321,13 +322,9 @@ __device__ __forceinline__ float prod_tree(const float (&q)[R]) {
   }
 }
 
-// y = gamma' + delta' L, the dot and z of one pair, in place on the tile (x: L on entry, z on exit).
+// The dot and z of one pair, in place on the tile (x: the pair's input y on entry, z on exit).
 template <int D, int R, int U>
 __device__ __forceinline__ void hj_pair_z(float (&x)[U][R], const float* r, HJParams<R>& prm) {
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_DP, e), prm.m(HJ_GP, e));
   prm.template load<HJ_IL, kHjW>(r);
   float dot[U];
   hj_dots<D, R, U>(x, prm, dot);
@@ -414,6 +411,11 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
     }
   r += kHjW * D;
   prm.template load<0, HJ_IL>(r);
+  // y_p = gamma_p + delta'_p L_p: the next record's {delta', gamma} slots (record n: the output's)
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_DP, e), prm.m(HJ_GP, e));
   float m = pr[0];
 #pragma unroll
   for (int u = 1; u < U; ++u) m = fmaxf(m, pr[u]);
@@ -438,6 +440,10 @@ __device__ __forceinline__ void hj_pair_exact(float (&x)[U][R], float (&acc)[U],
     }
   r += kHjW * D;
   prm.template load<0, HJ_IL>(r);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_DP, e), prm.m(HJ_GP, e));
 }
 
 template <int D, int R, int U, int LM, int AS = 1>
@@ -471,11 +477,7 @@ struct HJBody {
       prm.template load<0, HJ_IL>(r);
       for (int p = 0; p < n; ++p) hj_pair_exact<D, R, U, LADJ, AS>(x, acc, r, prm);
     }
-    // y_n = gamma_n + delta'_n L_n (record n)
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_DP, e), prm.m(HJ_GP, e));
+    // (y_n = gamma_n + delta'_n L_n was formed at the end of the last pair)
     hj_store<D, R, U, LM, TAIL, DBG>(a, ctot, col0, x, acc, old, stage);
   }
 };
