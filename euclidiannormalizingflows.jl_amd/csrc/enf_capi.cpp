@@ -630,7 +630,11 @@ enf_status enf_comm_init(enf_comm* comm, int32_t nranks, const uint8_t id[ENF_UN
 enf_status enf_comm_destroy(enf_comm comm) {
   ENF_TRY
   if (!comm) return ENF_OK;
-  ncclResult_t r = ncclCommDestroy(comm->comm);
+  // the documented teardown: ncclCommFinalize flushes every collective issued on the communicator
+  // (blocking communicator), then ncclCommDestroy frees its local resources
+  ncclResult_t r = ncclCommFinalize(comm->comm);
+  const ncclResult_t rd = ncclCommDestroy(comm->comm);
+  if (r == ncclSuccess) r = rd;
   delete comm;
   if (r != ncclSuccess) return fail(ENF_ERR_RCCL, std::string("ncclCommDestroy: ") + ncclGetErrorString(r));
   return ENF_OK;

@@ -168,6 +168,7 @@ def test_grad_rccl_single_rank_allreduce(enf, gpu):
     torch.cuda.synchronize()
     assert torch.equal(buf.cpu(), torch.arange(10, dtype=torch.float32))
     assert L.enf_comm_destroy(comm) == 0
+    torch.cuda.synchronize()  # a fault in the teardown is reported here, not by the next test
 
 
 @pytest.mark.parametrize("D,pairs", [(32, 1), (32, 3), (32, 4), (32, 8), (64, 1), (64, 4)])
