@@ -213,9 +213,20 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
   // flatten into steps: one per transform, one per Householder reflection column
   // (dense-Householder path: a chained HouseholderTrafo with k >= wy_min_k() reflections becomes
   // OP_DENSE steps of <= D reflections each, col = first column | count << 16)
-  const bool frag = enf::frag_path(D, ldx, ldy, X, Y, elem) && enf::frag_path(D, ldy, ldy, Y, Y, elem);
+  bool frag = enf::frag_path(D, ldx, ldy, X, Y, elem) && enf::frag_path(D, ldy, ldy, Y, Y, elem);
+  // padded fragment path: D a multiple of 16/elem but not a power of two, laid out as the next power
+  // of two (enf_internal.h frag_pad_dim) when every layer maps 0 to 0 with neutral parameters
+  int64_t dk = 0;
+  if (!frag) {
+    dk = enf::frag_pad_dim(D, ldx, ldy, X, Y, elem);
+    for (int32_t l = 0; l < nlayers && dk; ++l) {
+      const int op = layers[l].op;
+      if (op != ENF_OP_HOUSEHOLDER && op != ENF_OP_JOHNSON && op != ENF_OP_JOHNSON_INV && op != ENF_OP_SCALESHIFT) dk = 0;
+    }
+    frag = dk != 0;
+  }
   bool wy = false;
-  if (enf::wy_supported(D, frag))
+  if (!dk && enf::wy_supported(D, frag))
     for (int32_t l = 0; l < nlayers; ++l)
       if (layers[l].op == ENF_OP_HOUSEHOLDER && layers[l].k >= enf::wy_min_k()) wy = true;
   struct S { int32_t op, layer, col; };
@@ -242,12 +253,13 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
     a.D = (int32_t)D;
     a.N = N;
     a.frag = frag ? 1 : 0;
+    a.dk = (int32_t)dk;
     a.wy = wy ? 1 : 0;
     size_t recs = 0;
     int last_layer = -1;
     while (i < steps.size() && a.nsteps < enf::kMaxSteps) {
       const S& s = steps[i];
-      const size_t w = enf::record_elems(s.op, D, elem, frag) * elem;
+      const size_t w = enf::record_elems(s.op, dk ? dk : D, elem, frag) * elem;
       const bool new_layer = s.layer != last_layer;
       if (new_layer && a.nlayers >= enf::kMaxLayers) break;
       if (recs + w > (wy ? enf::kLdsParamBudgetWY : enf::kLdsParamBudget)) {

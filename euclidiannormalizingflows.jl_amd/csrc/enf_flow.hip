@@ -46,7 +46,7 @@ constexpr int kOpsAll = 0x3F;
 constexpr int kOpsHJ = (1 << OP_HOUSEHOLDER) | (1 << OP_JOHNSON);
 
 // Interpreter: runs the step table of the kernel arguments on one register tile, then stores it.
-template <typename T, int D, int U, int LM, bool TAIL, int DBG, int OPS = kOpsAll>
+template <typename T, int D, int U, int LM, bool TAIL, int DBG, int OPS = kOpsAll, bool PAD = false>
 __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict__ rec, T ctot,
                                           int64_t col0, Tile<T, D, U>& x,
                                           const T (&old)[LadjOut<T, D, U>::NLS][LadjOut<T, D, U>::W],
@@ -87,10 +87,10 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& a, const T* __restrict
       if constexpr ((OPS >> OP_CENTER_CONTRACT) & 1) step_center_contract<T, D, U, LADJ>(x, acc, r);
     }
   }
-  store_tile<T, D, U, LM, TAIL, DBG>(a, ctot, col0, x, acc, old, stage);
+  store_tile<T, D, U, LM, TAIL, DBG, PAD>(a, ctot, col0, x, acc, old, stage);
 }
 
-template <typename T, int D, int U, int LM, int OPS = kOpsAll>
+template <typename T, int D, int U, int LM, int OPS = kOpsAll, bool PAD = false>
 struct InterpBody {
   const FlowArgs& a;
   const T* rec;
@@ -99,12 +99,13 @@ struct InterpBody {
   template <bool TAIL, int DBG>
   __device__ __forceinline__ void tile(int64_t col0, Tile<T, D, U>& x,
                                        const T (&old)[LadjOut<T, D, U>::NLS][LadjOut<T, D, U>::W]) {
-    flow_tile<T, D, U, LM, TAIL, DBG, OPS>(a, rec, ctot, col0, x, old, stage);
+    flow_tile<T, D, U, LM, TAIL, DBG, OPS, PAD>(a, rec, ctot, col0, x, old, stage);
   }
 };
 
-// OCC: minimum waves per SIMD the register allocation must allow (launch-bounds occupancy hint)
-template <typename T, int D, int U, int LM, int OCC, int DBG = 0, int OPS = kOpsAll>
+// OCC: minimum waves per SIMD the register allocation must allow (launch-bounds occupancy hint).
+// PAD: the padded fragment path (a.dk = D > a.D, enf_internal.h frag_pad_dim).
+template <typename T, int D, int U, int LM, int OCC, int DBG = 0, int OPS = kOpsAll, bool PAD = false>
 __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* stepc = reinterpret_cast<double*>(smem);
@@ -121,10 +122,10 @@ __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
     if (threadIdx.x == 0 && c == 1234.5) ((T*)a.Y)[blockIdx.x] = rec[0];
     return;
   }
-  InterpBody<T, D, U, LM, OPS> body{a, rec, (T)0, stage};
+  InterpBody<T, D, U, LM, OPS, PAD> body{a, rec, (T)0, stage};
   // the prologue runs after the wave's first tile loads are issued (frag_stream), so the HBM latency
   // of the first tile overlaps the parameter loads and record construction
-  frag_stream<T, D, U, LM, DBG >= 4 ? 0 : DBG>(a, body, [&]() {
+  frag_stream<T, D, U, LM, DBG >= 4 ? 0 : DBG, PAD>(a, body, [&]() {
     body.ctot = (T)build_program<T, D, Frag<T, D>::V>(a, rec, stepc);
   });
 }
@@ -295,7 +296,7 @@ __global__ __launch_bounds__(256) void flow_lds_kernel(FlowArgs a, int ct, int d
 size_t program_lds_bytes(const FlowArgs& a, size_t elem) {
   const bool frag = frag_supported(a, elem);
   size_t n = 0;
-  for (int s = 0; s < a.nsteps; ++s) n += record_elems(a.steps[s].op, a.D, elem, frag);
+  for (int s = 0; s < a.nsteps; ++s) n += record_elems(a.steps[s].op, a.dk ? a.dk : a.D, elem, frag);
   return kLdsHeader + n * elem;
 }
 
@@ -325,15 +326,39 @@ hipError_t frag_grid(const void* kernel, int64_t N, int64_t cols_per_block, size
   return hipSuccess;
 }
 
-template <typename T, int D, int U, int LM, int OCC = 1, int DBG = 0, int OPS = kOpsAll>
+template <typename T, int D, int U, int LM, int OCC = 1, int DBG = 0, int OPS = kOpsAll, bool PAD = false>
 static hipError_t launch_frag(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
   using F = Frag<T, D>;
-  const void* k = reinterpret_cast<const void*>(&flow_frag_kernel<T, D, U, LM, OCC, DBG, OPS>);
+  const void* k = reinterpret_cast<const void*>(&flow_frag_kernel<T, D, U, LM, OCC, DBG, OPS, PAD>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, a.N, (int64_t)F::COLS_PER_INSTR * U * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_frag_kernel<T, D, U, LM, OCC, DBG, OPS>), dim3((unsigned)blocks), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((flow_frag_kernel<T, D, U, LM, OCC, DBG, OPS, PAD>), dim3((unsigned)blocks), dim3(256), lds, st,
+                     a);
   return hipGetLastError();
+}
+
+// The padded fragment path (a.dk = the power-of-two layout of a.D rows): reflections, Johnson layers
+// and ScaleShift only (the ops whose neutral parameters map 0 to 0 with ladj 0, enf_steps.h).
+constexpr int kOpsPad = (1 << OP_HOUSEHOLDER) | (1 << OP_JOHNSON) | (1 << OP_JOHNSON_INV) | (1 << OP_SCALESHIFT);
+template <typename T, int LADJ>
+static hipError_t dispatch_pad(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
+  switch (a.dk) {
+    case 8: return launch_frag<T, 8, 4, LADJ, 1, 0, kOpsPad, true>(a, lds, st, dev);
+    case 16: return launch_frag<T, 16, 4, LADJ, 1, 0, kOpsPad, true>(a, lds, st, dev);
+    case 32: return launch_frag<T, 32, 4, LADJ, 1, 0, kOpsPad, true>(a, lds, st, dev);
+    case 64:
+      if constexpr (std::is_same_v<T, float>) return launch_frag<T, 64, 4, LADJ, 1, 0, kOpsPad, true>(a, lds, st, dev);
+      else return launch_frag<T, 64, 2, LADJ, 1, 0, kOpsPad, true>(a, lds, st, dev);
+    case 128:
+      if constexpr (std::is_same_v<T, float>) return launch_frag<T, 128, 4, LADJ, 1, 0, kOpsPad, true>(a, lds, st, dev);
+      else return launch_frag<T, 128, 2, LADJ, 1, 0, kOpsPad, true>(a, lds, st, dev);
+    case 256:
+      if constexpr (std::is_same_v<T, float>) return launch_frag<T, 256, 4, LADJ, 1, 0, kOpsPad, true>(a, lds, st, dev);
+      break;
+    default: break;
+  }
+  return hipErrorInvalidValue;
 }
 
 // the op set of a flow (bit op per step)
@@ -345,6 +370,7 @@ static int flow_ops(const FlowArgs& a) {
 
 template <typename T, int LADJ>
 static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
+  if (a.dk) return dispatch_pad<T, LADJ>(a, lds, st, dev);
   if constexpr (std::is_same_v<T, float>) {
     static const int nospec = ENF_KNOB("ENF_NO_SPECIALIZE", 0);
     static const int dbg = ENF_KNOB("ENF_DEBUG_MODE", 0);

@@ -222,26 +222,35 @@ __device__ __forceinline__ int64_t frag_col(int64_t col0, int u, int lane) {
 // One wave tile = U fully coalesced 1-KiB wave-instructions (ldx == D, 16-B aligned).
 // DBG (diagnostic builds only, ENF_DEBUG_MODE): 1 = synthesize the tile instead of loading it,
 // 2 = also skip the stores (compute-only timing).
-template <typename T, int D, int U, bool TAIL, int DBG = 0>
+// PAD (padded fragment path, frag_pad_dim): D is the power-of-two layout, the columns are a.D < D rows
+// apart, and a lane whose rows start at or past a.D holds zeros and stores nothing.
+template <typename T, int D, int U, bool TAIL, int DBG = 0, bool PAD = false>
 __device__ __forceinline__ void load_tile(const FlowArgs& a, int64_t col0, T (&x)[U][Frag<T, D>::V]) {
   using F = Frag<T, D>;
   constexpr int V = F::V, G = F::G, SEG = F::SEG;
   const int lane = threadIdx.x & 63;
   const int r0 = D >= V ? V * (lane % G) : 0;
+  const int64_t ld = PAD ? (int64_t)a.D : (int64_t)D;
+  const bool live = !PAD || r0 < a.D;
   const T* __restrict__ X = (const T*)a.X;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t cf = frag_col<T, D>(col0, u, lane);
-    const int64_t eoff = cf * D + r0;
+    const int64_t eoff = cf * ld + r0;
     if (DBG >= 1) {
 #pragma unroll
       for (int e = 0; e < V; ++e) x[u][e] = (T)(lane + 3 * u + e) * (T)0.03125 - (T)1;
     } else if (!TAIL) {
-      const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X + eoff));
-      __builtin_memcpy(&x[u][0], &v4, 16);
+      if (live) {
+        const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X + eoff));
+        __builtin_memcpy(&x[u][0], &v4, 16);
+      } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e) x[u][e] = (T)0;
+      }
     } else {
 #pragma unroll
-      for (int e = 0; e < V; ++e) x[u][e] = (cf + e / SEG) < a.N ? X[eoff + e] : (T)0;
+      for (int e = 0; e < V; ++e) x[u][e] = (live && (cf + e / SEG) < a.N) ? X[eoff + e] : (T)0;
     }
   }
 }
@@ -340,7 +349,7 @@ __device__ __forceinline__ void tile_dots(const Tile<T, D, U>& x, const T (&v)[F
 }
 
 // ---- tile epilogue: store Y and the ladj
-template <typename T, int D, int U, int LM, bool TAIL, int DBG>
+template <typename T, int D, int U, int LM, bool TAIL, int DBG, bool PAD = false>
 __device__ __forceinline__ void store_tile(const FlowArgs& a, T ctot, int64_t col0, Tile<T, D, U>& x,
                                            Acc<T, D, U>& acc,
                                            const T (&old)[LadjOut<T, D, U>::NLS][LadjOut<T, D, U>::W],
@@ -351,19 +360,23 @@ __device__ __forceinline__ void store_tile(const FlowArgs& a, T ctot, int64_t co
   T* __restrict__ Y = (T*)a.Y;
   const int64_t N = a.N;
   const int r0 = D >= V ? V * (lane % G) : 0;
+  const int64_t ld = PAD ? (int64_t)a.D : (int64_t)D;
+  const bool live = !PAD || r0 < a.D;
   int64_t colf[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) colf[u] = frag_col<T, D>(col0, u, lane);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int64_t eoff = colf[u] * D + r0;
+    const int64_t eoff = colf[u] * ld + r0;
     if (DBG == 2) {
       if (x[u][0] == (T)1234.5) Y[eoff] = x[u][1];  // keeps the compute alive, never true in practice
     } else if (!TAIL) {
-      u32x4 v4;
-      __builtin_memcpy(&v4, &x[u][0], 16);
-      __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(Y + eoff));
-    } else {
+      if (live) {
+        u32x4 v4;
+        __builtin_memcpy(&v4, &x[u][0], 16);
+        __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(Y + eoff));
+      }
+    } else if (live) {
 #pragma unroll
       for (int e = 0; e < V; ++e)
         if (colf[u] + e / SEG < N) Y[eoff + e] = x[u][e];
@@ -413,7 +426,7 @@ __device__ __forceinline__ void store_tile(const FlowArgs& a, T ctot, int64_t co
 // Body::tile<TAIL, DBG>(col0, x, old) runs the flow on one register tile and stores it. pro() -- the
 // block prologue, with its barrier -- runs exactly once per wave, after the wave's first tile loads
 // are issued, so their HBM latency overlaps it.
-template <typename T, int D, int U, int LM, int DBG, typename Body, typename Pro>
+template <typename T, int D, int U, int LM, int DBG, bool PAD = false, typename Body, typename Pro>
 __device__ __forceinline__ void frag_stream(const FlowArgs& a, Body& body, Pro&& pro) {
   using F = Frag<T, D>;
   using LO = LadjOut<T, D, U>;
@@ -430,21 +443,21 @@ __device__ __forceinline__ void frag_stream(const FlowArgs& a, Body& body, Pro&&
   OT old;
   const int64_t t = wave_id;
   if (t < ntiles_full) {
-    load_tile<T, D, U, false, DBG>(a, t * COLS_PER_TILE, xa);
+    load_tile<T, D, U, false, DBG, PAD>(a, t * COLS_PER_TILE, xa);
     int64_t t1 = t + nwaves;
     load_ladj_old<T, D, U, LM>(a, t * COLS_PER_TILE, old);
-    load_tile<T, D, U, false, DBG>(a, (t1 < ntiles_full ? t1 : t) * COLS_PER_TILE, xb);
+    load_tile<T, D, U, false, DBG, PAD>(a, (t1 < ntiles_full ? t1 : t) * COLS_PER_TILE, xb);
     pro();
     body.template tile<false, DBG>(t * COLS_PER_TILE, xa, old);
     while (t1 < ntiles_full) {
       const int64_t t2 = t1 + nwaves;
       load_ladj_old<T, D, U, LM>(a, t1 * COLS_PER_TILE, old);
-      load_tile<T, D, U, false, DBG>(a, (t2 < ntiles_full ? t2 : t1) * COLS_PER_TILE, xa);
+      load_tile<T, D, U, false, DBG, PAD>(a, (t2 < ntiles_full ? t2 : t1) * COLS_PER_TILE, xa);
       body.template tile<false, DBG>(t1 * COLS_PER_TILE, xb, old);
       if (t2 >= ntiles_full) break;
       const int64_t t3 = t2 + nwaves;
       load_ladj_old<T, D, U, LM>(a, t2 * COLS_PER_TILE, old);
-      load_tile<T, D, U, false, DBG>(a, (t3 < ntiles_full ? t3 : t2) * COLS_PER_TILE, xb);
+      load_tile<T, D, U, false, DBG, PAD>(a, (t3 < ntiles_full ? t3 : t2) * COLS_PER_TILE, xb);
       body.template tile<false, DBG>(t2 * COLS_PER_TILE, xa, old);
       t1 = t3;
     }
@@ -453,7 +466,7 @@ __device__ __forceinline__ void frag_stream(const FlowArgs& a, Body& body, Pro&&
   }
   if (ntiles_full * COLS_PER_TILE < a.N && wave_id == ntiles_full % nwaves) {
     const int64_t c0 = ntiles_full * COLS_PER_TILE;
-    load_tile<T, D, U, true>(a, c0, xa);
+    load_tile<T, D, U, true, 0, PAD>(a, c0, xa);
     // tail: old ladj only for existing columns
     const int lane = threadIdx.x & 63;
 #pragma unroll

@@ -53,7 +53,7 @@ struct FlowArgs {
   int32_t frag;  // 1: fragment kernel (records laid out with RV = 16/elem), 0: generic kernel
   int32_t wy;  // 1: run on the dense-Householder MFMA kernel (the step table has OP_DENSE steps)
   int32_t img_off;  // dense kernel: LDS byte offset of the per-wave transpose images (set at launch)
-  int32_t pad_;
+  int32_t dk;       // padded fragment path: the power of two the kernel lays the D rows out as (0: D)
   LayerDesc layers[kMaxLayers];
   Step steps[kMaxSteps];
   int32_t desc[kMaxSteps + 1];  // per step: op | (record offset << 4); desc[nsteps] = sentinel 0
@@ -76,6 +76,19 @@ inline bool frag_path(int64_t D, int64_t ldx, int64_t ldy, const void* X, const 
   const int64_t dmax = elem == 4 ? 256 : 128;
   const bool pow2 = D >= 1 && D <= dmax && (D & (D - 1)) == 0;
   return pow2 && ldx == D && ldy == D && ((((uintptr_t)X) | ((uintptr_t)Y)) & 15) == 0;
+}
+
+// Padded fragment path: D not a power of two but whole 16-byte fragments per column (D a multiple of
+// 16/elem), contiguous 16-byte aligned columns, at most 256 (fp32) / 128 (fp64) rows once rounded up to
+// a power of two. The kernel lays the column out as Dp = that power of two; lanes whose rows lie past
+// D neither load nor store and carry neutral parameters (enf_steps.h build_program). Returns Dp, or 0.
+inline int64_t frag_pad_dim(int64_t D, int64_t ldx, int64_t ldy, const void* X, const void* Y, size_t elem) {
+  const int64_t dmax = elem == 4 ? 256 : 128, v = (int64_t)(16 / elem);
+  if (D < v || D > dmax || (D & (D - 1)) == 0 || D % v != 0 || ldx != D || ldy != D) return 0;
+  if (((((uintptr_t)X) | ((uintptr_t)Y)) & 15) != 0) return 0;
+  int64_t p = 1;
+  while (p < D) p <<= 1;
+  return p;
 }
 
 // Values of T in one step's LDS record: W * max(D, RV) (RV = 16/elem on the fragment path, else 1),

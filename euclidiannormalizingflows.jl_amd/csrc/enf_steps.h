@@ -88,9 +88,24 @@ __device__ __forceinline__ void param_values(int op, const LayerDesc& L, int col
 // (the frag kernels issue their first tile before the prologue) and they are not waited for here.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Padded fragment path (a.dk != 0): D (= DC) is the power-of-two layout and Dr = a.D the real rows;
+// the parameters are read and the constants summed over the Dr real rows, and the rows past Dr get
+// neutral records that map the zeros those lanes hold to 0 with ladj 0: reflection v = 0, ScaleShift
+// (1, 0), Johnson / JohnsonInv gamma = xi = 0, delta = lambda = 1.
+template <typename T>
+__device__ __forceinline__ void neutral_values(int op, T (&out)[8]) {
+  for (int q = 0; q < 8; ++q) out[q] = (T)0;
+  if (op == OP_SCALESHIFT) out[0] = (T)1;
+  if (op == OP_JOHNSON || op == OP_JOHNSON_INV) {
+    out[1] = (std::is_same_v<T, float> && op == OP_JOHNSON) ? (T)kLn2 : (T)1;  // delta (ln2 delta), 1/delta
+    out[3] = (T)1;                                                               // 1/lambda, lambda
+  }
+}
+
 template <typename T, int DC, int RV>
 __device__ double build_program(const FlowArgs& a, T* __restrict__ rec, double* __restrict__ stepc) {
   const int D = DC > 0 ? DC : a.D;
+  const int Dr = a.dk ? a.D : D;  // real rows
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int nent = D > RV ? D : RV;  // record entries per parameter
   if constexpr (std::is_same_v<T, double>)
@@ -105,9 +120,9 @@ __device__ double build_program(const FlowArgs& a, T* __restrict__ rec, double* 
     const int W = record_width(st.op);
     T* r = rec + st.off;
     double part = 0.0;
-    for (int d = lane; d < D; d += 64) {
+    for (int d = lane; d < Dr; d += 64) {
       if (st.op == OP_HOUSEHOLDER) {
-        const double v = (double)((const T*)L.p[0])[(int64_t)st.col * D + d];
+        const double v = (double)((const T*)L.p[0])[(int64_t)st.col * Dr + d];
         part += v * v;
       } else if (st.op == OP_SCALESHIFT) {
         part += log(fabs((double)((const T*)L.p[0])[d]));  // scale_shift_trafo.jl:22
@@ -131,7 +146,8 @@ __device__ double build_program(const FlowArgs& a, T* __restrict__ rec, double* 
       const int g = D >= RV ? i / RV : 0, e = i % RV;
       const int row = D >= RV ? i : e % D;
       T vals[8];
-      param_values<T>(st.op, L, st.col, D, row, hscale, vals);
+      if (row < Dr) param_values<T>(st.op, L, st.col, Dr, row, hscale, vals);
+      else neutral_values<T>(st.op, vals);
       for (int q = 0; q < W; ++q) r[(g * W + q) * RV + e] = vals[q];
     }
     if (lane == 0)

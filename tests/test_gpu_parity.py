@@ -27,7 +27,7 @@ def test_golden_flow(enf, gpu, oracle, name):
     assert_as_accurate(to_np(Y), to_np(L), Yt, Lt, Yx, Lx, X.dtype, what=name)
 
 
-DS = [1, 2, 3, 4, 5, 8, 16, 32, 64, 100, 128, 256]
+DS = [1, 2, 3, 4, 5, 8, 12, 16, 32, 36, 64, 100, 128, 256]
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
@@ -50,7 +50,7 @@ def test_single_op_vs_oracle(enf, gpu, oracle, dtype, op, D):
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-@pytest.mark.parametrize("D", [2, 32, 64, 128, 256])
+@pytest.mark.parametrize("D", [2, 24, 32, 64, 100, 128, 256])
 def test_config3_pattern_vs_oracle(enf, gpu, oracle, dtype, D):
     """J4∘H4∘…∘J1∘H1 (SURVEY.md §8(d) config 3 pattern) on 200k samples."""
     rng = np.random.default_rng(7 + D)
@@ -422,3 +422,43 @@ def test_fp64_johnson_ulp_and_large_z_ladj(enf, gpu, oracle, D):
     fin = np.isfinite(Lr)
     assert fin[:64].all()
     assert np.all(np.abs(L[fin] - Lr[fin]) <= 1e-12 * (np.abs(Lr[fin]) + 1))
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("D", [6, 12, 20, 100])
+def test_padded_fragment_path(enf, gpu, oracle, dtype, D):
+    """D a multiple of 16/sizeof(T) but not a power of two runs on the fragment kernel laid out as the
+    next power of two (csrc/enf_internal.h frag_pad_dim): every op it takes (ScaleShift, Johnson,
+    JohnsonInv, chained Householder) in one flow, tails of the wave tile, in place + accumulate through
+    the raw C ABI, and ladj = NULL."""
+    import torch
+
+    if dtype == np.float32 and D % 4:
+        pytest.skip("fp32 fragments hold 4 rows")
+    rng = np.random.default_rng(D)
+    layers = [(0, rand_params(rng, 0, D, dtype)), (5, rand_params(rng, 5, D, dtype, K=3)),
+              (3, rand_params(rng, 3, D, dtype)), (5, rand_params(rng, 5, D, dtype)), (4, rand_params(rng, 4, D, dtype)),
+              (3, rand_params(rng, 3, D, dtype))]
+    for N in (1, 63, 4097, 70_001):
+        X = np.asfortranarray(rng.standard_normal((D, N)).astype(dtype))
+        Y, L = enf.with_logabsdet_jacobian(make_flow(enf, layers), colmajor_cuda(X))
+        check_vs_oracle(oracle, layers, X, to_np(Y), to_np(L), dtype, what=f"padded D{D} N{N}")
+    dev = [[torch.from_numpy(np.ascontiguousarray(np.asarray(p).reshape(D, -1, order="F").T)).cuda() for p in ps]
+           for _, ps in layers]
+    lt = [(op, (np.asarray(ps[0]).reshape(D, -1, order="F").shape[1] if op == 5 else 0), [t.data_ptr() for t in dv])
+          for (op, ps), dv in zip(layers, dev)]
+    code = enf._lib.ENF_F32 if dtype == np.float32 else enf._lib.ENF_F64
+    buf = torch.from_numpy(np.ascontiguousarray(X.T)).cuda()
+    lad = torch.full((N,), 1.5, dtype=buf.dtype, device="cuda")
+    assert _raw_apply(enf, code, D, N, buf.data_ptr(), D, buf.data_ptr(), D, lad.data_ptr(), 1, lt) == 0
+    torch.cuda.synchronize()
+    # same kernel arithmetic as the out-of-place call above: Y bit for bit, ladj + 1.5 up to its rounding
+    Yo, Lo = to_np(Y), to_np(L).reshape(-1)
+    assert np.array_equal(buf.cpu().numpy().T, Yo)
+    eps = np.finfo(dtype).eps
+    assert np.all(np.abs(lad.cpu().numpy() - (Lo + 1.5)) <= 2 * eps * (np.abs(Lo) + 1.5))
+    Y2 = torch.zeros_like(buf)
+    X2 = torch.from_numpy(np.ascontiguousarray(X.T)).cuda()
+    assert _raw_apply(enf, code, D, N, X2.data_ptr(), D, Y2.data_ptr(), D, None, 0, lt) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(Y2.cpu().numpy(), buf.cpu().numpy())
