@@ -62,8 +62,10 @@ __device__ __forceinline__ void d2_load(const D2Args& a, int64_t col0, int lane,
       x[u][0] = (double)(lane + 3 * u) * 0.03125 - 1.0;
       x[u][1] = (double)(lane - 5 * u) * 0.0625 + 0.5;
     } else if (!TAIL) {
-      const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.X + 2 * c));
-      __builtin_memcpy(&x[u][0], &v4, 16);
+      if (ENF_INB(c < a.N, "d2 load X", c, a.N)) {
+        const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.X + 2 * c));
+        __builtin_memcpy(&x[u][0], &v4, 16);
+      }
     } else {
       x[u][0] = c < a.N ? a.X[2 * c] : 0.0;
       x[u][1] = c < a.N ? a.X[2 * c + 1] : 0.0;
@@ -108,16 +110,18 @@ __device__ __forceinline__ void d2_tile(const D2Args& a, const D2Prog& P, const 
     if (DBG == 2) {
       if (x[u][0] == 1234.5) a.Y[2 * c] = x[u][1];  // keeps the compute alive, never true in practice
     } else if (!TAIL) {
-      u32x4 v4;
-      __builtin_memcpy(&v4, &x[u][0], 16);
-      __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(a.Y + 2 * c));
+      if (ENF_INB(c < a.N, "d2 store Y", c, a.N)) {
+        u32x4 v4;
+        __builtin_memcpy(&v4, &x[u][0], 16);
+        __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(a.Y + 2 * c));
+      }
     } else if (c < a.N) {
       a.Y[2 * c] = x[u][0];
       a.Y[2 * c + 1] = x[u][1];
     }
     if (LM > 0 && DBG != 2) {
       const double v = fma(1.0, lad[u], P.ctot) + old[u];
-      if (!TAIL || c < a.N) a.ladj[c] = v;
+      if ((!TAIL && ENF_INB(c < a.N, "d2 ladj", c, a.N)) || (TAIL && c < a.N)) a.ladj[c] = v;
     }
   }
 }

@@ -120,9 +120,11 @@ __device__ __forceinline__ void hj_load(const HJArgs& a, int64_t col0, float (&x
 #pragma unroll
         for (int e = 0; e < 4; ++e) x[u][4 * h + e] = (float)(lane + 3 * u + 5 * h + e) * 0.03125f - 1.f;
       } else if (!TAIL) {
-        const u32x4 v4 = DBG == 8 ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X + off))
-                                  : *reinterpret_cast<const u32x4*>(X + off);
-        __builtin_memcpy(&x[u][4 * h], &v4, 16);
+        if (ENF_INB(c < a.N, "hj load X", c, a.N)) {
+          const u32x4 v4 = DBG == 8 ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X + off))
+                                    : *reinterpret_cast<const u32x4*>(X + off);
+          __builtin_memcpy(&x[u][4 * h], &v4, 16);
+        }
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) x[u][4 * h + e] = c < a.N ? X[off + e] : 0.f;
@@ -163,6 +165,7 @@ __device__ __forceinline__ void hj_store(const HJArgs& a, float ctot, int64_t co
       } else if (!TAIL) {
         u32x4 v4;
         __builtin_memcpy(&v4, &x[u][4 * h], 16);
+        if (!ENF_INB(c < a.N, "hj store Y", c, a.N)) continue;
         if (DBG == 9) *reinterpret_cast<u32x4*>(Y + off) = v4;
         else __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(Y + off));
       } else if (c < a.N) {
@@ -183,7 +186,7 @@ __device__ __forceinline__ void hj_store(const HJArgs& a, float ctot, int64_t co
       const int c = k * 64 + (L::TC >= 64 ? lane : lane % L::TC);
       const float v = fmaf((float)kLn2, stage[c], ctot) + old[k];
       const int64_t col = col0 + c;
-      if (!TAIL || col < a.N) ladj[col] = v;
+      if ((!TAIL && ENF_INB(col < a.N, "hj ladj", col, a.N)) || (TAIL && col < a.N)) ladj[col] = v;
     }
   }
 }

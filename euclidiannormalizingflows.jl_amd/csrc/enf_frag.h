@@ -241,7 +241,7 @@ __device__ __forceinline__ void load_tile(const FlowArgs& a, int64_t col0, T (&x
 #pragma unroll
       for (int e = 0; e < V; ++e) x[u][e] = (T)(lane + 3 * u + e) * (T)0.03125 - (T)1;
     } else if (!TAIL) {
-      if (live) {
+      if (live && (!PAD || ENF_INB(eoff + V <= a.N * a.ldx, "frag load X", eoff, a.N * a.ldx))) {
         const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X + eoff));
         __builtin_memcpy(&x[u][0], &v4, 16);
       } else {
@@ -371,7 +371,7 @@ __device__ __forceinline__ void store_tile(const FlowArgs& a, T ctot, int64_t co
     if (DBG == 2) {
       if (x[u][0] == (T)1234.5) Y[eoff] = x[u][1];  // keeps the compute alive, never true in practice
     } else if (!TAIL) {
-      if (live) {
+      if (live && (!PAD || ENF_INB(eoff + V <= a.N * a.ldy, "frag store Y", eoff, a.N * a.ldy))) {
         u32x4 v4;
         __builtin_memcpy(&v4, &x[u][0], 16);
         __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(Y + eoff));
@@ -392,8 +392,11 @@ __device__ __forceinline__ void store_tile(const FlowArgs& a, T ctot, int64_t co
         for (int c = 0; c < CPF; ++c) {
           const int64_t col = colf[u] + c;
           const T v = fma(Unit<T>::v, acc[u][c], ctot) + old[u][c];
-          if (!TAIL) ladj[col] = v;
-          else if (col < N) ladj[col] = v;
+          if (!TAIL) {
+            if (!PAD || ENF_INB(col < N, "frag ladj", col, N)) ladj[col] = v;
+          } else if (col < N) {
+            ladj[col] = v;
+          }
         }
       }
     } else {
@@ -408,8 +411,11 @@ __device__ __forceinline__ void store_tile(const FlowArgs& a, T ctot, int64_t co
         const int c = k * 64 + (LO::TC >= 64 ? lane : lane % LO::TC);
         const T v = fma(Unit<T>::v, stage[c], ctot) + old[k][0];
         const int64_t col = col0 + c;
-        if (!TAIL) ladj[col] = v;
-        else if (col < N) ladj[col] = v;
+        if (!TAIL) {
+          if (!PAD || ENF_INB(col < N, "frag ladj staged", col, N)) ladj[col] = v;
+        } else if (col < N) {
+          ladj[col] = v;
+        }
       }
     }
   }

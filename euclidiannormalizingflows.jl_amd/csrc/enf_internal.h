@@ -101,6 +101,22 @@ inline size_t record_elems(int op, int64_t D, size_t elem, bool frag) {
   return (n + q - 1) / q * q;
 }
 
+// Bounds-check build (`make bcheck`, a diagnostics aid, never shipped): the global tile accesses of the
+// fused flow kernels check their index against the tensor's extent; a violation is printed and the
+// access skipped.
+#ifndef ENF_BOUNDS
+#define ENF_BOUNDS 0
+#endif
+#if ENF_BOUNDS
+#define ENF_INB(ok, what, idx, lim)                                                                   \
+  ((ok) ? true                                                                                        \
+        : (printf("ENF_OOB %s idx=%lld lim=%lld blk=%d thr=%d\n", what, (long long)(idx), (long long)(lim), \
+                  (int)blockIdx.x, (int)threadIdx.x),                                                 \
+           false))
+#else
+#define ENF_INB(ok, what, idx, lim) true
+#endif
+
 // Tuning and diagnostic knobs. The shipping library (libenf.so) is built with ENF_DIAG=0: every
 // knob is its compile-time default, nothing is read from the environment and the diagnostic kernel
 // variants (ENF_DEBUG_MODE: synthesized tiles / no stores) are not compiled in. The diagnostics
