@@ -6,7 +6,8 @@
 //
 // Per pair p (the register tile holds y, the previous Johnson output, on entry -- X itself for p = 0):
 //   dot = vh'y,  vh = v sqrt(2/v'v)                 householder_trafo! (householder_trafo.jl:8-11)
-//   z   = y/lambda - xi/lambda - dot vh/lambda      (y - vh dot - xi)/lambda (johnson_trafo.jl:30)
+//   z   = (y - dot vh)/lambda - xi/lambda           the reflection's output, then (x - xi)/lambda as
+//                                                    fma(x, 1/lambda, -xi/lambda) (johnson_trafo.jl:30)
 //   L_p = asinh(z)/ln2                              asinh2 (enf_frag.h): log2(|z| + sqrt(q)),
 //                                                    q = 1 + z^2, or the Taylor form for |z| < 1/8
 //   ladj += log|delta/lambda| - log(q)/2            johnson_trafo.jl:41; the constant part once per
@@ -326,19 +327,21 @@ __device__ __forceinline__ float prod_tree(const float (&q)[R]) {
 }
 
 // The dot and z of one pair, in place on the tile (x: the pair's input y on entry, z on exit).
+// In the reference's operation order: the reflection's output y - vh (vh'y), then (. - xi)/lambda as
+// fma(., 1/lambda, -xi/lambda) (the records' vh/lambda slot is not read).
 template <int D, int R, int U>
 __device__ __forceinline__ void hj_pair_z(float (&x)[U][R], const float* r, HJParams<R>& prm) {
-  prm.template load<HJ_IL, kHjW>(r);
+  prm.template load<HJ_IL, HJ_RR>(r);
   float dot[U];
   hj_dots<D, R, U>(x, prm, dot);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_IL, e), prm.m(HJ_NXI, e));
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(-dot[u], prm.m(HJ_VH, e), x[u][e]);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < R; ++e) x[u][e] = fmaf(-dot[u], prm.m(HJ_RR, e), x[u][e]);
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_IL, e), prm.m(HJ_NXI, e));
 }
 
 // One pair (reflection + Johnson) on the register tile, fast form. x holds L (pair 0: the input x)
