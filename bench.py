@@ -241,7 +241,11 @@ def main():
         cpu = cpu_baseline(layers, D, np_dtype, args.cpu_seconds)
     train = None
     headline = (D, N, args.pairs, args.dtype, args.pattern) == (32, 10_000_000, 4, "f32", None)
-    if headline and not args.no_train and not args.selftest_cpu:
+    if args.selftest_cpu and not args.no_train:  # the config-5 leg's rank plumbing on gloo
+        import bench_train
+
+        train = bench_train.train_leg_selftest(world, rank, steps=min(args.steps, 20))
+    elif headline and not args.no_train:
         train = train_leg(dev, world, rank)
 
     if rank == 0:
@@ -283,15 +287,16 @@ def main():
 def train_leg(dev, world, rank):
     """Config 5 (optimize_whitening, D = 32, N = 1e7, B = 1e5, 4x(J∘H), ADAGrad)
     on the same ranks after the headline measurement, reported beside it as the `train` object (its
-    own metric, steps/s; not part of `value`). One epoch (100 steps) after 5 warm-up steps. One rank:
-    the fused step (enf_whitening_step) replayed as a HIP graph. Several ranks: each minibatch split
-    over the ranks, the gradient sums combined by torch.distributed's all-reduce (RCCL over xGMI; the
-    backend of this harness's own barriers), eager launches -- the graph-captured libenf RCCL step
-    (EnfComm) is bench_train.py's. Errors are reported in the object, never replace the headline."""
+    own metric, steps/s; not part of `value`). One epoch (100 steps) after 5 warm-up steps, the timed
+    steps captured once as a HIP graph and replayed. One rank: the fused step (enf_whitening_step).
+    Several ranks: each minibatch split over the ranks, the gradient sums combined by RCCL over xGMI
+    called through libenf (EnfComm, enf_allreduce_sum) on the kernels' stream, so gradient, all-reduce
+    and update of every step are in the graph (bench_train.py's fastest data-parallel step). Errors are
+    reported in the object, never replace the headline."""
     import bench_train
 
     try:
-        return bench_train.train_leg(dev, world, rank, graph=world == 1, comm_kind="enf" if world == 1 else "torch")
+        return bench_train.train_leg(dev, world, rank, graph=True, comm_kind="enf")
     except Exception as e:  # noqa: BLE001 -- the headline line is printed regardless
         return {"error": f"{type(e).__name__}: {e}"}
 

@@ -37,20 +37,20 @@ import enf_launch  # noqa: E402
 from bench import build_flow, gather_ranks, max_over_ranks  # noqa: E402
 
 
-def selftest_cpu(args, world, rank):
-    """The harness on gloo without a GPU: each rank sums a stand-in gradient over its share of every
-    minibatch, the shares are summed across ranks, and every rank must end with the same update."""
+def train_leg_selftest(world, rank, N=10_000_000, nbatches=100, steps=100):
+    """The data-parallel step's plumbing on the CPU (torch.distributed already initialised on gloo when
+    world > 1): each rank sums a stand-in gradient over its share of every minibatch, the shares are
+    summed across ranks, and every rank must end with the same update. Returns the record (rank 0's is
+    printed); measures nothing."""
     import torch
 
-    if world > 1:
-        torch.distributed.init_process_group("gloo")
     from enf_pkg import load
 
-    plan = load().minibatch_plan(args.N, args.nbatches, rank, world)
-    Xh = np.cos(np.arange(args.N, dtype=np.float64))
+    plan = load().minibatch_plan(N, nbatches, rank, world)
+    Xh = np.cos(np.arange(N, dtype=np.float64))
     theta = torch.zeros(3, dtype=torch.float64)
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(steps):
         B, lo, hi = plan[i % len(plan)]
         g = torch.tensor([float(Xh[lo:hi].sum()), float((Xh[lo:hi] ** 2).sum()), float(hi - lo)], dtype=torch.float64)
         if world > 1:
@@ -60,11 +60,31 @@ def selftest_cpu(args, world, rank):
     wall = time.perf_counter() - t0
     per_rank = gather_ranks(wall, torch.device("cpu"), world, rank)
     th = gather_ranks(float(theta.sum()), torch.device("cpu"), world, rank)
+    return {"metric": "optimize_whitening training steps/s (config 5)", "value": steps / max(per_rank),
+            "unit": "steps/s", "n_gpus": world, "steps": steps, "selftest": "cpu (measures nothing)",
+            "per_rank_s": per_rank, "ranks_agree": len(set(th)) == 1,
+            "step": step_description(world == 1, world, "enf", True),
+            "config": {"parallelism": f"dp{world}", "B": plan[0][0]}}
+
+
+def step_description(fused, world, comm_kind, graph):
+    """What one timed config-5 step runs (the `step` / `launch` fields of the record)."""
+    if fused:
+        return "enf_whitening_step (fused, 1 rank)"
+    comm = ("libenf EnfComm (RCCL over xGMI on the kernels' stream" + (", captured in the HIP graph)" if graph else ")")
+            if comm_kind == "enf" else "torch.distributed all_reduce (eager)")
+    return f"enf_flow_negll_grad + {comm} + enf_whitening_apply"
+
+
+def selftest_cpu(args, world, rank):
+    """The harness on gloo without a GPU (train_leg_selftest)."""
+    import torch
+
+    if world > 1:
+        torch.distributed.init_process_group("gloo")
+    res = train_leg_selftest(world, rank, args.N, args.nbatches, args.steps)
     if rank == 0:
-        print(json.dumps({"metric": "optimize_whitening training steps/s (config 5)", "value": args.steps / max(per_rank),
-                          "unit": "steps/s", "n_gpus": world, "steps": args.steps, "selftest": "cpu (measures nothing)",
-                          "per_rank_s": per_rank, "ranks_agree": len(set(th)) == 1,
-                          "config": {"parallelism": f"dp{world}", "B": plan[0][0]}}))
+        print(json.dumps(res))
     if world > 1:
         torch.distributed.destroy_process_group()
 
@@ -249,9 +269,7 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
         "grad_kernel_ms_median" if not fused else "fused_step_ms_median": grad_ms,
         "grad_kernel_ms_max_rank" if not fused else "fused_step_ms_max_rank": grad_ms_max, "dtype": "f32",
         "launch": "HIP graph of the timed steps (torch.cuda.CUDAGraph), replayed" if graph else "eager",
-        "step": "enf_whitening_step (fused, 1 rank)" if fused else
-                "enf_flow_negll_grad + RCCL sum (" + ("libenf EnfComm" if comm is not None else "torch.distributed")
-                + ") + enf_whitening_apply",
+        "step": step_description(fused, world, "enf" if comm is not None else "torch", graph),
         "per_rank_ms_per_step": per_rank_ms,
         "data": "synthetic: X = f_true^-1(Z), Z ~ N(0,1) (torch Philox 0x5EED), f_true seed 7, init seed 42",
         "config": {"workload": f"optimize_whitening D={D}, N={N}, nbatches={nbatches} "
@@ -259,6 +277,11 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
                    "per_rank_share": plan[0][2] - plan[0][1], "parallelism": f"dp{world}"},
         "negll_first": negll[0], "negll_last": negll[-1],
     }
+    if graph:
+        # the graph holds the captured RCCL all-reduce: release it (and let its work drain) before the
+        # communicator (the order optimize_whitening uses)
+        del cg
+        torch.cuda.synchronize()
     if comm is not None:
         comm.close()
     return res

@@ -24,7 +24,8 @@ UNIQUE_ID_BYTES = 128
 EXPORTED = (
     "enf_version", "enf_last_error", "enf_device_count", "enf_set_device", "enf_get_device",
     "enf_malloc", "enf_free", "enf_memcpy", "enf_stream_synchronize", "enf_flow_apply", "enf_flow_apply_host",
-    "enf_flow_param_count", "enf_flow_negll_grad_workspace", "enf_flow_negll_grad",
+    "enf_flow_param_count", "enf_flow_negll_grad_workspace", "enf_flow_negll_grad", "enf_flow_negll_workspace",
+    "enf_flow_negll",
     "enf_adagrad_step", "enf_householder_normalize", "enf_householder_normalize_strided", "enf_comm_unique_id", "enf_comm_init",
     "enf_comm_destroy", "enf_allreduce_sum", "enf_johnsonsu_eval", "enf_johnsonsu_sample",
     "enf_whitening_step", "enf_whitening_apply", "enf_flow_vjp", "enf_flow_apply_cpu",
@@ -67,6 +68,9 @@ _SIGS = {
                                                      ctypes.POINTER(_sz)]),
     "enf_flow_negll_grad": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _vp, _i64, ctypes.POINTER(Layer), _i32,
                                            _vp, _vp, _sz, _vp]),
+    "enf_flow_negll_workspace": (ctypes.c_int, [ctypes.c_int, _i64, _i64, ctypes.POINTER(_sz)]),
+    "enf_flow_negll": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _vp, _i64, ctypes.POINTER(Layer), _i32, _vp, _vp, _sz,
+                                      _vp]),
     "enf_flow_apply_cpu": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i32,
                                           ctypes.POINTER(Layer), _i32, _i32]),
     "enf_flow_vjp": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _vp, _i64, _vp, _i64, _vp, ctypes.POINTER(Layer), _i32,

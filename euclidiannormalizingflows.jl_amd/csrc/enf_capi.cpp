@@ -77,6 +77,8 @@ enf_status validate_layers(int64_t D, const enf_layer* layers, int32_t nlayers) 
     if (np < 0) return fail(ENF_ERR_INVALID, "layer " + std::to_string(l) + ": unknown op " + std::to_string(layers[l].op));
     if (layers[l].op == ENF_OP_HOUSEHOLDER && layers[l].k < 1)
       return fail(ENF_ERR_INVALID, "layer " + std::to_string(l) + ": HouseholderTrafo needs k >= 1 columns");
+    if (layers[l].op == ENF_OP_SCALESHIFT && layers[l].k != 0 && layers[l].k != 1)
+      return fail(ENF_ERR_INVALID, "layer " + std::to_string(l) + ": ScaleShiftTrafo k must be 0 (length-D a) or 1 (length-1 a)");
     if (D > 0)
       for (int q = 0; q < np; ++q)
         if (!layers[l].p[q])
@@ -215,14 +217,10 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
   // OP_DENSE steps of <= D reflections each, col = first column | count << 16)
   bool frag = enf::frag_path(D, ldx, ldy, X, Y, elem) && enf::frag_path(D, ldy, ldy, Y, Y, elem);
   // padded fragment path: D a multiple of 16/elem but not a power of two, laid out as the next power
-  // of two (enf_internal.h frag_pad_dim) when every layer maps 0 to 0 with neutral parameters
+  // of two (enf_internal.h frag_pad_dim); every op has neutral parameters that map 0 to 0 with ladj 0
   int64_t dk = 0;
   if (!frag) {
     dk = enf::frag_pad_dim(D, ldx, ldy, X, Y, elem);
-    for (int32_t l = 0; l < nlayers && dk; ++l) {
-      const int op = layers[l].op;
-      if (op != ENF_OP_HOUSEHOLDER && op != ENF_OP_JOHNSON && op != ENF_OP_JOHNSON_INV && op != ENF_OP_SCALESHIFT) dk = 0;
-    }
     frag = dk != 0;
   }
   bool wy = false;
@@ -289,6 +287,9 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
     a.ldy = ldy;
     a.ladj = ladj;
     a.accumulate = first ? accumulate_ladj : 1;
+#if ENF_BOUNDS
+    a.csum = enf::flow_args_csum(a);
+#endif
     hipError_t e = enf::launch_flow(a, dtype == ENF_F64, st, dev);
     if (e != hipSuccess) return hip_fail(e, "flow kernel launch");
     first = false;
@@ -483,6 +484,31 @@ enf_status enf_flow_negll_grad(enf_dtype dtype, int64_t D, int64_t N, const void
   if (N == 0) return ENF_OK;
   if (D > 0 && !X) return fail(ENF_ERR_INVALID, "X is NULL");
   return enf::negll_grad(dtype == ENF_F64, D, N, X, ldx, layers, nlayers, out, workspace, workspace_bytes,
+                         (hipStream_t)hip_stream);
+  ENF_CATCH
+}
+
+enf_status enf_flow_negll_workspace(enf_dtype dtype, int64_t D, int64_t N, size_t* bytes) {
+  ENF_TRY
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
+  if (D < 0 || N < 0) return fail(ENF_ERR_INVALID, "D and N must be >= 0");
+  if (!bytes) return fail(ENF_ERR_INVALID, "bytes is NULL");
+  return enf::negll_loss_workspace(dtype == ENF_F64, D, N, bytes);
+  ENF_CATCH
+}
+
+enf_status enf_flow_negll(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
+                          int32_t nlayers, void* out, void* workspace, size_t workspace_bytes, void* hip_stream) {
+  ENF_TRY
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
+  if (D < 0 || N < 0) return fail(ENF_ERR_INVALID, "D and N must be >= 0");
+  if (ldx < (D > 0 ? D : 1)) return fail(ENF_ERR_INVALID, "ldx < D");
+  enf_status vs = validate_layers(D, layers, nlayers);
+  if (vs != ENF_OK) return vs;
+  if (!out) return fail(ENF_ERR_INVALID, "out is NULL");
+  if (N == 0) return ENF_OK;
+  if (D > 0 && !X) return fail(ENF_ERR_INVALID, "X is NULL");
+  return enf::negll_loss(dtype == ENF_F64, D, N, X, ldx, layers, nlayers, out, workspace, workspace_bytes,
                          (hipStream_t)hip_stream);
   ENF_CATCH
 }

@@ -22,6 +22,8 @@
 //
 // Execution: column blocks of kBlock samples, each block through all layers while it sits in cache;
 // blocks are shared by worker threads (std::thread, static round-robin).
+#include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -83,7 +85,8 @@ void layer_block(const HostLayer& L, int64_t D, int64_t nc, T* Y, int64_t ld, T*
   switch (L.op) {
     case ENF_OP_SCALESHIFT: {
       T s = T(0);
-      for (int64_t d = 0; d < D; ++d) s += std::log(std::fabs(p0[d]));
+      // sum(log.(abs.(f.a))) over a's own length (k = 1: a length-1 `a` broadcast to the D rows)
+      for (int64_t d = 0; d < (L.k == 1 ? std::min<int64_t>(D, 1) : D); ++d) s += std::log(std::fabs(p0[d]));
       for (int64_t j = 0; j < nc; ++j) {
         T* y = Y + j * ld;
         for (int64_t d = 0; d < D; ++d) y[d] = std::fma(y[d], p0[d], p1[d]);
@@ -170,9 +173,12 @@ void run_cpu(int64_t D, int64_t N, const T* X, int64_t ldx, T* Y, int64_t ldy, T
     }
   }
   const int64_t nblocks = (N + kBlock - 1) / kBlock;
-  auto worker = [&](int w) {
+  // blocks are claimed from a shared counter, so the blocks of a worker that could not be started run on
+  // the others (each block's arithmetic is independent of which thread runs it)
+  std::atomic<int64_t> next{0};
+  auto worker = [&](int) {
     std::vector<T> lt((size_t)nl * kBlock);
-    for (int64_t b = w; b < nblocks; b += nthreads) {
+    for (int64_t b = next.fetch_add(1); b < nblocks; b = next.fetch_add(1)) {
       const int64_t c0 = b * kBlock, nc = N - c0 < kBlock ? N - c0 : kBlock;
       T* Yb = Y + c0 * ldy;
       const T* Xb = X + c0 * ldx;
@@ -194,7 +200,13 @@ void run_cpu(int64_t D, int64_t N, const T* X, int64_t ldx, T* Y, int64_t ldy, T
     return;
   }
   std::vector<std::thread> pool;
-  for (int w = 1; w < nthreads; ++w) pool.emplace_back(worker, w);
+  pool.reserve((size_t)nthreads);
+  try {
+    for (int w = 1; w < nthreads; ++w) pool.emplace_back(worker, w);
+  } catch (...) {
+    // thread or resource limit: go on with the workers already started (never leave a joinable thread
+    // to a destructor, which would terminate the process)
+  }
   worker(0);
   for (auto& t : pool) t.join();
 }
@@ -206,7 +218,7 @@ enf_status flow_apply_cpu(bool f64, int64_t D, int64_t N, const void* X, int64_t
   std::vector<HostLayer> hl((size_t)nlayers);
   for (int l = 0; l < nlayers; ++l) {
     hl[l].op = layers[l].op;
-    hl[l].k = layers[l].op == ENF_OP_HOUSEHOLDER ? layers[l].k : 0;
+    hl[l].k = (layers[l].op == ENF_OP_HOUSEHOLDER || layers[l].op == ENF_OP_SCALESHIFT) ? layers[l].k : 0;
     for (int q = 0; q < 4; ++q) hl[l].p[q] = layers[l].p[q];
   }
   int nt = nthreads;

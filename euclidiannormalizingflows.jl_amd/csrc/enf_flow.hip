@@ -113,6 +113,7 @@ __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
   T* stage = reinterpret_cast<T*>(smem + kLdsScalars) + (threadIdx.x >> 6) * kStagePerWave;
   T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
   (void)ctotp;
+  ENF_KARG_CHECK(a);
   if constexpr (DBG == 5) {  // diagnostics: nothing (the launch floor of the grid)
     if (threadIdx.x == 0 && a.N == -1) ((T*)a.Y)[blockIdx.x] = (T)0;
     return;
@@ -212,6 +213,7 @@ __global__ __launch_bounds__(256) void flow_generic_kernel(FlowArgs a) {
   double* ctotp = stepc + kMaxSteps;
   T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
   (void)ctotp;
+  ENF_KARG_CHECK(a);
   const double ctot = build_program<T, 0, 1>(a, rec, stepc);
   const int D = a.D;
   const T* __restrict__ X = (const T*)a.X;
@@ -244,6 +246,7 @@ __global__ __launch_bounds__(256) void flow_lds_kernel(FlowArgs a, int ct, int d
   double* ctotp = stepc + kMaxSteps;
   T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
   (void)ctotp;
+  ENF_KARG_CHECK(a);
   const double ctot = build_program<T, 0, 1>(a, rec, stepc);
   const int D = a.D;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -338,9 +341,9 @@ static hipError_t launch_frag(const FlowArgs& a, size_t lds, hipStream_t st, con
   return hipGetLastError();
 }
 
-// The padded fragment path (a.dk = the power-of-two layout of a.D rows): reflections, Johnson layers
-// and ScaleShift only (the ops whose neutral parameters map 0 to 0 with ladj 0, enf_steps.h).
-constexpr int kOpsPad = (1 << OP_HOUSEHOLDER) | (1 << OP_JOHNSON) | (1 << OP_JOHNSON_INV) | (1 << OP_SCALESHIFT);
+// The padded fragment path (a.dk = the power-of-two layout of a.D rows): every op has neutral
+// parameters that map 0 to 0 with ladj 0 (enf_steps.h neutral_values).
+constexpr int kOpsPad = kOpsAll;
 template <typename T, int LADJ>
 static hipError_t dispatch_pad(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
   switch (a.dk) {
@@ -467,6 +470,9 @@ hipError_t launch_flow(const FlowArgs& a, bool f64, hipStream_t st, const Device
   if (!no_lds && a.D >= 1 && (size_t)ct * dp * elem <= wave_kb && ct >= 16 && (int64_t)ct * a.D <= (1 << 14)) {
     FlowArgs b = a;
     b.img_off = (int32_t)((lds + 15) / 16 * 16);
+#if ENF_BOUNDS
+    b.csum = flow_args_csum(b);
+#endif
     const size_t ldsb = (size_t)b.img_off + 4 * (size_t)ct * dp * elem;
     const uint32_t magic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)a.D - 1) / (uint64_t)a.D);
     const void* k = f64 ? (ladj ? (const void*)&flow_lds_kernel<double, true> : (const void*)&flow_lds_kernel<double, false>)

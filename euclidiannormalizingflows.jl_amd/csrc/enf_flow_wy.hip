@@ -312,6 +312,7 @@ __global__ __launch_bounds__(256) void flow_wy_kernel(FlowArgs a) {
   double* hs = reinterpret_cast<double*>(smem + kLdsScalars);  // dense-prologue scratch (the stage area)
   T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
   (void)ctotp;
+  ENF_KARG_CHECK(a);
   const double ctot_d = build_program<T, D, Frag<T, D>::V>(a, rec, stepc);
   for (int s = 0; s < a.nsteps; ++s)
     if (a.steps[s].op == OP_DENSE) {
@@ -357,6 +358,9 @@ template <typename T, int LM>
 hipError_t dispatch_wy(const FlowArgs& a0, size_t lds, hipStream_t st, const DeviceInfo& dev) {
   FlowArgs a = a0;
   a.img_off = (int32_t)((lds + 15) / 16 * 16);
+#if ENF_BOUNDS
+  a.csum = flow_args_csum(a);
+#endif
   if (a.D == 32) return launch_wy_t<T, 32, LM>(a, a.img_off + 4 * WYT<T, 32>::kBytesPerWave, st, dev);
   if (a.D == 64) return launch_wy_t<T, 64, LM>(a, a.img_off + 4 * WYT<T, 64>::kBytesPerWave, st, dev);
   return hipErrorInvalidValue;

@@ -229,11 +229,13 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
   constexpr int SEG = D >= V ? V : D;
   constexpr int COLS = 64 / G * CPF;  // columns per wave tile (one fragment per lane)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // LDS: [grad accumulators: 4 waves x nparams doubles][loss: 4 waves x double][records][activations]
+  // LDS: [grad accumulators: nw waves x nparams doubles][loss: nw (<= 4) waves x double][records][activations]
+  // (nw = blockDim.x / 64: 4, or fewer when D > 64 makes the per-wave accumulators large)
+  const int nw = blockDim.x >> 6;
   const int gbytes = ((a.nparams * 8 + 15) / 16) * 16;
   double* gacc = reinterpret_cast<double*>(smem + (threadIdx.x >> 6) * gbytes);  // this wave's
-  double* lossw = reinterpret_cast<double*>(smem + 4 * gbytes);
-  T* rec = reinterpret_cast<T*>(smem + 4 * gbytes + 64);
+  double* lossw = reinterpret_cast<double*>(smem + nw * gbytes);
+  T* rec = reinterpret_cast<T*>(smem + nw * gbytes + 64);
   int nrec = 0;
   for (int s = 0; s < a.nsteps; ++s) nrec += grad_nparams(a.op[s]) * (D > V ? D : V);
   T* act = rec + ((nrec + 3) / 4) * 4 + (threadIdx.x >> 6) * (a.nsteps * 64 * V);
@@ -278,7 +280,7 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
   const int grp = D >= V ? lane % G : 0;
   const int64_t ntiles = (a.N + COLS - 1) / COLS;
   double lossp = 0.0;
-  for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < ntiles; t += (int64_t)gridDim.x * 4) {
+  for (int64_t t = (int64_t)blockIdx.x * nw + wave; t < ntiles; t += (int64_t)gridDim.x * nw) {
     const int64_t c0 = t * COLS + (lane / G) * CPF;
     T x[V];
     bool valid[V];
@@ -310,13 +312,16 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
         }
       } else {
         const int np = grad_nparams(op);
+        // ScaleShiftTrafo with a length-1 `a` (layer k = 1): its ladj constant log|a| counts once, on row 0
+        // (scale_shift_trafo.jl:22 sums over a's own length)
+        const bool ss1 = op == OP_SCALESHIFT && a.layers[a.layer[s]].k == 1;
 #pragma unroll
         for (int e = 0; e < V; ++e) {
           T p[4];
           for (int q = 0; q < np; ++q) p[q] = r[q * V + e];
           T l = 0;
           x[e] = fwd_elem<T>(op, x[e], p, l);
-          lad[e / SEG] += l;
+          if (!ss1 || r0 + e % SEG == 0) lad[e / SEG] += l;
         }
       }
     }
@@ -378,12 +383,15 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
           }
         }
       } else {
+        const bool ss1 = op == OP_SCALESHIFT && a.layers[a.layer[s]].k == 1;
 #pragma unroll
         for (int e = 0; e < V; ++e) {
           T p[4], dp[4] = {0, 0, 0, 0};
           for (int q = 0; q < np; ++q) p[q] = r[q * V + e];
-          const T gx = bwd_elem<T>(op, xin[e], g[e], p, dp, VJP ? cl[e / SEG] : (T)-1);
           const int row = r0 + e % SEG;
+          // (ScaleShift's ladj cotangent only reaches its ladj term, which a length-1 `a` has on row 0 only)
+          const T clw = (ss1 && row != 0) ? (T)0 : (VJP ? cl[e / SEG] : (T)-1);
+          const T gx = bwd_elem<T>(op, xin[e], g[e], p, dp, clw);
           for (int q = 0; q < np; ++q)
             wave_accumulate<G, CPF, SEG>(gacc + a.goff[s] + q * a.D, row, valid[e] ? dp[q] : (T)0, lane, a.D);
           g[e] = valid[e] ? gx : (T)0;
@@ -404,11 +412,17 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
   __syncthreads();
   if (!a.partial) return;  // enf_flow_vjp without parameter cotangents
   double* out = (double*)a.partial + (int64_t)blockIdx.x * (1 + a.nparams);
-  if (tid == 0) out[0] = lossw[0] + lossw[1] + lossw[2] + lossw[3];
+  if (tid == 0) {  // the waves' values in wave order (deterministic)
+    double l = lossw[0];
+    for (int w = 1; w < nw; ++w) l += lossw[w];
+    out[0] = l;
+  }
   const double* g0 = reinterpret_cast<const double*>(smem);
+  const int w8 = gbytes / 8;
   for (int i = tid; i < a.nparams; i += blockDim.x) {
-    const int w = gbytes / 8;
-    out[1 + i] = ((g0[i] + g0[w + i]) + g0[2 * w + i]) + g0[3 * w + i];
+    double v = g0[i];
+    for (int w = 1; w < nw; ++w) v += g0[w * w8 + i];
+    out[1 + i] = v;
   }
 }
 
@@ -462,8 +476,9 @@ __device__ __forceinline__ void finalize_totals(const ReduceArgs& r) {
   double* tot = r.tot;
   const int64_t n = 1 + (int64_t)r.nparams;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  // Householder columns h = w, w + 4, ... of this wave: their entries (D <= 64: one per lane) and
-  // norms, loaded while the slices are summed (they do not depend on the totals)
+  // Householder columns h = w, w + 4, ... of this wave: their first 64 entries (one per lane; D > 64
+  // adds entries lane + 64, lane + 128, ... below) loaded while the slices are summed (they do not
+  // depend on the totals)
   constexpr int kPerWave = (kMaxGradSteps + 3) / 4;
   double vh[kPerWave], nrm[kPerWave];
 #pragma unroll
@@ -478,7 +493,13 @@ __device__ __forceinline__ void finalize_totals(const ReduceArgs& r) {
   }
 #pragma unroll
   for (int j = 0; j < kPerWave; ++j) {
+    const int h = w + 4 * j;
     double vv = vh[j] * vh[j];
+    if (h < r.nh)
+      for (int d = lane + 64; d < r.D; d += 64) {
+        const double v = (double)((const T*)r.hcol[h])[d];
+        vv += v * v;
+      }
     for (int m = 32; m >= 1; m >>= 1) vv += __shfl_xor(vv, m);
     nrm[j] = sqrt(vv);
   }
@@ -489,11 +510,15 @@ __device__ __forceinline__ void finalize_totals(const ReduceArgs& r) {
     const int h = w + 4 * j;
     if (h >= r.nh) break;  // wave-uniform
     double* gw = tot + 1 + r.hoff[h];
+    const T* vc = (const T*)r.hcol[h];
     const double g = lane < r.D ? gw[lane] : 0.0;
     const double wv = vh[j] / nrm[j];
     double wd = -1.4142135623730951 * g * wv;
+    for (int d = lane + 64; d < r.D; d += 64) wd += -1.4142135623730951 * gw[d] * ((double)vc[d] / nrm[j]);
     for (int m = 32; m >= 1; m >>= 1) wd += __shfl_xor(wd, m);
     if (lane < r.D) gw[lane] = (-1.4142135623730951 * g - wv * wd) / nrm[j];
+    for (int d = lane + 64; d < r.D; d += 64)
+      gw[d] = (-1.4142135623730951 * gw[d] - ((double)vc[d] / nrm[j]) * wd) / nrm[j];
   }
   __syncthreads();
 }
@@ -569,9 +594,13 @@ struct Plan {
   ReduceArgs ra;
   size_t lds = 0;
   int blocks = 0;
+  int nw = 4;  // waves per block of the generic kernel
 };
 
-bool grad_D_supported(int64_t D) { return D >= 1 && D <= 64; }
+// Kernel rows Dp (D rounded up to a power of two) up to 256 fp32 / 128 fp64: a column is at most one
+// 64-lane group of 16-byte fragments (the flow kernels' fragment layout).
+bool grad_D_supported(int64_t D, bool f64) { return D >= 1 && D <= (f64 ? 128 : 256); }
+constexpr size_t kGradLdsMax = 160 * 1024;
 
 // kernel rows: D rounded up to a power of two
 int64_t grad_Dp(int64_t D) {
@@ -583,7 +612,8 @@ int64_t grad_Dp(int64_t D) {
 enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, int32_t nlayers, Plan& P) {
   std::memset(&P.ga, 0, sizeof P.ga);
   std::memset(&P.ra, 0, sizeof P.ra);
-  if (!grad_D_supported(D)) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: D must be <= 64");
+  if (!grad_D_supported(D, f64))
+    return set_error(ENF_ERR_UNSUPPORTED, f64 ? "enf_flow_negll_grad: fp64 D must be <= 128" : "enf_flow_negll_grad: fp32 D must be <= 256");
   if (nlayers > kMaxGradLayers) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: more than 16 layers");
   const int V = f64 ? 2 : 4;
   const int64_t Dp = grad_Dp(D);
@@ -620,11 +650,14 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
   const size_t esz = f64 ? 8 : 4;
   const size_t gbytes = ((size_t)goff * 8 + 15) / 16 * 16;
   const size_t rbytes = ((size_t)(roff + 3) / 4) * 4 * esz;
-  const size_t abytes = (size_t)4 * s * 64 * V * esz;
-  P.lds = 4 * gbytes + 64 + rbytes + abytes;  // generic kernel; checked where it is launched
+  const size_t abytes = (size_t)s * 64 * V * esz;  // per wave
+  // 4 waves per block, fewer when their per-wave gradient accumulators and activations do not fit
+  P.nw = 4;
+  while (P.nw > 1 && P.nw * (gbytes + abytes) + 64 + rbytes > kGradLdsMax) P.nw >>= 1;
+  P.lds = P.nw * (gbytes + abytes) + 64 + rbytes;  // generic kernel; checked where it is launched
   const int cols = (int)(64 / (Dp >= V ? Dp / V : 1) * (Dp >= V ? 1 : V / Dp));
   const int64_t tiles = (N + cols - 1) / cols;
-  int64_t blocks = (tiles + 3) / 4;
+  int64_t blocks = (tiles + P.nw - 1) / P.nw;
   DeviceInfo dev;
   if (current_device_info(&dev) != ENF_OK) return ENF_ERR_HIP;
   // blocks per CU (2: what the fused kernel's LDS lets stay resident; measured best at config 5)
@@ -646,7 +679,7 @@ hipError_t launch_grad_D(const Plan& P, hipStream_t st) {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((negll_grad_kernel<T, DD, VJP>), dim3(P.blocks), dim3(256), P.lds, st, P.ga);
+  hipLaunchKernelGGL((negll_grad_kernel<T, DD, VJP>), dim3(P.blocks), dim3(64 * P.nw), P.lds, st, P.ga);
   return hipGetLastError();
 }
 
@@ -655,8 +688,14 @@ hipError_t launch_grad(const Plan& P, hipStream_t st) {
   hipError_t e0 = hipSuccess;
   switch (P.ga.Dp) {
 #define ENF_G(DD) case DD: e0 = launch_grad_D<T, DD, VJP>(P, st); break;
-    ENF_G(1) ENF_G(2) ENF_G(4) ENF_G(8) ENF_G(16) ENF_G(32) ENF_G(64)
+    ENF_G(1) ENF_G(2) ENF_G(4) ENF_G(8) ENF_G(16) ENF_G(32) ENF_G(64) ENF_G(128)
 #undef ENF_G
+    case 256:
+      if constexpr (std::is_same_v<T, float>) {
+        e0 = launch_grad_D<T, 256, VJP>(P, st);
+        break;
+      }
+      return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
   return e0;
@@ -692,7 +731,7 @@ enf_status grad_parts(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx
   if (!f64 && !generic && hj_grad_eligible(D, ldx, X, layers, nlayers)) {
     e = launch_hj_grad(D, N, X, layers, nlayers, P.ga.nparams, (double*)workspace, P.blocks, st);
   } else {
-    if (P.lds > 160 * 1024) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: flow too large for LDS");
+    if (P.lds > kGradLdsMax) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: flow too large for LDS");
     e = f64 ? launch_grad<double>(P, st) : launch_grad<float>(P, st);
   }
   if (e == hipSuccess) {
@@ -724,7 +763,7 @@ enf_status flow_vjp(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, 
   Plan P;
   enf_status s = make_plan(f64, D, N, layers, nlayers, P);
   if (s != ENF_OK) return s;
-  if (P.lds > 160 * 1024) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_vjp: flow too large for LDS");
+  if (P.lds > kGradLdsMax) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_vjp: flow too large for LDS");
   P.ga.X = X;
   P.ga.ldx = ldx;
   P.ga.dY = dY;

@@ -40,6 +40,8 @@ struct Step {
 };
 
 struct FlowArgs {
+  uint32_t csum;  // bounds-check build only: checksum of the tables below (flow_args_csum), else 0
+  int32_t pad0_;
   const void* X;
   void* Y;
   void* ladj;  // nullptr: no ladj
@@ -58,6 +60,18 @@ struct FlowArgs {
   Step steps[kMaxSteps];
   int32_t desc[kMaxSteps + 1];  // per step: op | (record offset << 4); desc[nsteps] = sentinel 0
 };
+
+// Checksum of a FlowArgs from X through desc[] (FNV-1a over 32-bit words). The bounds-check build
+// (ENF_BOUNDS) sets it on the host right before each launch and every block of the interpreter kernels
+// recomputes it from its kernel-argument copy: a mismatch means the kernel read kernel arguments other
+// than the ones launched (printed as ENF_KARG_STALE).
+__host__ __device__ inline uint32_t flow_args_csum(const FlowArgs& a) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&a);
+  const size_t n = (offsetof(FlowArgs, desc) + sizeof(a.desc)) / 4;
+  uint32_t h = 2166136261u;
+  for (size_t i = offsetof(FlowArgs, X) / 4; i < n; ++i) h = (h ^ w[i]) * 16777619u;
+  return h;
+}
 
 struct DeviceInfo {
   int num_cu = 0;
@@ -113,8 +127,18 @@ inline size_t record_elems(int op, int64_t D, size_t elem, bool frag) {
         : (printf("ENF_OOB %s idx=%lld lim=%lld blk=%d thr=%d\n", what, (long long)(idx), (long long)(lim), \
                   (int)blockIdx.x, (int)threadIdx.x),                                                 \
            false))
+#define ENF_KARG_CHECK(a)                                                                             \
+  do {                                                                                                \
+    if (threadIdx.x == 0) {                                                                           \
+      const uint32_t h_ = flow_args_csum(a);                                                          \
+      if (h_ != (a).csum)                                                                             \
+        printf("ENF_KARG_STALE blk=%d got=%08x want=%08x N=%lld D=%d nsteps=%d\n", (int)blockIdx.x, h_, \
+               (a).csum, (long long)(a).N, (a).D, (a).nsteps);                                         \
+    }                                                                                                 \
+  } while (0)
 #else
 #define ENF_INB(ok, what, idx, lim) true
+#define ENF_KARG_CHECK(a) do { } while (0)
 #endif
 
 // Tuning and diagnostic knobs. The shipping library (libenf.so) is built with ENF_DIAG=0: every

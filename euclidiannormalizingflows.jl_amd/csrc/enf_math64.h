@@ -185,7 +185,7 @@ __device__ __forceinline__ double logprod64_tab(const double (&q)[NQ], const dou
   return qs < __builtin_huge_val() ? l : qs;
 }
 
-// sinh(w) over the whole double range// sinh(w) over the whole double range (johnson_trafo.jl:36), odd, +-Inf -> +-Inf, NaN -> NaN:
+// sinh(w) over the whole double range (johnson_trafo.jl:36), odd, +-Inf -> +-Inf, NaN -> NaN:
 //   |w| < 1: the odd Taylor series to w^17 (truncation < 1e-17 relative);
 //   else e^|w|/2 - e^-|w|/2 with e^|w| = 2^k e^r (msun e_exp.c reduction, |r| <= ln2/2, e^r by its
 //   Taylor series to r^13, truncation < 2^-57) and both halves scaled by ldexp, so sinh stays finite

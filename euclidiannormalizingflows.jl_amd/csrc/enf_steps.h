@@ -91,7 +91,10 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // Padded fragment path (a.dk != 0): D (= DC) is the power-of-two layout and Dr = a.D the real rows;
 // the parameters are read and the constants summed over the Dr real rows, and the rows past Dr get
 // neutral records that map the zeros those lanes hold to 0 with ladj 0: reflection v = 0, ScaleShift
-// (1, 0), Johnson / JohnsonInv gamma = xi = 0, delta = lambda = 1.
+// (1, 0), Johnson / JohnsonInv gamma = xi = 0, delta = lambda = 1, CenterStretch / CenterContract
+// a = c = 0, b = 1 (center_stretch(0) = sign(0)... + c = 0 and center_contract(0) = 0; both ladjs are
+// log|1/2 + 1/2| = 0, center_stretch.jl:4-22; exactly so in the fp32 steps: exp2(0) = 1, sqrt(4) = 2,
+// log2(1) = 0, rcp(2) = 1/2).
 template <typename T>
 __device__ __forceinline__ void neutral_values(int op, T (&out)[8]) {
   for (int q = 0; q < 8; ++q) out[q] = (T)0;
@@ -99,6 +102,17 @@ __device__ __forceinline__ void neutral_values(int op, T (&out)[8]) {
   if (op == OP_JOHNSON || op == OP_JOHNSON_INV) {
     out[1] = (std::is_same_v<T, float> && op == OP_JOHNSON) ? (T)kLn2 : (T)1;  // delta (ln2 delta), 1/delta
     out[3] = (T)1;                                                               // 1/lambda, lambda
+  }
+  if (op == OP_CENTER_STRETCH || op == OP_CENTER_CONTRACT) {
+    if constexpr (std::is_same_v<T, float>) {  // {b log2e, c, ln2/b, exp(ba), exp(2ba), ba log2e, a, b}
+      out[0] = (float)kLog2e;
+      out[2] = (float)kLn2;
+      out[3] = 1.0f;
+      out[4] = 1.0f;
+      out[7] = 1.0f;
+    } else {  // {a, b, c}
+      out[1] = 1.0;
+    }
   }
 }
 
@@ -125,7 +139,8 @@ __device__ double build_program(const FlowArgs& a, T* __restrict__ rec, double* 
         const double v = (double)((const T*)L.p[0])[(int64_t)st.col * Dr + d];
         part += v * v;
       } else if (st.op == OP_SCALESHIFT) {
-        part += log(fabs((double)((const T*)L.p[0])[d]));  // scale_shift_trafo.jl:22
+        // scale_shift_trafo.jl:22, summed over a's own length (k = 1: a length-1 a broadcast to the rows)
+        if (L.k != 1 || d == 0) part += log(fabs((double)((const T*)L.p[0])[d]));
       } else if (st.op == OP_JOHNSON || st.op == OP_JOHNSON_INV) {
         // log|delta/lambda| (johnson_trafo.jl:41,51); the inverse negates (johnson_trafo.jl:104)
         const double c = log(fabs((double)((const T*)L.p[1])[d])) - log(fabs((double)((const T*)L.p[3])[d]));

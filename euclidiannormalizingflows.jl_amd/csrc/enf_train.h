@@ -17,6 +17,9 @@ enf_status negll_grad_workspace(bool f64, int64_t D, int64_t N, const enf_layer*
                                 size_t* bytes);
 enf_status negll_grad(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
                       int32_t nlayers, void* out, void* workspace, size_t workspace_bytes, hipStream_t st);
+enf_status negll_loss_workspace(bool f64, int64_t D, int64_t N, size_t* bytes);
+enf_status negll_loss(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
+                      int32_t nlayers, void* out, void* workspace, size_t workspace_bytes, hipStream_t st);
 enf_status flow_vjp(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const void* dY, int64_t lddy,
                     const void* dladj, const enf_layer* layers, int32_t nlayers, void* dX, int64_t lddx, void* dparams,
                     void* workspace, size_t workspace_bytes, hipStream_t st);

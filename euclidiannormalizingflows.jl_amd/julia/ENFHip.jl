@@ -167,6 +167,9 @@ function _layers(fs, D, ::Type{T}) where {T}
             push!(keep, M)
             ptrs[q] = M.buf.ptr
         end
+        # ScaleShiftTrafo with a length-1 vector `a`: k = 1, its ladj constant log|a[1]| counts once
+        # (src/scale_shift_trafo.jl:22; enf_layer.k in include/enf.h)
+        op == OP_SCALESHIFT && f.a isa AbstractVector && length(f.a) == 1 && (k = 1)
         push!(layers, EnfLayer(op, Int32(k), Tuple(ptrs)))
     end
     layers, keep
@@ -229,14 +232,30 @@ function stream_with_logabsdet_jacobian(f::_Supported, X::Matrix{T}; chunk_cols:
 end
 
 # --- mvnormal_negll_trafo / mvnormal_negll_trafograd (src/optimize_whitening.jl:7-22) ----------
-const _log2π = log(2π)
 
-# negll = -(sum(std_normal_logpdf.(Y)) + sum(ladj)) / n, with the reference's two sums (:12)
-function mvnormal_negll_trafo(trafo::_Supported, X::HipMatrix)
-    Y, L = _apply(trafo, X, true)
-    y = Array(Y)
-    l = Array(L)
-    -(sum(@. -(abs2(y) + _log2π) / 2) + sum(l)) / X.N
+# negll = -(sum(std_normal_logpdf.(Y)) + sum(ladj)) / n (:12), the flow and both sums on the device
+# (enf_flow_negll: one deterministic double reduction of (y^2 + log 2pi)/2 - ladj); only the scalar is
+# copied back. The flow runs in its promoted element type R, as mvnormal_negll_trafograd's.
+function mvnormal_negll_trafo(trafo::_Supported, X::HipMatrix{T}) where {T}
+    fs = _leaves(trafo)
+    R = _flow_eltype(fs, T)
+    Xr = _convert(X, R)
+    layers, keep = _layers(fs, Xr.D, R)
+    wsb = Ref{Csize_t}(0)
+    GC.@preserve wsb begin
+        check(ccall((:enf_flow_negll_workspace, libenf), Cint, (Cint, Int64, Int64, Ref{Csize_t}),
+                    _dt(R), Xr.D, Xr.N, wsb))
+    end
+    ws = HipBuffer(max(Int(wsb[]), 1))
+    out = HipMatrix(zeros(R, 1, 1))
+    GC.@preserve Xr layers keep ws out begin
+        check(ccall((:enf_flow_negll, libenf), Cint,
+                    (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Ptr{EnfLayer}, Int32, Ptr{Cvoid}, Ptr{Cvoid},
+                     Csize_t, Ptr{Cvoid}),
+                    _dt(R), Xr.D, Xr.N, Xr.buf.ptr, Xr.D, layers, length(layers), out.buf.ptr, ws.ptr, ws.bytes,
+                    C_NULL))
+    end
+    Array(out)[1] / Xr.N
 end
 
 _flow_eltype(fs, ::Type{T}) where {T} = foldl((R, f) -> _promoted(R, f), fs; init = float(T))
@@ -433,7 +452,8 @@ function optimize_whitening(smpls::HipMatrix{T}, initial_trafo::Function, optimi
             i += 1
             ptrs[q] = theta.buf.ptr + offs[i] * sizeof(R)
         end
-        k = op == OP_HOUSEHOLDER ? Int32(length(getfield(f, :V)) ÷ D) : Int32(0)
+        k = op == OP_HOUSEHOLDER ? Int32(length(getfield(f, :V)) ÷ D) :
+            (op == OP_SCALESHIFT && f.a isa AbstractVector && length(f.a) == 1) ? Int32(1) : Int32(0)
         push!(layers, EnfLayer(op, k, Tuple(ptrs)))
     end
     world, rank = comm === nothing ? (1, 0) : (comm.nranks, comm.rank)

@@ -251,6 +251,11 @@ class ScaleShiftTrafo(Trafo):
         ainv = 1 / a
         return ScaleShiftTrafo(_restore_type(self.a, ainv), _restore_type(self.b, -ainv * _as_param_array(self.b)))
 
+    def _k(self) -> int:
+        # enf_layer.k = 1: `a` is a length-1 vector (expanded to the D rows on the device) whose ladj
+        # constant sum(log.(abs.(a))) counts its single entry once (src/scale_shift_trafo.jl:22)
+        return 1 if _is_vector(self.a) and np.size(_as_cpu_array(self.a)) == 1 else 0
+
     def _check_ladj_signature(self, is_vector_input):
         # with_logabsdet_jacobian is defined only for vector a and matrix x (scale_shift_trafo.jl:18-21)
         if not _is_vector(self.a) or is_vector_input:

@@ -189,15 +189,20 @@ def _scaleshift_a_segments(state: FlowState):
     return out
 
 
+def _scaleshift_a_range(state: FlowState, seg: int, t) -> tuple:
+    """[start, end) of the entries of a ScaleShiftTrafo's `a` that its ladj sums: all D rows of a
+    length-D vector, the single entry of a length-1 vector (expanded to D copies in theta;
+    src/scale_shift_trafo.jl:22 sums over a's own length)."""
+    s0, s1 = int(state.offsets[seg]), int(state.offsets[seg + 1])
+    return (s0, s0 + 1) if t._k() == 1 else (s0, s1)
+
+
 def _scaleshift_ladj_const(state: FlowState) -> float:
-    c, seg = 0.0, 0
-    th = None
-    for t in state.trafos:
-        for _ in t.FIELDS:
-            if isinstance(t, ScaleShiftTrafo) and _ == "a":
-                th = state.theta.detach().cpu().numpy() if th is None else th
-                c += float(np.sum(np.log(np.abs(th[state.offsets[seg]:state.offsets[seg + 1]]))))
-            seg += 1
+    c = 0.0
+    th = state.theta.detach().cpu().numpy()
+    for seg, t in _scaleshift_a_segments(state):
+        s0, s1 = _scaleshift_a_range(state, seg, t)
+        c += float(np.sum(np.log(np.abs(th[s0:s1]))))
     return c
 
 
@@ -282,8 +287,24 @@ def flow_vjp(trafo, X, dY, dladj=None, param_grads: bool = False):
 
 
 def mvnormal_negll_trafo(trafo, X) -> float:
-    """-(sum(std_normal_logpdf.(Y)) + sum(ladj)) / nsamples (src/optimize_whitening.jl:7-15)."""
-    return mvnormal_negll_trafograd(trafo, X)[0]
+    """-(sum(std_normal_logpdf.(Y)) + sum(ladj)) / nsamples (src/optimize_whitening.jl:7-15): the flow
+    and the reduction on the device (enf_flow_negll, any flow with_logabsdet_jacobian takes); only the
+    scalar comes back."""
+    M, _, _ = _to_device_matrix(X)
+    dtype = _dtype_of(trafo, M)
+    M = _colmajor(M, dtype)
+    D, N = M.shape
+    state = FlowState(trafo, D, dtype, M.device)
+    L = _lib.lib()
+    dt = _lib.ENF_F64 if dtype == torch.float64 else _lib.ENF_F32
+    nb = ctypes.c_size_t(0)
+    _lib.check(L.enf_flow_negll_workspace(dt, D, N, ctypes.byref(nb)))
+    ws = torch.empty(max(1, (nb.value + 7) // 8), dtype=torch.float64, device=M.device)
+    out = torch.zeros(1, dtype=dtype, device=M.device)
+    with torch.cuda.device(M.device):
+        _lib.check(L.enf_flow_negll(dt, D, N, M.data_ptr(), _ld(M), state.layers(), len(state.trafos), out.data_ptr(),
+                                    ws.data_ptr(), ws.numel() * 8, torch.cuda.current_stream(M.device).cuda_stream))
+    return float((out / N).item())
 
 
 def trainable_runs(state: "FlowState"):
@@ -389,7 +410,7 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
     hist = torch.zeros(nepochs * len(plan), dtype=torch.float64, device=M.device)
     hbatches = householder_batches(state)
     segs = trainable_runs(state)
-    ss_a = [(int(state.offsets[i]), int(state.offsets[i + 1])) for i, _ in _scaleshift_a_segments(state)]
+    ss_a = [_scaleshift_a_range(state, i, t) for i, t in _scaleshift_a_segments(state)]
     tied = state.tied_segments()
     # one rank: the fused step (gradient, loss, ADAGrad and re-normalisation in three launches)
     fused = world == 1 and not tied and comm is None

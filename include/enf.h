@@ -68,7 +68,11 @@ typedef enum {
 
 typedef struct {
   int32_t op;        /* enf_op */
-  int32_t k;         /* HOUSEHOLDER: number of reflection columns (>= 1); otherwise ignored */
+  int32_t k;         /* HOUSEHOLDER: number of reflection columns (>= 1).
+                      * SCALESHIFT: 0 = `a` is a length-D vector; 1 = `a` is a LENGTH-1 vector that the
+                      * caller broadcast to the D rows p[0] points at: the ladj constant is log|a[1]|
+                      * once (sum(log.(abs.(f.a))) over the length-1 vector, src/scale_shift_trafo.jl:22)
+                      * and so is its gradient (1/a on row 0 only). Otherwise ignored (0). */
   const void* p[4];  /* device pointers */
 } enf_layer;
 
@@ -134,13 +138,23 @@ enf_status enf_flow_param_count(int64_t D, const enf_layer* layers, int32_t nlay
  * out has 1 + param_count entries and is ACCUMULATED into (zero it first). Divide by the
  * global batch size after the cross-GPU sum to obtain negll and its gradient.
  * workspace: device scratch of enf_flow_negll_grad_workspace() bytes.
- * Limits: D <= 64, at most 16 layers / 32 steps (ENF_ERR_UNSUPPORTED otherwise). */
+ * Limits: D <= 256 (fp32) / 128 (fp64), at most 16 layers / 32 steps (ENF_ERR_UNSUPPORTED otherwise). */
 enf_status enf_flow_negll_grad_workspace(enf_dtype dtype, int64_t D, int64_t N,
                                          const enf_layer* layers, int32_t nlayers,
                                          size_t* bytes);
 enf_status enf_flow_negll_grad(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
                                const enf_layer* layers, int32_t nlayers, void* out,
                                void* workspace, size_t workspace_bytes, void* hip_stream);
+/* mvnormal_negll_trafo (src/optimize_whitening.jl:7-15) without the gradient, for any flow
+ * enf_flow_apply takes (no dimension / step limits): out[0] (device, dtype) += the unnormalised
+ *   sum_j [ sum_d (y_dj^2 + log 2pi)/2 - ladj_j ]        (negll = out[0] / N)
+ * with (Y, ladj) = with_logabsdet_jacobian(flow, X), reduced on the device in double in a fixed order
+ * (deterministic). workspace: device scratch of enf_flow_negll_workspace() bytes (holds Y, ladj and
+ * the partial sums). Asynchronous on hip_stream. */
+enf_status enf_flow_negll_workspace(enf_dtype dtype, int64_t D, int64_t N, size_t* bytes);
+enf_status enf_flow_negll(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
+                          const enf_layer* layers, int32_t nlayers, void* out, void* workspace,
+                          size_t workspace_bytes, void* hip_stream);
 /* Vector-Jacobian product of (Y, ladj) = with_logabsdet_jacobian(flow, X) (the Zygote pullback the
  * reference's rrules build: householder_trafo_pullback_x / chained_householder_trafo_pullback_x,
  * src/householder_trafo.jl:43-54,105-124, and broadcast AD of the elementwise maps). Given the

@@ -42,6 +42,11 @@ def test_bench_launches_two_ranks():
     # whole-job aggregate: both ranks' samples over the max-over-ranks wall time
     assert out["value"] == pytest.approx(2 * 1000 * 3 / (out["ms_per_step"] * 3 / 1e3), rel=1e-6)
     assert out["scaling"] == "weak"
+    # the config-5 leg at N = 2: minibatch shares tile every batch, the ranks agree, and the step the GPU
+    # run times is the graph-captured libenf RCCL (EnfComm) data-parallel step
+    t = out["train"]
+    assert t["n_gpus"] == 2 and t["ranks_agree"] and len(t["per_rank_s"]) == 2
+    assert "EnfComm" in t["step"] and "captured in the HIP graph" in t["step"]
 
 
 def test_bench_world_mismatch_is_an_error():

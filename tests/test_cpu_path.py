@@ -162,3 +162,37 @@ def test_host_data_needs_no_gpu(enf, monkeypatch):
     Yt, Lt = enf.with_logabsdet_jacobian(f, torch.from_numpy(X))
     assert np.array_equal(Y, Y2) and np.array_equal(L, L2)
     assert isinstance(Yt, torch.Tensor) and not Yt.is_cuda and np.array_equal(Yt.numpy(), Y)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_scaleshift_length1_a_ladj_counts_once(enf, dtype):
+    """ScaleShiftTrafo([a], [b]) on D = 4 rows: ladj = sum(log.(abs.(f.a))) over a's own length, i.e.
+    log|a| once per sample (src/scale_shift_trafo.jl:22; enf_layer.k = 1), not D log|a|; a length-D a
+    keeps the sum over its D entries. Values computed by hand."""
+    rng = np.random.default_rng(4)
+    X = np.asfortranarray(rng.standard_normal((4, 7)).astype(dtype))
+    f1 = enf.ScaleShiftTrafo(np.array([-2.5], dtype), np.array([0.25], dtype))
+    Y, L = enf.with_logabsdet_jacobian(f1, X)
+    assert np.allclose(Y, -2.5 * X.astype(np.float64) + 0.25, rtol=1e-6, atol=1e-6)
+    assert np.allclose(np.asarray(L).reshape(-1), np.log(2.5), rtol=1e-6)
+    a = np.array([0.5, -2.0, 3.0, 1.5], dtype)
+    fD = enf.ScaleShiftTrafo(a, np.zeros(4, dtype))
+    _, LD = enf.with_logabsdet_jacobian(fD, X)
+    assert np.allclose(np.asarray(LD).reshape(-1), np.log(np.abs(a.astype(np.float64))).sum(), rtol=1e-6)
+    assert f1._k() == 1 and fD._k() == 0
+
+
+def test_capi_scaleshift_k_validated(enf):
+    """enf_layer.k of a ScaleShift layer is 0 (length-D a) or 1 (length-1 a); anything else is refused."""
+    lib = enf._lib
+    a = np.array([2.0, 2.0]); b = np.zeros(2)
+    X = np.zeros((3, 2)); Y = np.zeros((3, 2)); L = np.zeros(3)
+    arr = (lib.Layer * 1)()
+    arr[0].op, arr[0].p[0], arr[0].p[1] = lib.OP_SCALESHIFT, a.ctypes.data, b.ctypes.data
+    for k, want in ((0, lib.ENF_OK), (1, lib.ENF_OK), (2, lib.ENF_ERR_INVALID), (-1, lib.ENF_ERR_INVALID)):
+        arr[0].k = k
+        rc = lib.lib().enf_flow_apply_cpu(lib.ENF_F64, 2, 3, X.ctypes.data, 2, Y.ctypes.data, 2, L.ctypes.data, 0,
+                                          arr, 1, 1)
+        assert rc == want, (k, rc)
+        if rc == lib.ENF_OK:
+            assert np.allclose(L, np.log(2.0) * (1 if k == 1 else 2))

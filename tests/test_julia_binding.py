@@ -216,3 +216,14 @@ def test_parser_sees_known_prototypes(sym):
     ret, params = protos[sym]
     assert ret == "enf_status"
     assert params[0] == "enf_dtype" and "const enf_layer*" in params
+
+
+def test_julia_loss_is_reduced_on_the_device():
+    """mvnormal_negll_trafo(::HipMatrix) (src/optimize_whitening.jl:7-15) calls enf_flow_negll (the device
+    reduction) and copies only the scalar back: no Array(Y) / Array(L) of the whole batch."""
+    src = open(JL).read()
+    m = re.search(r"function mvnormal_negll_trafo\(.*?\nend\n", src, flags=re.S)
+    assert m, "mvnormal_negll_trafo method not found"
+    body = m.group(0)
+    assert ":enf_flow_negll_workspace" in body and ":enf_flow_negll," in body
+    assert "_apply(" not in body and "Array(Y)" not in body and "Array(L)" not in body
