@@ -396,6 +396,12 @@ static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, cons
     // config 2: the compiled J o H program at D = 2 (ENF_NO_D2=1 in the diagnostics build: the interpreter)
     static const int no_d2 = ENF_KNOB("ENF_NO_D2", 0);
     if (!no_d2 && d2_program(a)) return launch_d2_program(a, LADJ, st, dev);
+    // the compiled fp64 (J o H)^n program at D = 32 / 64 (ENF_NO_SPECIALIZE=1: the interpreter)
+    static const int nospec = ENF_KNOB("ENF_NO_SPECIALIZE", 0);
+    if (!nospec && hj_program_pairs(a) > 0) {
+      hipError_t e = launch_hj64_program(a, LADJ, st, dev);
+      if (e != hipErrorNotSupported) return e;
+    }
   }
 #if ENF_DIAG
   if (a.D == 2) {  // C2 diagnostics: 1 = synthesized tile, 2 = also no stores, 4 = prologue only

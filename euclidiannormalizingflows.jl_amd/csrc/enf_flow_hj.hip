@@ -329,9 +329,9 @@ __device__ __forceinline__ float prod_tree(const float (&q)[R]) {
 // The dot and z of one pair, in place on the tile (x: the pair's input y on entry, z on exit).
 // In the reference's operation order: the reflection's output y - vh (vh'y), then (. - xi)/lambda as
 // fma(., 1/lambda, -xi/lambda) (the records' vh/lambda slot is not read).
-template <int D, int R, int U>
+template <int D, int R, int U, bool RL = true>
 __device__ __forceinline__ void hj_pair_z(float (&x)[U][R], const float* r, HJParams<R>& prm) {
-  prm.template load<HJ_IL, HJ_RR>(r);
+  if constexpr (RL) prm.template load<HJ_IL, HJ_RR>(r);
   float dot[U];
   hj_dots<D, R, U>(x, prm, dot);
 #pragma unroll
@@ -351,10 +351,62 @@ __device__ __forceinline__ void hj_pair_z(float (&x)[U][R], const float* r, HJPa
 // for the tile). AS selects the asinh form: 1 = the mask-first merge asinh2_mask / asinh2_pick (the
 // product), and in the diagnostics build only 3 = the same merge with its mask taken from the log2
 // (asinh2_merge), 2 = asinh2_med3 (z' = sqrt(K) z, enf_frag.h) and 0 = round 1's absolute-error form.
-template <int D, int R, int U, bool LADJ, int AS = 1>
+// The Johnson part of one pair (AS = 1 form) on ONE slab of the tile (VAR bit 1, diagnostics build):
+// the temporaries of one slab only, for a lower register count (occupancy 5).
+template <int R, bool LADJ>
+__device__ __forceinline__ float hj_johnson_slab(float (&x)[R], float& acc, uint32_t csign) {
+  float q[R], t[R];
+  uint32_t msel[R];
+#pragma unroll
+  for (int e = 0; e < R; ++e) q[e] = fmaf(x[e], x[e], 1.0f);
+#pragma unroll
+  for (int e = 0; e < R; ++e) msel[e] = asinh2_mask(q[e], csign);
+  if constexpr (R == 8) {
+    sqrt8(t, q);
+  } else {
+#pragma unroll
+    for (int e = 0; e < R; ++e) t[e] = hw_sqrt(q[e]);
+  }
+  const float pr = prod_tree<R>(q);
+#pragma unroll
+  for (int e = 0; e < R; ++e) q[e] = asinh2_small(x[e], q[e]);
+#pragma unroll
+  for (int e = 0; e < R; ++e) t[e] = fabsf(x[e]) + t[e];
+  if constexpr (R == 8) {
+    log2_8_inplace(t);
+  } else {
+#pragma unroll
+    for (int e = 0; e < R; ++e) t[e] = hw_log2(t[e]);
+  }
+  if (LADJ) acc = fmaf(-0.5f, hw_log2(pr), acc);
+#pragma unroll
+  for (int e = 0; e < R; ++e) x[e] = asinh2_pick(q[e], t[e], msel[e]);
+  return pr;
+}
+
+// VAR (diagnostics build only): bit 1 = the Johnson part slab by slab (hj_johnson_slab); bit 2 = no
+// per-pair record reads (every pair uses the records loaded before the pair loop: WRONG results, a
+// timing probe of the LDS record traffic).
+template <int D, int R, int U, bool LADJ, int AS = 1, int VAR = 0>
 __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U], const float*& r, HJParams<R>& prm,
                                               uint32_t csign) {
-  hj_pair_z<D, R, U>(x, r, prm);
+  constexpr bool RL = !(VAR & 2);
+  hj_pair_z<D, R, U, RL>(x, r, prm);
+  if constexpr ((VAR & 1) && AS == 1) {
+    float pr1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) pr1[u] = hj_johnson_slab<R, LADJ>(x[u], acc[u], csign);
+    r += kHjW * D;
+    if constexpr (RL) prm.template load<0, HJ_IL>(r);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_DP, e), prm.m(HJ_GP, e));
+    float m1 = pr1[0];
+#pragma unroll
+    for (int u = 1; u < U; ++u) m1 = fmaxf(m1, pr1[u]);
+    return m1;
+  }
   // stage by stage over the whole tile (U*R independent chains per stage)
   float q[U][R], t[U][R], pr[U];
   uint32_t msel[U][R];  // AS == 1: the select mask of asinh2_pick, from q (before the transcendentals)
@@ -416,7 +468,7 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
         x[u][e] = copysignf(t[u][e], x[u][e]);
     }
   r += kHjW * D;
-  prm.template load<0, HJ_IL>(r);
+  if constexpr (RL) prm.template load<0, HJ_IL>(r);
   // y_p = gamma_p + delta'_p L_p: the next record's {delta', gamma} slots (record n: the output's)
 #pragma unroll
   for (int u = 0; u < U; ++u)
@@ -452,7 +504,7 @@ __device__ __forceinline__ void hj_pair_exact(float (&x)[U][R], float (&acc)[U],
     for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_DP, e), prm.m(HJ_GP, e));
 }
 
-template <int D, int R, int U, int LM, int AS = 1>
+template <int D, int R, int U, int LM, int AS = 1, int VAR = 0>
 struct HJBody {
   const HJArgs& a;
   const float* rec;  // this lane's record group
@@ -469,10 +521,11 @@ struct HJBody {
     const float* r = rec;
     HJParams<R> prm;
     prm.template load<0, HJ_IL>(r);
+    if constexpr ((VAR & 2) != 0) prm.template load<HJ_IL, HJ_RR>(r);
     const uint32_t csign = sign_mask_vgpr();
     // branch-free pair loop; a tile with a product overflow (|z| large, Inf, NaN) is redone below
     float m = 0.f;
-    for (int p = 0; p < n; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ, AS>(x, acc, r, prm, csign));
+    for (int p = 0; p < n; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ, AS, VAR>(x, acc, r, prm, csign));
     // column-uniform: the exact form's dot products read every lane of a column (DPP)
     m = group_max<HJLay<D, R, U>::G>(m);
     if (__builtin_expect(!(m <= FLT_MAX), 0)) {
@@ -528,7 +581,7 @@ __device__ __forceinline__ void hj_stream(const HJArgs& a, Body& body) {
   }
 }
 
-template <int D, int R, int U, int LM, int OCC, int DBG, int AS = 1>
+template <int D, int R, int U, int LM, int OCC, int DBG, int AS = 1, int VAR = 0>
 __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   const int n = a.n;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -538,7 +591,7 @@ __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   float* rec = reinterpret_cast<float*>(smem + kHjHeader);
   build_hj_program<D, R, AS>(a, n, rec, scr, ctotp);
   constexpr int G = HJLay<D, R, U>::G;
-  HJBody<D, R, U, LM, AS> body{a, rec + ((threadIdx.x & 63) % G) * kHjW * R, *ctotp, stage, n};
+  HJBody<D, R, U, LM, AS, VAR> body{a, rec + ((threadIdx.x & 63) % G) * kHjW * R, *ctotp, stage, n};
   hj_stream<D, R, U, LM, DBG>(a, body);
 }
 
@@ -551,14 +604,14 @@ int hj_program_pairs(const FlowArgs& a) {
   return a.nsteps / 2;
 }
 
-template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, int AS = 1>
+template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, int AS = 1, int VAR = 0>
 static hipError_t launch_hj(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
   const size_t lds = hj_lds_bytes(D, h.n);
-  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, AS>);
+  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, AS, VAR>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)HJLay<D, R, U>::TC * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, AS>), dim3((unsigned)blocks), dim3(256), lds, st, h);
+  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, AS, VAR>), dim3((unsigned)blocks), dim3(256), lds, st, h);
   return hipGetLastError();
 }
 
@@ -580,6 +633,13 @@ static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, c
 #if ENF_DIAG
     if constexpr (LM == 1) {
       static const int as = ENF_KNOB("ENF_HJ_ASINH", 1);
+      // ENF_HJ_VAR: 1 = Johnson part slab by slab at occupancy 5, 3 = the same without per-pair record
+      // reads, 2 = no per-pair record reads (timing probes; 2 and 3 give wrong results)
+      static const int var = ENF_KNOB("ENF_HJ_VAR", 0);
+      if (dbg == 0 && var == 1) return launch_hj<32, 8, 2, 1, 5, 0, 1, 1>(a, st, dev);
+      if (dbg == 0 && var == 2) return launch_hj<32, 8, 2, 1, 4, 0, 1, 2>(a, st, dev);
+      if (dbg == 0 && var == 3) return launch_hj<32, 8, 2, 1, 5, 0, 1, 3>(a, st, dev);
+      if (dbg == 2 && var == 1) return launch_hj<32, 8, 2, 1, 5, 2, 1, 1>(a, st, dev);
       if (dbg == 1) return launch_hj_as<1, 1>(as, a, st, dev);
       if (dbg == 2) return launch_hj_as<2, 1>(as, a, st, dev);
       if (dbg == 8) return launch_hj_as<8, 1>(as, a, st, dev);

@@ -190,3 +190,66 @@ def test_mvnormal_negll_trafo_device_reduction(enf, gpu, oracle, dtype, D):
     if D <= 256:
         ng, _ = enf.mvnormal_negll_trafograd(f, colmajor_cuda(X))
         assert abs(got - ng) <= tol * (abs(ref) + 1)
+
+
+def _hj64_layers(rng, D, pairs):
+    layers = []
+    for _ in range(pairs):
+        layers += [(5, rand_params(rng, 5, D, np.float64)), (3, rand_params(rng, 3, D, np.float64))]
+    return layers
+
+
+@pytest.mark.parametrize("D", [32, 64])
+@pytest.mark.parametrize("pairs", [1, 2, 4, 8, 9])
+def test_hj64_program_vs_oracle(enf, gpu, oracle, D, pairs):
+    """The compiled fp64 (J∘H)^n program (enf_flow_hj64.hip; n <= 8, n = 9 runs on the interpreter):
+    forward + ladj at 1e-12 against the oracle (and the x87 evaluation), ragged tail, multi-tile waves,
+    the plain call f(X) equal to the Y of the ladj call."""
+    rng = np.random.default_rng(7000 + 100 * D + pairs)
+    layers = _hj64_layers(rng, D, pairs)
+    N = 100_003
+    X = np.asfortranarray(rng.standard_normal((D, N)))
+    f = make_flow(enf, layers)
+    Y, L = enf.with_logabsdet_jacobian(f, colmajor_cuda(X))
+    check_vs_oracle(oracle, layers, X, to_np(Y), to_np(L), np.float64, what=f"hj64 D{D} n{pairs}")
+    assert np.array_equal(to_np(f(colmajor_cuda(X))), to_np(Y))
+
+
+def test_hj64_program_edge_values_accumulate_inplace(enf, gpu, oracle):
+    """fp64 program: huge (>= 2^26), infinite and NaN entries follow the reference (asinh64_tab's whole
+    range, logprod64_tab's Inf / NaN); accumulate_ladj and Y aliasing X through the raw C ABI."""
+    import torch
+
+    from parity import col_err, ladj_err
+    from test_gpu_parity import _raw_apply
+
+    rng = np.random.default_rng(64)
+    D, N = 32, 20_001
+    layers = _hj64_layers(rng, D, 4)
+    X = rng.standard_normal((D, N))
+    X[3, 7] = 3e30
+    X[0, 100] = -1e25
+    X[5, 101] = np.inf
+    X[D - 1, 2000] = np.nan
+    X[:, 4095] = 1e8
+    X = np.asfortranarray(X)
+    Yr, Lr = oracle.flow_apply(layers, X)
+    Y, L = enf.with_logabsdet_jacobian(make_flow(enf, layers), colmajor_cuda(X))
+    Y, L = to_np(Y), to_np(L).reshape(-1)
+    assert np.array_equal(np.isnan(Y), np.isnan(Yr)) and np.array_equal(np.isnan(L), np.isnan(Lr))
+    assert np.array_equal(np.isinf(Y), np.isinf(Yr)) and np.array_equal(np.isinf(L), np.isinf(Lr))
+    fin = np.isfinite(Yr)
+    assert col_err(np.where(fin, Y, 0), np.where(fin, Yr, 0)) < 1e-12
+    finl = np.isfinite(Lr)
+    assert ladj_err(L[finl], Lr[finl]) < 1e-12
+    good = np.setdiff1d(np.arange(N), [7, 100, 101, 2000, 4095])
+    check_vs_oracle(oracle, layers, np.asfortranarray(X[:, good]), Y[:, good], L[good], np.float64, what="hj64 edge")
+    dev = [[torch.from_numpy(np.ascontiguousarray(p)).cuda() for p in ps] for _, ps in layers]
+    lt = [(op, 1 if op == 5 else 0, [t.data_ptr() for t in ts]) for (op, _), ts in zip(layers, dev)]
+    buf = colmajor_cuda(X).t().contiguous()
+    L0 = torch.full((N,), 3.25, dtype=torch.float64, device="cuda")
+    assert _raw_apply(enf, 1, D, N, buf.data_ptr(), D, buf.data_ptr(), D, L0.data_ptr(), 1, lt) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(buf.cpu().numpy().T, Y, equal_nan=True)
+    Lb = L0.cpu().numpy() - 3.25
+    assert np.all(np.abs(Lb[finl] - L[finl]) <= 1e-13 * (np.abs(L[finl]) + 3.25))
