@@ -86,7 +86,8 @@ __device__ __forceinline__ void d2_tile(const D2Args& a, const D2Prog& P, const 
     const int64_t c = col0 + (int64_t)u * 64 + lane;
     old[u] = (LM == 2 && (!TAIL || c < a.N)) ? a.ladj[c] : 0.0;
   }
-  double lad[U];
+  double lad[U], z[U][2];
+  bool far = false;  // some |z| >= 2^26, Inf or NaN in this lane
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     // HouseholderTrafo: x - vh (vh'x)
@@ -95,13 +96,28 @@ __device__ __forceinline__ void d2_tile(const D2Args& a, const D2Prog& P, const 
     const double x0 = fma(-dot, P.vh0, x[u][0]);
     const double x1 = fma(-dot, P.vh1, x[u][1]);
     // JohnsonTrafo
-    const double z0 = (x0 - P.xi0) * P.il0;
-    const double z1 = (x1 - P.xi1) * P.il1;
-    x[u][0] = fma(P.d0, asinh64_tab(z0, tab), P.g0);
-    x[u][1] = fma(P.d1, asinh64_tab(z1, tab), P.g1);
-    if (LM > 0) {
-      const double q[2] = {fma(z0, z0, 1.0), fma(z1, z1, 1.0)};
-      lad[u] = 0.0 - 0.5 * logprod64_tab<2>(q, tab);
+    z[u][0] = (x0 - P.xi0) * P.il0;
+    z[u][1] = (x1 - P.xi1) * P.il1;
+    far = far || !asinh64_fin_ok(z[u][0]) || !asinh64_fin_ok(z[u][1]);
+  }
+  if (!__any(far)) {
+    // the whole wave in |z| < 2^26: the range-free asinh and the plain log of the q product (bit-identical
+    // to asinh64_tab / logprod64_tab there; no product of two q < 2^53 overflows)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      x[u][0] = fma(P.d0, asinh64_tab_fin(z[u][0], tab), P.g0);
+      x[u][1] = fma(P.d1, asinh64_tab_fin(z[u][1], tab), P.g1);
+      if (LM > 0) lad[u] = 0.0 - 0.5 * log64_tab(fma(z[u][0], z[u][0], 1.0) * fma(z[u][1], z[u][1], 1.0), 0, tab);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      x[u][0] = fma(P.d0, asinh64_tab(z[u][0], tab), P.g0);
+      x[u][1] = fma(P.d1, asinh64_tab(z[u][1], tab), P.g1);
+      if (LM > 0) {
+        const double q[2] = {fma(z[u][0], z[u][0], 1.0), fma(z[u][1], z[u][1], 1.0)};
+        lad[u] = 0.0 - 0.5 * logprod64_tab<2>(q, tab);
+      }
     }
   }
 #pragma unroll

@@ -230,6 +230,7 @@ __device__ __forceinline__ void h64_pair(double (&x)[U][8], double (&acc)[U], co
   h64_param(r + H64_XI * 8, pxi);
   h64_param(r + H64_IL * 8, pil);
   double q[U][8];
+  bool far = false;  // some |z| >= 2^26, Inf or NaN in this lane
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -237,17 +238,35 @@ __device__ __forceinline__ void h64_pair(double (&x)[U][8], double (&acc)[U], co
       const double z = (x[u][e] - pxi[e]) * pil[e];
       x[u][e] = z;
       q[u][e] = fma(z, z, 1.0);
+      far = far || !asinh64_fin_ok(z);
     }
   double pd[8], pg[8];
   h64_param(r + H64_DL * 8, pd);
   h64_param(r + H64_GM * 8, pg);
+  if (!__any(far)) {
+    // the whole wave in |z| < 2^26: the range-free asinh and the plain table log of the q product (the same
+    // values as asinh64_tab / logprod64_tab there: the product of 8 q < 2^53 stays below 2^424)
 #pragma unroll
-  for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) x[u][e] = fma(pd[e], asinh64_tab(x[u][e], tab), pg[e]);
-  if (LADJ)
+      for (int e = 0; e < 8; ++e) x[u][e] = fma(pd[e], asinh64_tab_fin(x[u][e], tab), pg[e]);
+    if (LADJ)
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc[u] -= 0.5 * logprod64_tab<8>(q[u], tab);
+      for (int u = 0; u < U; ++u) {
+        double p = q[u][0];
+#pragma unroll
+        for (int e = 1; e < 8; ++e) p *= q[u][e];
+        acc[u] -= 0.5 * log64_tab(p, 0, tab);
+      }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[u][e] = fma(pd[e], asinh64_tab(x[u][e], tab), pg[e]);
+    if (LADJ)
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] -= 0.5 * logprod64_tab<8>(q[u], tab);
+  }
 }
 
 template <int D, int U, int LM, bool TAIL>

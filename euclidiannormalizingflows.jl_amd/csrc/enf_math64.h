@@ -166,6 +166,27 @@ __device__ __forceinline__ double asinh64_tab(double x, const double* __restrict
   return __builtin_copysign(r, x);
 }
 
+// asinh64_tab for |x| < 2^26 and finite only (no range selects): the fused kernels take it for a wave whose
+// arguments are all in that range (a wave-uniform vote), asinh64_tab otherwise. Same operations and
+// roundings as asinh64_tab's a < 2^26 branch, so the same results there.
+__device__ __forceinline__ double asinh64_tab_fin(double x, const double* __restrict__ tab) {
+  const double a = __builtin_fabs(x);
+  const double q = fma(a, a, 1.0);
+  const double y = __builtin_amdgcn_rsq(q);
+  double g = q * y, h = 0.5 * y;
+  const double rr = fma(-g, h, 0.5);
+  g = fma(g, rr, g);
+  h = fma(h, rr, h);
+  const double eq = fma(a, a, 1.0 - q);
+  const double corr = (fma(-g, g, q) + eq) * h;
+  const double u0 = a + g;
+  const double c0 = (a - (u0 - g)) + corr;
+  const double cu = c0 * ((g - a) + corr);
+  return __builtin_copysign(log64_tab(u0, 0, tab) + cu, x);
+}
+// true when asinh64_tab_fin applies to x (|x| < 2^26; false for Inf and NaN)
+__device__ __forceinline__ bool asinh64_fin_ok(double x) { return __builtin_fabs(x) < 67108864.0; }
+
 // log(q_1 q_2 ... q_n) for n values q_i >= 1 (a fragment column segment's 1 + z^2): the exponents
 // are summed as integers and the mantissas multiplied (< 2^n), so no product overflows; +Inf if a
 // factor is +Inf, NaN if one is NaN (the reference's log(1/sqrt(Inf)) = -Inf, NaN propagation).

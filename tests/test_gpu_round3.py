@@ -18,7 +18,7 @@ from parity import check_vs_oracle, colmajor_cuda, make_flow, rand_params, to_np
 pytestmark = pytest.mark.gpu
 
 
-def _fd_check(oracle, layers, X, g, D, idx, rel=1e-5):
+def _fd_check(oracle, layers, X, g, D, idx, rel=1e-5, floor=1e-3):
     from test_gpu_train import flat, oracle_negll, unflat
 
     th0 = flat(layers, D)
@@ -30,7 +30,7 @@ def _fd_check(oracle, layers, X, g, D, idx, rel=1e-5):
         tp[i] += h
         tm[i] -= h
         fd = (oracle_negll(oracle, unflat(layers, tp, D), X) - oracle_negll(oracle, unflat(layers, tm, D), X)) / (2 * h)
-        assert abs(g[i] - fd) <= rel * (abs(fd) + 1e-3 * scale), (i, g[i], fd)
+        assert abs(g[i] - fd) <= rel * (abs(fd) + floor * scale), (i, g[i], fd)
 
 
 @pytest.mark.parametrize("D", [100, 128])
@@ -53,20 +53,25 @@ def test_negll_grad_large_D_finite_differences(enf, gpu, oracle, D):
     _fd_check(oracle, layers, X, g, D, idx)
 
 
-def test_negll_grad_D256_fp32_vs_fp64(enf, gpu):
-    """fp32 D = 256 (one column per wave instruction) against the fp64 kernel on the same inputs."""
+def test_negll_grad_D256_fp32(enf, gpu, oracle):
+    """fp32 at D = 256 (one column per wave instruction; fp64 stops at 128): the loss against the oracle's
+    fp64 loss of the same fp32 inputs, the gradient against its central differences on 64 coordinates
+    (fp32 accuracy: 1e-3 of the gradient's scale)."""
+    from test_gpu_train import oracle_negll
+
     rng = np.random.default_rng(256)
     D = 256
-    layers = [(5, rand_params(rng, 5, D, np.float64)), (3, rand_params(rng, 3, D, np.float64)),
-              (0, rand_params(rng, 0, D, np.float64)), (4, rand_params(rng, 4, D, np.float64))]
-    X = np.asfortranarray(0.8 * rng.standard_normal((D, 2049)))
-    n64, g64 = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X))
-    l32 = [(op, [np.asarray(p, np.float32) for p in ps]) for op, ps in layers]
-    n32, g32 = enf.mvnormal_negll_trafograd(make_flow(enf, l32), colmajor_cuda(X.astype(np.float32)))
-    a = np.concatenate([np.asarray(x, np.float64).reshape(-1) for per in g64 for x in per])
-    b = np.concatenate([np.asarray(x, np.float64).reshape(-1) for per in g32 for x in per])
-    assert abs(n32 - n64) <= 1e-4 * (abs(n64) + 1)
-    assert np.abs(a - b).max() <= 1e-3 * np.abs(a).max()
+    layers = [(5, rand_params(rng, 5, D, np.float32)), (3, rand_params(rng, 3, D, np.float32)),
+              (0, rand_params(rng, 0, D, np.float32)), (4, rand_params(rng, 4, D, np.float32))]
+    X = np.asfortranarray((0.8 * rng.standard_normal((D, 2049))).astype(np.float32))
+    n32, g32 = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X))
+    l64 = [(op, [np.asarray(p, np.float64) for p in ps]) for op, ps in layers]
+    X64 = np.asfortranarray(X.astype(np.float64))
+    ref = oracle_negll(oracle, l64, X64)
+    assert abs(n32 - ref) <= 1e-4 * (abs(ref) + 1)
+    g = np.concatenate([np.asarray(x, np.float64).reshape(-1, order="F") for per in g32 for x in per])
+    idx = [v * D + int(r) for v in range(g.size // D) for r in rng.choice(D, 6, replace=False)]
+    _fd_check(oracle, l64, X64, g, D, idx, rel=1e-3, floor=0.1)
 
 
 @pytest.mark.parametrize("D", [100, 128])
