@@ -142,26 +142,42 @@ __device__ __forceinline__ void d2_tile(const D2Args& a, const D2Prog& P, const 
   }
 }
 
-template <int U, int LM, int DBG>
+// P: tiles in flight per wave (the current one and P - 1 prefetched): at N = 1e6 a wave has ~4 tiles, so
+// with one tile of lookahead only ~2 KiB per wave is in flight, far below what the HBM latency needs.
+// PB (diagnostics A/B): the program constants computed once per block by one wave (wave b % 4 of block b, so
+// the four SIMDs share the work) and broadcast through LDS after an LDS-only barrier, and one log table per
+// block, instead of every wave computing its own.
+template <int U, int LM, int DBG, int P = 2, bool PB = false>
 __global__ __launch_bounds__(256, U == 1 ? 8 : 4) void flow_d2_kernel(D2Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  double* tab = reinterpret_cast<double*>(smem) + wave * kD2Tab;
+  double* tab = reinterpret_cast<double*>(smem) + (PB ? 0 : wave * kD2Tab);
+  double* progl = reinterpret_cast<double*>(smem) + kD2Tab;  // PB: the 11 broadcast constants
   constexpr int64_t CT = 64 * U;
   const int64_t ntiles_full = a.N / CT;
   const int64_t wave_id = (int64_t)blockIdx.x * 4 + wave;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
-  double xa[U][2], xb[U][2];
-  // the first tile's loads go out before the prologue, which then overlaps their latency
+  double xs[P][U][2];
+  // the first P tiles' loads go out before the prologue, which then overlaps their latency (a tile past the
+  // last full one re-reads the wave's first tile instead: every load is issued, so the vmcnt waits stay
+  // static)
   const bool full0 = wave_id < ntiles_full;
-  if (full0) d2_load<U, false, DBG>(a, wave_id * CT, lane, xa);
-  // the wave's copy of the log table
-  if (lane < kLogTabN) {
-    tab[3 * lane] = kLogTab[3 * lane];
-    tab[3 * lane + 1] = kLogTab[3 * lane + 1];
-    tab[3 * lane + 2] = kLogTab[3 * lane + 2];
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const int64_t tk = wave_id + k * nwaves;
+    if (full0) d2_load<U, false, DBG>(a, (tk < ntiles_full ? tk : wave_id) * CT, lane, xs[k]);
   }
+  // the wave's (PB: the block's) copy of the log table
+  if (!PB || wave == 1) {
+    if (lane < kLogTabN) {
+      tab[3 * lane] = kLogTab[3 * lane];
+      tab[3 * lane + 1] = kLogTab[3 * lane + 1];
+      tab[3 * lane + 2] = kLogTab[3 * lane + 2];
+    }
+  }
+  D2Prog P_;
+  if (!PB || wave == (int)(blockIdx.x & 3)) {
   // parameters (build_program / param_values in enf_steps.h, same operations and ocml functions, so the
   // same values). A VALU instruction costs the whole wave whatever its active lanes, so the four logs and
   // the three divisions run as one log and one division over lanes: lanes 0, 1 take log|delta_d| and
@@ -176,41 +192,52 @@ __global__ __launch_bounds__(256, U == 1 ? 8 : 4) void flow_d2_kernel(D2Args a) 
   pc += __shfl_xor(pc, 1);
   const double hscale = sqrt(d2_readlane(qt, 2));
   const double vh = vr * hscale;
-  D2Prog P;
-  P.vh0 = d2_readlane(vh, 0);
-  P.vh1 = d2_readlane(vh, 1);
-  P.il0 = d2_readlane(qt, 0);
-  P.il1 = d2_readlane(qt, 1);
-  P.ctot = (0.0 + 0.0) + d2_readlane(pc, 0);  // the step constants summed in step order (H: 0)
-  P.g0 = a.g[0];
-  P.g1 = a.g[1];
-  P.d0 = a.d[0];
-  P.d1 = a.d[1];
-  P.xi0 = a.xi[0];
-  P.xi1 = a.xi[1];
+  P_.vh0 = d2_readlane(vh, 0);
+  P_.vh1 = d2_readlane(vh, 1);
+  P_.il0 = d2_readlane(qt, 0);
+  P_.il1 = d2_readlane(qt, 1);
+  P_.ctot = (0.0 + 0.0) + d2_readlane(pc, 0);  // the step constants summed in step order (H: 0)
+  P_.g0 = a.g[0];
+  P_.g1 = a.g[1];
+  P_.d0 = a.d[0];
+  P_.d1 = a.d[1];
+  P_.xi0 = a.xi[0];
+  P_.xi1 = a.xi[1];
+  if (PB && lane == 0) {
+    progl[0] = P_.vh0; progl[1] = P_.vh1; progl[2] = P_.il0; progl[3] = P_.il1; progl[4] = P_.ctot;
+    progl[5] = P_.g0; progl[6] = P_.g1; progl[7] = P_.d0; progl[8] = P_.d1; progl[9] = P_.xi0; progl[10] = P_.xi1;
+  }
+  }
+  if constexpr (PB) {  // LDS-only barrier: the prefetched tiles stay in flight
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    P_.vh0 = progl[0]; P_.vh1 = progl[1]; P_.il0 = progl[2]; P_.il1 = progl[3]; P_.ctot = progl[4];
+    P_.g0 = progl[5]; P_.g1 = progl[6]; P_.d0 = progl[7]; P_.d1 = progl[8]; P_.xi0 = progl[9]; P_.xi1 = progl[10];
+  }
   // the table writes are complete before any lane of this wave reads it (LDS is in order per wave)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-  // persistent loop with the next tile's loads in flight (as frag_stream)
+  // persistent loop, P tiles in flight: compute buffer k, then refill it with the tile P strides ahead
   if (full0) {
-    int64_t t = wave_id, t1 = t + nwaves;
-    d2_load<U, false, DBG>(a, (t1 < ntiles_full ? t1 : t) * CT, lane, xb);
-    d2_tile<U, LM, false, DBG>(a, P, tab, t * CT, lane, xa);
-    while (t1 < ntiles_full) {
-      const int64_t t2 = t1 + nwaves;
-      d2_load<U, false, DBG>(a, (t2 < ntiles_full ? t2 : t1) * CT, lane, xa);
-      d2_tile<U, LM, false, DBG>(a, P, tab, t1 * CT, lane, xb);
-      if (t2 >= ntiles_full) break;
-      const int64_t t3 = t2 + nwaves;
-      d2_load<U, false, DBG>(a, (t3 < ntiles_full ? t3 : t2) * CT, lane, xb);
-      d2_tile<U, LM, false, DBG>(a, P, tab, t2 * CT, lane, xa);
-      t1 = t3;
+    int64_t t = wave_id;
+    for (;;) {
+      bool done = false;
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        if (!done) {
+          d2_tile<U, LM, false, DBG>(a, P_, tab, t * CT, lane, xs[k]);
+          const int64_t tn = t + P * nwaves;
+          d2_load<U, false, DBG>(a, (tn < ntiles_full ? tn : wave_id) * CT, lane, xs[k]);
+          t += nwaves;
+          done = t >= ntiles_full;
+        }
+      }
+      if (done) break;
     }
   }
   if (ntiles_full * CT < a.N && wave_id == ntiles_full % nwaves) {
     const int64_t c0 = ntiles_full * CT;
-    d2_load<U, true, 0>(a, c0, lane, xa);
-    d2_tile<U, LM, true, 0>(a, P, tab, c0, lane, xa);
+    d2_load<U, true, 0>(a, c0, lane, xs[0]);
+    d2_tile<U, LM, true, 0>(a, P_, tab, c0, lane, xs[0]);
   }
 }
 
@@ -220,10 +247,10 @@ bool d2_program(const FlowArgs& a) {
   return a.frag && a.D == 2 && a.nsteps == 2 && a.steps[0].op == OP_HOUSEHOLDER && a.steps[1].op == OP_JOHNSON;
 }
 
-template <int U, int LM, int DBG>
+template <int U, int LM, int DBG, int P = 2, bool PB = false>
 static hipError_t launch_d2_u(const D2Args& h, hipStream_t st, const DeviceInfo& dev) {
-  const size_t lds = 4 * kD2Tab * sizeof(double);
-  const void* k = reinterpret_cast<const void*>(&flow_d2_kernel<U, LM, DBG>);
+  const size_t lds = 4 * kD2Tab * sizeof(double) + 16 * sizeof(double);
+  const void* k = reinterpret_cast<const void*>(&flow_d2_kernel<U, LM, DBG, P, PB>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)64 * U * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
@@ -233,7 +260,7 @@ static hipError_t launch_d2_u(const D2Args& h, hipStream_t st, const DeviceInfo&
   static const int bpc_env = ENF_KNOB("ENF_BLOCKS_PER_CU", 0);
   const int64_t cap = (int64_t)dev.num_cu * 2;
   if (bpc_env == 0 && blocks > cap) blocks = cap;
-  hipLaunchKernelGGL((flow_d2_kernel<U, LM, DBG>), dim3((unsigned)blocks), dim3(256), lds, st, h);
+  hipLaunchKernelGGL((flow_d2_kernel<U, LM, DBG, P, PB>), dim3((unsigned)blocks), dim3(256), lds, st, h);
   return hipGetLastError();
 }
 
@@ -244,12 +271,22 @@ static hipError_t launch_d2_lm(const D2Args& h, hipStream_t st, const DeviceInfo
   // synthesized tile / also no stores
   static const int u = ENF_KNOB("ENF_D2_U", 2);
   static const int dbg = ENF_KNOB("ENF_D2_DBG", 0);
+  // ENF_D2_P: tiles in flight per wave
+  static const int pf = ENF_KNOB("ENF_D2_P", 4);
+  static const int pb = ENF_KNOB("ENF_D2_PB", 0);
+  if (dbg == 0 && u == 2 && pb == 1 && pf == 4) return launch_d2_u<2, LM, 0, 4, true>(h, st, dev);
+  if (dbg == 0 && u == 2 && pb == 1 && pf == 2) return launch_d2_u<2, LM, 0, 2, true>(h, st, dev);
+  if (dbg == 2 && pb == 1) return launch_d2_u<2, LM, 2, 4, true>(h, st, dev);
+  if (dbg == 0 && u == 2 && pf == 3) return launch_d2_u<2, LM, 0, 3>(h, st, dev);
+  if (dbg == 0 && u == 2 && pf == 2) return launch_d2_u<2, LM, 0, 2>(h, st, dev);
+  if (dbg == 0 && u == 1 && pf == 4) return launch_d2_u<1, LM, 0, 4>(h, st, dev);
   if (dbg == 1) return launch_d2_u<2, LM, 1>(h, st, dev);
   if (dbg == 2) return launch_d2_u<2, LM, 2>(h, st, dev);
   if (u == 1) return launch_d2_u<1, LM, 0>(h, st, dev);
 #endif
-  // U = 2: 103 VGPRs (4 waves per SIMD); U = 4 interleaves 8 asinh chains and spills at 128 VGPRs
-  return launch_d2_u<2, LM, 0>(h, st, dev);
+  // U = 2, 4 tiles in flight per wave (85 VGPRs; P = 4 vs 2: 11.70 vs 12.00 us on one box,
+  // profiles/r03_c2_variants.txt); U = 4 interleaves 8 asinh chains and spilled at 128 VGPRs (round 2)
+  return launch_d2_u<2, LM, 0, 4>(h, st, dev);
 }
 
 hipError_t launch_d2_program(const FlowArgs& a, int lm, hipStream_t st, const DeviceInfo& dev) {

@@ -4,4 +4,6 @@ mkdir -p gpurun_out/r3mb
 : > gpurun_out/r3mb/mb20.txt
 for st in max-ilp iterative-ilp max-memory-clause; do echo "== $st" >> gpurun_out/r3mb/mb20.txt; timeout -k 5 60 ./tools/microbench20_$st 4 >> gpurun_out/r3mb/mb20.txt 2>&1 || exit 1; done
 timeout -k 5 60 ./tools/microbench17 4 >> gpurun_out/r3mb/mb20.txt 2>&1 || exit 1
-timeout -k 5 60 ./tools/microbench21 4 > gpurun_out/r3mb/mb21.txt 2>&1; rc=$?; cat gpurun_out/r3mb/mb20.txt gpurun_out/r3mb/mb21.txt; exit $rc
+timeout -k 5 60 ./tools/microbench21 4 > gpurun_out/r3mb/mb21.txt 2>&1 || exit 1
+cat gpurun_out/r3mb/mb20.txt gpurun_out/r3mb/mb21.txt
+bash tools/r3_c2ab.sh
