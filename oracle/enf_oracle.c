@@ -193,10 +193,13 @@
     free(lt);                                                                                      \
     return rc;                                                                                     \
   }                                                                                                \
-  /* Same computation, column blocks spread over nthreads OpenMP threads (CPU baseline #2). */    \
+  /* Same computation, column blocks spread over nthreads OpenMP threads (CPU baseline #2). Blocks */ \
+  /* of 256 columns keep every temporary below glibc's mmap threshold (128 KiB at D = 32 fp32), so */ \
+  /* the per-block malloc/free stays in the threads' arenas instead of mmap/munmap + page zeroing   */ \
+  /* serialised on the address-space lock (4096-column blocks scaled 10x on 256 threads).          */ \
   int or_flow_apply_mt_##S(int64_t D, int64_t N, const T* X, int64_t ldx, T* Y, int64_t ldy,       \
                            T* ladj, const oracle_layer* layers, int32_t nlayers, int nthreads) {   \
-    const int64_t B = 4096;                                                                        \
+    const int64_t B = 256;                                                                         \
     const int64_t nb = (N + B - 1) / B;                                                            \
     int rc = 0;                                                                                    \
     _Pragma("omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(|: rc)")        \
