@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -301,25 +303,67 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
 // ------------------------------------------------------------------- host-resident batches ----
 namespace {
 
-// Page-lock a host range for the duration of a call unless it already is (hipHostRegister makes
-// the async copies true DMA and lets them overlap the kernels).
-struct HostPin {
-  void* p = nullptr;
-  bool mine = false;
-  hipError_t pin(void* ptr, size_t bytes) {
+// Page-lock the host arrays of a call for its duration (hipHostRegister makes the async copies true
+// DMA and lets them overlap the kernels). The arrays are registered as DISJOINT page-aligned ranges:
+// X, Y and ladj are separate allocations that often share a boundary page (numpy arrays in the heap
+// are not page-aligned), and registering each one on its own locked that page twice, once per
+// overlapping registration. Each page is now locked at most once: the page ranges of the arrays are
+// merged where they overlap or touch, and every merged range is one hipHostRegister (every page of
+// it holds bytes of one of the arrays, so it is mapped). An array the caller has registered already
+// is left alone (its copies are DMA anyway).
+struct HostPins {
+  std::vector<void*> mine;
+  struct R { uintptr_t lo, hi; };
+  std::vector<R> want;
+  static bool registered(const void* p) {
     hipPointerAttribute_t at;
     std::memset(&at, 0, sizeof at);
-    if (hipPointerGetAttributes(&at, ptr) == hipSuccess && at.type != hipMemoryTypeUnregistered) return hipSuccess;
+    const bool r = hipPointerGetAttributes(&at, p) == hipSuccess && at.type != hipMemoryTypeUnregistered;
     (void)hipGetLastError();  // clear the "not registered" status
-    hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
-    if (e == hipSuccess) {
-      p = ptr;
-      mine = true;
-    }
-    return e;
+    return r;
   }
-  ~HostPin() {
-    if (mine) (void)hipHostUnregister(p);
+  void add(const void* p, size_t bytes) {
+    if (!p || bytes == 0 || registered(p)) return;
+#if ENF_DIAG
+    // ENF_PIN_LEGACY=1 (diagnostics build, tools/pin_overlap_probe.py): round 2's registration, one
+    // hipHostRegister per array at its exact, unaligned range (shared boundary pages locked twice)
+    static const int legacy = enf::env_int("ENF_PIN_LEGACY", 0);
+    if (legacy) {
+      want.push_back({(uintptr_t)p, (uintptr_t)p + bytes});
+      return;
+    }
+#endif
+    const uintptr_t pg = 4096;
+    const uintptr_t lo = (uintptr_t)p / pg * pg, hi = ((uintptr_t)p + bytes + pg - 1) / pg * pg;
+    want.push_back({lo, hi});
+  }
+  hipError_t pin() {
+#if ENF_DIAG
+    static const int legacy = enf::env_int("ENF_PIN_LEGACY", 0);
+    if (legacy) {
+      for (const R& r : want) {
+        hipError_t e = hipHostRegister((void*)r.lo, r.hi - r.lo, hipHostRegisterDefault);
+        if (e != hipSuccess) return e;
+        mine.push_back((void*)r.lo);
+      }
+      return hipSuccess;
+    }
+#endif
+    std::sort(want.begin(), want.end(), [](const R& a, const R& b) { return a.lo < b.lo; });
+    std::vector<R> merged;
+    for (const R& r : want) {
+      if (!merged.empty() && r.lo <= merged.back().hi) merged.back().hi = std::max(merged.back().hi, r.hi);
+      else merged.push_back(r);
+    }
+    for (const R& r : merged) {
+      hipError_t e = hipHostRegister((void*)r.lo, r.hi - r.lo, hipHostRegisterDefault);
+      if (e != hipSuccess) return e;
+      mine.push_back((void*)r.lo);
+    }
+    return hipSuccess;
+  }
+  ~HostPins() {
+    for (void* p : mine) (void)hipHostUnregister(p);
   }
 };
 
@@ -359,11 +403,14 @@ enf_status enf_flow_apply_host(enf_dtype dtype, int64_t D, int64_t N, const void
   hipStream_t st = (hipStream_t)hip_stream;
   // host ranges (the last column only spans D values)
   const size_t xb = ((size_t)(N - 1) * ldx + D) * elem, yb = ((size_t)(N - 1) * ldy + D) * elem;
-  HostPin px, py, pl;
-  hipError_t e = px.pin(const_cast<void*>(X), xb);
-  if (e == hipSuccess && Y != X) e = py.pin(Y, yb);
-  if (e == hipSuccess && ladj) e = pl.pin(ladj, (size_t)N * elem);
+  HostPins pins;
+  pins.add(X, xb);
+  if (Y != X) pins.add(Y, yb);
+  if (ladj) pins.add(ladj, (size_t)N * elem);
+  hipError_t e = pins.pin();
   if (e != hipSuccess) return hip_fail(e, "hipHostRegister");
+  // declared after the pins: destroyed (streams synchronised by hipStreamDestroy, slots freed) before
+  // the host ranges are unregistered, also on an early error return
   Ring r;
   const size_t slot_bytes = ((size_t)D * C + (size_t)C) * elem;
   for (int s = 0; s < Ring::kSlots; ++s) {

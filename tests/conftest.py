@@ -14,6 +14,15 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libenf.so on the device)")
+    # diagnostics only: ENF_GUARD_ALLOC=1 | 2 puts every torch device allocation on guard
+    # pages (tools/guard_alloc.cpp: data ending / starting at an unmapped page), so an out-of-range read or
+    # write of any kernel faults in that kernel. Must be installed before the first device allocation.
+    if os.environ.get("ENF_GUARD_ALLOC"):
+        import torch
+
+        so = os.path.join(ROOT, "tools", "libguard_alloc.so")
+        alloc = torch.cuda.memory.CUDAPluggableAllocator(so, "enf_guard_malloc", "enf_guard_free")
+        torch.cuda.memory.change_current_allocator(alloc)
 
 
 @pytest.fixture(scope="session")

@@ -342,9 +342,10 @@ def test_hj_program_exact_redo_edge_values(enf, gpu, oracle, D):
 
 
 @pytest.mark.parametrize("chunk", [0, 1000, 4097, 70_001])
-def test_host_streaming_equals_device_path(enf, gpu, chunk):
+def test_host_streaming_equals_device_path(enf, gpu, oracle, chunk):
     """enf_flow_apply_host (host-resident batch, chunked through a device ring) gives exactly the
-    device path's results: the same kernels per column, any chunking; in place on the host too."""
+    device path's results: the same kernels per column, any chunking; in place on the host too; and
+    (one chunking) the oracle's results on the first two chunks and the ragged tail."""
     rng = np.random.default_rng(31)
     D, N = 32, 200_003
     layers = _hj_layers(rng, D, 4)
@@ -356,6 +357,10 @@ def test_host_streaming_equals_device_path(enf, gpu, chunk):
     Xi = X.copy(order="F")
     Yi, Li = enf.stream_with_logabsdet_jacobian(f, Xi, chunk_cols=chunk, out=Xi)
     assert Yi is Xi and np.array_equal(Xi, Yh) and np.array_equal(Li, Lh)
+    if chunk == 4097:  # and against the oracle (not only HIP against HIP): the first two chunks and the ragged tail
+        cols = np.r_[0:2 * chunk, N - 3000:N]
+        check_vs_oracle(oracle, layers, np.asfortranarray(X[:, cols]), Yh[:, cols],
+                        Lh[:, cols], np.float32, what="host streaming fp32")
 
 
 def test_host_streaming_fp64_mixed_ops(enf, gpu, oracle):
