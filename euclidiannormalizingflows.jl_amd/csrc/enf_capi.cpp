@@ -12,6 +12,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "enf_internal.h"
@@ -303,86 +304,108 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
 // ------------------------------------------------------------------- host-resident batches ----
 namespace {
 
-// Page-lock the host arrays of a call for its duration (hipHostRegister makes the async copies true
-// DMA and lets them overlap the kernels). The arrays are registered as DISJOINT page-aligned ranges:
-// X, Y and ladj are separate allocations that often share a boundary page (numpy arrays in the heap
-// are not page-aligned), and registering each one on its own locked that page twice, once per
-// overlapping registration. Each page is now locked at most once: the page ranges of the arrays are
-// merged where they overlap or touch, and every merged range is one hipHostRegister (every page of
-// it holds bytes of one of the arrays, so it is mapped). An array the caller has registered already
-// is left alone (its copies are DMA anyway).
-struct HostPins {
-  std::vector<void*> mine;
-  struct R { uintptr_t lo, hi; };
-  std::vector<R> want;
-  static bool registered(const void* p) {
-    hipPointerAttribute_t at;
-    std::memset(&at, 0, sizeof at);
-    const bool r = hipPointerGetAttributes(&at, p) == hipSuccess && at.type != hipMemoryTypeUnregistered;
-    (void)hipGetLastError();  // clear the "not registered" status
-    return r;
-  }
-  void add(const void* p, size_t bytes) {
-    if (!p || bytes == 0 || registered(p)) return;
-#if ENF_DIAG
-    // ENF_PIN_LEGACY=1 (diagnostics build, tools/pin_overlap_probe.py): round 2's registration, one
-    // hipHostRegister per array at its exact, unaligned range (shared boundary pages locked twice)
-    static const int legacy = enf::env_int("ENF_PIN_LEGACY", 0);
-    if (legacy) {
-      want.push_back({(uintptr_t)p, (uintptr_t)p + bytes});
-      return;
+// Round 3: the ring no longer page-locks the caller's arrays (hipHostRegister / hipHostUnregister of
+// arbitrary, non-page-aligned heap ranges). A process that had registered and released host arrays
+// later hit hipErrorIllegalAddress in ordinary pageable torch copies of NEW heap arrays placed on the
+// released pages (tools/pin_overlap_probe.py). The ring now owns its host staging:
+// pinned slots from hipHostMalloc, filled from / drained to the caller's arrays by threaded host
+// copies that overlap the device work of the other slots.
+// The slot buffers (device ring and pinned host staging) are cached per process for the device of the
+// last call and reused while large enough (pinning hundreds of MB costs far more than a chunk's copy);
+// a concurrent call that finds the cache in use allocates its own and frees them on return. A slot is
+// at most kStageCap bytes, so the cache stays small (6 x 32 MB pinned host, 3 x 32 MB device).
+constexpr size_t kStageCap = (size_t)32 << 20;
+constexpr int kRingSlots = 3;
+struct RingBufs {
+  void* buf[kRingSlots] = {};   // device: D x C chunk, then C ladj values
+  void* hin[kRingSlots] = {};   // pinned host: the chunk going up
+  void* hout[kRingSlots] = {};  // pinned host: the results coming down
+  size_t bytes = 0;
+  int dev = -1;
+  void release() {
+    for (int s = 0; s < kRingSlots; ++s) {
+      if (buf[s]) (void)hipFree(buf[s]);
+      if (hin[s]) (void)hipHostFree(hin[s]);
+      if (hout[s]) (void)hipHostFree(hout[s]);
+      buf[s] = hin[s] = hout[s] = nullptr;
     }
-#endif
-    const uintptr_t pg = 4096;
-    const uintptr_t lo = (uintptr_t)p / pg * pg, hi = ((uintptr_t)p + bytes + pg - 1) / pg * pg;
-    want.push_back({lo, hi});
+    bytes = 0;
+    dev = -1;
   }
-  hipError_t pin() {
-#if ENF_DIAG
-    static const int legacy = enf::env_int("ENF_PIN_LEGACY", 0);
-    if (legacy) {
-      for (const R& r : want) {
-        hipError_t e = hipHostRegister((void*)r.lo, r.hi - r.lo, hipHostRegisterDefault);
-        if (e != hipSuccess) return e;
-        mine.push_back((void*)r.lo);
+  hipError_t ensure(size_t need, int device) {
+    if (bytes >= need && dev == device) return hipSuccess;
+    release();
+    for (int s = 0; s < kRingSlots; ++s) {
+      hipError_t e = hipMalloc(&buf[s], need);
+      if (e == hipSuccess) e = hipHostMalloc(&hin[s], need, hipHostMallocDefault);
+      if (e == hipSuccess) e = hipHostMalloc(&hout[s], need, hipHostMallocDefault);
+      if (e != hipSuccess) {
+        release();
+        return e;
       }
-      return hipSuccess;
     }
-#endif
-    std::sort(want.begin(), want.end(), [](const R& a, const R& b) { return a.lo < b.lo; });
-    std::vector<R> merged;
-    for (const R& r : want) {
-      if (!merged.empty() && r.lo <= merged.back().hi) merged.back().hi = std::max(merged.back().hi, r.hi);
-      else merged.push_back(r);
-    }
-    for (const R& r : merged) {
-      hipError_t e = hipHostRegister((void*)r.lo, r.hi - r.lo, hipHostRegisterDefault);
-      if (e != hipSuccess) return e;
-      mine.push_back((void*)r.lo);
-    }
+    bytes = need;
+    dev = device;
     return hipSuccess;
   }
-  ~HostPins() {
-    for (void* p : mine) (void)hipHostUnregister(p);
-  }
 };
+std::mutex g_ring_mu;
+RingBufs g_ring_cache;
 
 struct Ring {
-  static constexpr int kSlots = 3;
-  void* buf[kSlots] = {};
+  static constexpr int kSlots = kRingSlots;
+  std::unique_lock<std::mutex> lk{g_ring_mu, std::try_to_lock};
+  RingBufs own;
+  RingBufs& b = lk.owns_lock() ? g_ring_cache : own;
   hipEvent_t h2d[kSlots] = {}, comp[kSlots] = {}, d2h[kSlots] = {};
   hipStream_t up = nullptr, down = nullptr;
   ~Ring() {
+    if (up) (void)hipStreamSynchronize(up);
+    if (down) (void)hipStreamSynchronize(down);
     for (int s = 0; s < kSlots; ++s) {
-      if (buf[s]) (void)hipFree(buf[s]);
       if (h2d[s]) (void)hipEventDestroy(h2d[s]);
       if (comp[s]) (void)hipEventDestroy(comp[s]);
       if (d2h[s]) (void)hipEventDestroy(d2h[s]);
     }
     if (up) (void)hipStreamDestroy(up);
     if (down) (void)hipStreamDestroy(down);
+    own.release();
   }
 };
+
+// cols columns of `width` bytes from src (column stride ss bytes) to dst (stride ds), split over up to 8
+// host threads for large copies (a single thread moves ~10 GB/s; the PCIe link ~2-5x that)
+void host_copy_cols(char* dst, size_t ds, const char* src, size_t ss, size_t width, int64_t cols) {
+  const size_t bytes = width * (size_t)cols;
+  const auto part = [&](int64_t c0, int64_t c1) {
+    if (ds == width && ss == width) {
+      std::memcpy(dst + (size_t)c0 * width, src + (size_t)c0 * width, (size_t)(c1 - c0) * width);
+    } else {
+      for (int64_t c = c0; c < c1; ++c) std::memcpy(dst + (size_t)c * ds, src + (size_t)c * ss, width);
+    }
+  };
+  int nt = (int)std::min<size_t>(8, bytes >> 22);  // one thread per 4 MiB, at most 8
+  const unsigned hc = std::thread::hardware_concurrency();
+  if (hc > 0 && nt > (int)hc) nt = (int)hc;
+  if (nt <= 1 || cols < nt) {
+    part(0, cols);
+    return;
+  }
+  std::vector<std::thread> pool;
+  pool.reserve((size_t)nt);
+  int started = 0;
+  try {
+    for (int t = 1; t < nt; ++t) {
+      pool.emplace_back(part, cols * t / nt, cols * (t + 1) / nt);
+      ++started;
+    }
+  } catch (...) {
+  }
+  part(0, cols / nt);
+  // columns of threads that could not be started: on this thread
+  if (started < nt - 1) part(cols * (started + 1) / nt, cols);
+  for (auto& th : pool) th.join();
+}
 
 }  // namespace
 
@@ -398,23 +421,18 @@ enf_status enf_flow_apply_host(enf_dtype dtype, int64_t D, int64_t N, const void
   if (!X || !Y) return fail(ENF_ERR_INVALID, "X or Y is NULL");
   if (X == Y && ldx != ldy) return fail(ENF_ERR_INVALID, "in-place call (X == Y) needs ldx == ldy");
   const size_t elem = dtype == ENF_F64 ? 8 : 4;
-  int64_t C = chunk_cols > 0 ? chunk_cols : ((int64_t)256 << 20) / (int64_t)((D + 1) * elem);  // ~256 MB slots
+  // chunk: chunk_cols columns (0: as many as fill a slot), at most one slot of kStageCap bytes
+  const int64_t cap = std::max<int64_t>(1, (int64_t)(kStageCap / ((size_t)(D + 1) * elem)));
+  int64_t C = chunk_cols > 0 ? std::min(chunk_cols, cap) : cap;
   if (C > N) C = N;
   hipStream_t st = (hipStream_t)hip_stream;
-  // host ranges (the last column only spans D values)
-  const size_t xb = ((size_t)(N - 1) * ldx + D) * elem, yb = ((size_t)(N - 1) * ldy + D) * elem;
-  HostPins pins;
-  pins.add(X, xb);
-  if (Y != X) pins.add(Y, yb);
-  if (ladj) pins.add(ladj, (size_t)N * elem);
-  hipError_t e = pins.pin();
-  if (e != hipSuccess) return hip_fail(e, "hipHostRegister");
-  // declared after the pins: destroyed (streams synchronised by hipStreamDestroy, slots freed) before
-  // the host ranges are unregistered, also on an early error return
+  int device = 0;
+  hipError_t e = hipGetDevice(&device);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
   Ring r;
   const size_t slot_bytes = ((size_t)D * C + (size_t)C) * elem;
+  if ((e = r.b.ensure(slot_bytes, device)) != hipSuccess) return hip_fail(e, "ingest ring / staging allocation");
   for (int s = 0; s < Ring::kSlots; ++s) {
-    if ((e = hipMalloc(&r.buf[s], slot_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc (ingest ring)");
     if ((e = hipEventCreateWithFlags(&r.h2d[s], hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&r.comp[s], hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&r.d2h[s], hipEventDisableTiming)) != hipSuccess)
@@ -429,22 +447,33 @@ enf_status enf_flow_apply_host(enf_dtype dtype, int64_t D, int64_t N, const void
   const char* Xc = (const char*)X;
   char* Yc = (char*)Y;
   char* Lc = (char*)ladj;
-  int64_t i = 0;
-  for (int64_t c0 = 0; c0 < N; c0 += C, ++i) {
+  const int64_t nchunks = (N + C - 1) / C;
+  const size_t colb = (size_t)D * elem;
+  // results of chunk j: staging -> the caller's Y (and ladj)
+  auto drain = [&](int64_t j) -> hipError_t {
+    const int s = (int)(j % Ring::kSlots);
+    const int64_t c0 = j * C, cols = N - c0 < C ? N - c0 : C;
+    hipError_t ee = hipEventSynchronize(r.d2h[s]);
+    if (ee != hipSuccess) return ee;
+    const char* h = (const char*)r.b.hout[s];
+    host_copy_cols(Yc + (size_t)c0 * ldy * elem, (size_t)ldy * elem, h, colb, colb, cols);
+    if (ladj) std::memcpy(Lc + (size_t)c0 * elem, h + (size_t)D * C * elem, (size_t)cols * elem);
+    return hipSuccess;
+  };
+  for (int64_t i = 0; i < nchunks; ++i) {
     const int s = (int)(i % Ring::kSlots);
-    const int64_t cols = N - c0 < C ? N - c0 : C;
-    char* dX = (char*)r.buf[s];
+    const int64_t c0 = i * C, cols = N - c0 < C ? N - c0 : C;
+    // slot reuse: chunk i - 3's results leave the staging first (its upload finished before them); in
+    // place (Y == X), chunk i - 3's columns are not chunk i's, so the order of the host copies is free
+    if (i >= Ring::kSlots && (e = drain(i - Ring::kSlots)) != hipSuccess) return hip_fail(e, "ingest drain");
+    char* hi = (char*)r.b.hin[s];
+    host_copy_cols(hi, colb, Xc + (size_t)c0 * ldx * elem, (size_t)ldx * elem, colb, cols);
+    if (ladj && accumulate_ladj) std::memcpy(hi + (size_t)D * C * elem, Lc + (size_t)c0 * elem, (size_t)cols * elem);
+    char* dX = (char*)r.b.buf[s];
     char* dL = dX + (size_t)D * C * elem;
-    // slot reuse: wait until its previous results have left the device
-    if (i >= Ring::kSlots && (e = hipStreamWaitEvent(r.up, r.d2h[s], 0)) != hipSuccess)
-      return hip_fail(e, "hipStreamWaitEvent");
-    // a dense chunk (ld == D) is one linear copy: the 2D path is a different, slower copy engine
-    // program for the same bytes (tools/ingest_bench.py)
-    e = ldx == D ? hipMemcpyAsync(dX, Xc + (size_t)c0 * ldx * elem, (size_t)D * cols * elem, hipMemcpyHostToDevice, r.up)
-                 : hipMemcpy2DAsync(dX, D * elem, Xc + (size_t)c0 * ldx * elem, ldx * elem, D * elem, cols,
-                                    hipMemcpyHostToDevice, r.up);
+    e = hipMemcpyAsync(dX, hi, (size_t)D * cols * elem, hipMemcpyHostToDevice, r.up);
     if (e == hipSuccess && ladj && accumulate_ladj)
-      e = hipMemcpyAsync(dL, Lc + (size_t)c0 * elem, cols * elem, hipMemcpyHostToDevice, r.up);
+      e = hipMemcpyAsync(dL, hi + (size_t)D * C * elem, cols * elem, hipMemcpyHostToDevice, r.up);
     if (e == hipSuccess) e = hipEventRecord(r.h2d[s], r.up);
     if (e == hipSuccess) e = hipStreamWaitEvent(st, r.h2d[s], 0);
     if (e != hipSuccess) return hip_fail(e, "ingest H2D");
@@ -453,15 +482,15 @@ enf_status enf_flow_apply_host(enf_dtype dtype, int64_t D, int64_t N, const void
     if (fs != ENF_OK) return fs;
     if ((e = hipEventRecord(r.comp[s], st)) != hipSuccess || (e = hipStreamWaitEvent(r.down, r.comp[s], 0)) != hipSuccess)
       return hip_fail(e, "ingest compute event");
-    e = ldy == D ? hipMemcpyAsync(Yc + (size_t)c0 * ldy * elem, dX, (size_t)D * cols * elem, hipMemcpyDeviceToHost, r.down)
-                 : hipMemcpy2DAsync(Yc + (size_t)c0 * ldy * elem, ldy * elem, dX, D * elem, D * elem, cols,
-                                    hipMemcpyDeviceToHost, r.down);
-    if (e == hipSuccess && ladj) e = hipMemcpyAsync(Lc + (size_t)c0 * elem, dL, cols * elem, hipMemcpyDeviceToHost, r.down);
+    char* ho = (char*)r.b.hout[s];
+    e = hipMemcpyAsync(ho, dX, (size_t)D * cols * elem, hipMemcpyDeviceToHost, r.down);
+    if (e == hipSuccess && ladj) e = hipMemcpyAsync(ho + (size_t)D * C * elem, dL, cols * elem, hipMemcpyDeviceToHost, r.down);
     if (e == hipSuccess) e = hipEventRecord(r.d2h[s], r.down);
     if (e != hipSuccess) return hip_fail(e, "ingest D2H");
   }
-  // synchronous: the results are in host memory (and the ring can be released) on return
-  if ((e = hipStreamSynchronize(r.down)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  // synchronous: the last chunks' results are in the caller's arrays on return
+  for (int64_t j = nchunks > Ring::kSlots ? nchunks - Ring::kSlots : 0; j < nchunks; ++j)
+    if ((e = drain(j)) != hipSuccess) return hip_fail(e, "ingest drain");
   return ENF_OK;
   ENF_CATCH
 }

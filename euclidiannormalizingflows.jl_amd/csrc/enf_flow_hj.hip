@@ -595,6 +595,281 @@ __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   hj_stream<D, R, U, LM, DBG>(a, body);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Wave-specialised form of the same program (round 3): the transcendentals on waves of their own.
+//
+// On gfx950 a v_sqrt / v_log interleaved with a wave's own FMAs costs ~5.5 ns of SIMD time instead of the
+// ~3.7 ns it costs in a run of transcendentals (tools/microbench21: 224 FMAs + 32 transcendentals per wave,
+// 416 ns per wave-iteration vs 240 + 118 alone), while transcendentals issued by OTHER waves of the SIMD
+// largely overlap a wave's FMA stream (tools/microbench22: two FMA waves + two transcendental waves per SIMD
+// 1.27 ms vs 1.67 ms for the same work mixed in every wave). So a block of 16 waves splits each pair:
+//  * F waves (0-7, two per SIMD) own the tiles: dot, reflection and z of pair p; later the small-|z| form,
+//    the merge and y = gamma + delta' L of pair p (the shipped kernel's operations, in its order);
+//  * T waves (8-15, two per SIMD; T wave 8 + f serves F wave f) take z through LDS and return
+//    t = log2(|z| + sqrt(1 + z^2)); they also keep the ladj (the -1/2 log2 of the q product of a lane's 8
+//    rows, one log2 per 8 rows, as before) and store it, and stage the next tiles' X through LDS.
+// Every F wave keeps two tiles in flight (slots A and B, one step apart), so that while the T wave works on
+// one slot's transcendentals the F wave works on the other slot. Steps are paced by one block barrier; a
+// step moves 16 values per lane each way. Identical arithmetic to flow_hj_kernel (AS = 1), so identical
+// results; the exact-range redo of a tile whose q product overflows is run by its F wave.
+constexpr int kHjSpecDefault = 0;         // product default of ENF_HJ_SPEC (dispatch_hj)
+constexpr int kHjsF = 8;                  // F waves per block; T waves kHjsF .. 2 kHjsF - 1
+constexpr int kHjsSlot = 64 * 16;         // floats of one slot: 16 values per lane
+constexpr size_t kHjsStage = (size_t)2 * kHjsF * kStagePerWave * sizeof(float);
+constexpr size_t kHjsFlags = 16 * sizeof(int);  // overflow flag per F wave and slot
+constexpr size_t kHjsExch = (size_t)kHjsF * 2 * kHjsSlot * sizeof(float);  // z / t exchange
+constexpr size_t kHjsXArea = kHjsExch;                                      // next tiles' X
+static size_t hjs_lds_bytes(int D, int n) {
+  return kHjScratch + kHjsStage + kHjsFlags + kHjsExch + kHjsXArea + (size_t)(n + 1) * kHjW * D * sizeof(float);
+}
+
+// LDS slot of one lane: 16 values in 4 16-byte vectors at a stride of 1 KiB (conflict-free b128 access)
+template <int R, int U>
+__device__ __forceinline__ void slot_write(float* __restrict__ slot, int lane, const float (&v)[U][R]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int h = 0; h < R / 4; ++h) {
+      u32x4 w;
+      __builtin_memcpy(&w, &v[u][4 * h], 16);
+      *reinterpret_cast<u32x4*>(slot + (u * (R / 4) + h) * 256 + 4 * lane) = w;
+    }
+}
+template <int R, int U>
+__device__ __forceinline__ void slot_read(const float* __restrict__ slot, int lane, float (&v)[U][R]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int h = 0; h < R / 4; ++h) {
+      const u32x4 w = *reinterpret_cast<const u32x4*>(slot + (u * (R / 4) + h) * 256 + 4 * lane);
+      __builtin_memcpy(&v[u][4 * h], &w, 16);
+    }
+}
+
+// F: y of pair p - 1 from the T wave's t (x holds that pair's z on entry), record r = record p
+template <int R, int U>
+__device__ __forceinline__ void hjs_merge(float (&x)[U][R], const float (&t)[U][R], const HJParams<R>& prm,
+                                          uint32_t csign) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < R; ++e) {
+      const float q = fmaf(x[u][e], x[u][e], 1.0f);
+      const uint32_t m = asinh2_mask(q, csign);
+      const float L = asinh2_pick(asinh2_small(x[u][e], q), t[u][e], m);
+      x[u][e] = fmaf(L, prm.m(HJ_DP, e), prm.m(HJ_GP, e));
+    }
+}
+
+// Y of a finished tile (F wave); the ladj is the T wave's
+template <int D, int R, int U>
+__device__ __forceinline__ void hjs_store_y(const HJArgs& a, int64_t col0, const float (&x)[U][R]) {
+  using L = HJLay<D, R, U>;
+  const int lane = threadIdx.x & 63;
+  float* __restrict__ Y = (float*)a.Y;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t c = L::col(col0, u, lane);
+#pragma unroll
+    for (int h = 0; h < L::NF; ++h) {
+      u32x4 v4;
+      __builtin_memcpy(&v4, &x[u][4 * h], 16);
+      if (ENF_INB(c < a.N, "hjs store Y", c, a.N))
+        __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(Y + c * D + L::row(h, lane)));
+    }
+  }
+}
+
+template <int D, int LM>
+__global__ __launch_bounds__(1024, 1) void flow_hjs_kernel(HJArgs a) {
+  constexpr int R = 8, U = 2;
+  using L = HJLay<D, R, U>;
+  constexpr int G = L::G;
+  const int n = a.n;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* scr = reinterpret_cast<double*>(smem);
+  float* ctotp = reinterpret_cast<float*>(scr + 2 * kHjMaxPairs);
+  unsigned char* p0 = smem + kHjScratch;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  float* stage = reinterpret_cast<float*>(p0) + wave * kStagePerWave;
+  int* flags = reinterpret_cast<int*>(p0 + kHjsStage);
+  float* exch = reinterpret_cast<float*>(p0 + kHjsStage + kHjsFlags);
+  float* xarea = exch + kHjsF * 2 * kHjsSlot;
+  float* rec = xarea + kHjsF * 2 * kHjsSlot;
+  const bool isF = wave < kHjsF;
+  const int f = isF ? wave : wave - kHjsF;
+  float* ex[2] = {exch + (2 * f) * kHjsSlot, exch + (2 * f + 1) * kHjsSlot};
+  float* xa[2] = {xarea + (2 * f) * kHjsSlot, xarea + (2 * f + 1) * kHjsSlot};
+
+  constexpr int64_t CT = L::TC;
+  const int64_t ntiles = a.N / CT;
+  const int64_t stride = (int64_t)gridDim.x * kHjsF;
+  const int64_t g = (int64_t)blockIdx.x * kHjsF + f;  // this F wave's (or its partner's) tile stream
+  const int64_t K = g < ntiles ? (ntiles - 1 - g) / stride + 1 : 0;
+  const int64_t g0 = (int64_t)blockIdx.x * kHjsF;
+  const int64_t Kmax = g0 < ntiles ? (ntiles - 1 - g0) / stride + 1 : 0;
+  auto tile_col = [&](int64_t k) { return (g + k * stride) * CT; };
+
+  // T waves: the first tile of each slot, loaded before the prologue
+  float xt[2][U][R];
+  if (!isF) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      if (s < K) hj_load<D, R, U, false, 0>(a, tile_col(s), xt[s]);
+  }
+  build_hj_program<D, R, 1>(a, n, rec, scr, ctotp);  // ends with a block barrier
+  const float ctot = *ctotp;
+  const float* recl = rec + (lane % G) * kHjW * R;
+  if (!isF) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      if (s < K) slot_write<R, U>(xa[s], lane, xt[s]);
+    if (lane < 2) flags[2 * f + lane] = 0;
+  }
+  __syncthreads();
+
+  // steps: slot A (X = 0) holds tiles 0, 2, 4, ... of the stream and gets F steps 0, 2, 4, ...; slot B tiles
+  // 1, 3, ... and steps 1, 3, ...; a tile takes n F steps (pair p's z phase, merged with pair p - 1's y),
+  // its last y comes with the first step of the slot's next tile. T processes at step s the slot F touched
+  // at step s - 1.
+  const int64_t nA = (Kmax + 1) / 2, nB = Kmax / 2;
+  const int64_t S = Kmax == 0 ? 0 : ((2 * n * nA > 2 * n * nB + 1) ? 2 * n * nA : 2 * n * nB + 1) + 1;
+  const uint32_t csign = sign_mask_vgpr();
+  float x[2][U][R];        // F: the two slots' tiles (z after a z phase, y after a merge)
+  float acc[2][U] = {};    // T: ladj partials of the two slots' tiles
+  float mx[2] = {0.f, 0.f};  // T: largest q product of the slot's tile
+  HJParams<R> prm;
+
+  auto f_step = [&](auto XC, int64_t s) {
+    constexpr int X = decltype(XC)::value;
+    if (s < X) return;
+    const int64_t q = (s - X) >> 1;
+    const int64_t j = q / n;
+    const int p = (int)(q - j * n);
+    const int64_t k = 2 * j + X;
+    if (p == 0 && j > 0 && k - 2 < K) {
+      // the slot's previous tile: its last y (record n), or the exact-range redo from X
+      const int64_t c0 = tile_col(k - 2);
+      if (flags[2 * f + X] == 0) {
+        float t[U][R];
+        slot_read<R, U>(ex[X], lane, t);
+        prm.template load<0, HJ_IL>(recl + n * kHjW * D);
+        hjs_merge<R, U>(x[X], t, prm, csign);
+        hjs_store_y<D, R, U>(a, c0, x[X]);
+      } else {
+        float old[L::NLS];
+        hj_load<D, R, U, false, 0>(a, c0, x[X]);
+        hj_load_old<D, R, U, LM>(a, c0, old, false);
+        float accx[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) accx[u] = 0.f;
+        const float* r = recl;
+        HJParams<R> pe;
+        pe.template load<0, HJ_IL>(r);
+        for (int pp = 0; pp < n; ++pp) hj_pair_exact<D, R, U, LM != 0, 1>(x[X], accx, r, pe);
+        hj_store<D, R, U, LM, false, 0>(a, ctot, c0, x[X], accx, old, stage);
+      }
+    }
+    if (k >= K) return;
+    const float* rp = recl + p * kHjW * D;
+    prm.template load<0, HJ_IL>(rp);
+    if (p == 0) {
+      slot_read<R, U>(xa[X], lane, x[X]);
+    } else {
+      float t[U][R];
+      slot_read<R, U>(ex[X], lane, t);
+      hjs_merge<R, U>(x[X], t, prm, csign);
+    }
+    hj_pair_z<D, R, U>(x[X], rp, prm);
+    slot_write<R, U>(ex[X], lane, x[X]);
+  };
+
+  auto t_step = [&](auto YC, int64_t s) {
+    constexpr int Y = decltype(YC)::value;
+    if (s < Y + 1) return;
+    const int64_t q = (s - 1 - Y) >> 1;
+    const int64_t j = q / n;
+    const int p = (int)(q - j * n);
+    const int64_t k = 2 * j + Y;
+    if (k >= K) return;
+    if (p == 0 && k + 2 < K) hj_load<D, R, U, false, 0>(a, tile_col(k + 2), xt[Y]);  // the slot's next tile
+    float z[U][R], t[U][R];
+    slot_read<R, U>(ex[Y], lane, z);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float qv[R];
+#pragma unroll
+      for (int e = 0; e < R; ++e) qv[e] = fmaf(z[u][e], z[u][e], 1.0f);
+      sqrt8(t[u], qv);
+      const float pr = prod_tree<R>(qv);
+#pragma unroll
+      for (int e = 0; e < R; ++e) t[u][e] = fabsf(z[u][e]) + t[u][e];
+      log2_8_inplace(t[u]);
+      if (LM > 0) acc[Y][u] = fmaf(-0.5f, hw_log2(pr), acc[Y][u]);
+      mx[Y] = fmaxf(mx[Y], pr);
+    }
+    slot_write<R, U>(ex[Y], lane, t);
+    if (p == n - 1) {
+      // tile done: the F wave redoes it in the exact form when some q product overflowed (+Inf / NaN)
+      const bool ovf = __any(!(mx[Y] <= FLT_MAX));
+      if (lane == 0) flags[2 * f + Y] = ovf ? 1 : 0;
+      if (LM > 0 && !ovf) {
+        const int64_t c0 = tile_col(k);
+        float old[L::NLS];
+        hj_load_old<D, R, U, LM>(a, c0, old, false);
+        float* __restrict__ ladj = (float*)a.ladj;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float tot = group_sum<G>(acc[Y][u]);
+          if ((lane % G) == 0) stage[u * L::CPS + lane / G] = tot;
+        }
+#pragma unroll
+        for (int kk = 0; kk < L::NLS; ++kk) {
+          const int c = kk * 64 + (L::TC >= 64 ? lane : lane % L::TC);
+          const float v = fmaf((float)kLn2, stage[c], ctot) + old[kk];
+          if (ENF_INB(c0 + c < a.N, "hjs ladj", c0 + c, a.N)) ladj[c0 + c] = v;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[Y][u] = 0.f;
+      mx[Y] = 0.f;
+      if (k + 2 < K) slot_write<R, U>(xa[Y], lane, xt[Y]);  // waits for the load issued at p == 0
+    }
+  };
+
+  // one loop per role (wave-uniform branch; both execute the same S barriers), so that neither keeps the
+  // other's registers live
+  if (isF) {
+    for (int64_t s = 0; s < S; s += 2) {
+      f_step(std::integral_constant<int, 0>{}, s);
+      __syncthreads();
+      if (s + 1 < S) {
+        f_step(std::integral_constant<int, 1>{}, s + 1);
+        __syncthreads();
+      }
+    }
+  } else {
+    for (int64_t s = 0; s < S; s += 2) {
+      t_step(std::integral_constant<int, 1>{}, s);
+      __syncthreads();
+      if (s + 1 < S) {
+        t_step(std::integral_constant<int, 0>{}, s + 1);
+        __syncthreads();
+      }
+    }
+  }
+  // the ragged last tile: one F wave, whole program in its own registers (flow_hj_kernel's tail path)
+  if (isF && ntiles * CT < a.N && g == ntiles % stride) {
+    HJBody<D, R, U, LM, 1, 0> body{a, recl, ctot, stage, n};
+    const int64_t c0 = ntiles * CT;
+    float xt0[U][R], old[L::NLS];
+    hj_load<D, R, U, true, 0>(a, c0, xt0);
+    hj_load_old<D, R, U, LM>(a, c0, old, true);
+    body.template tile<true, 0>(c0, xt0, old);
+  }
+}
+
 int hj_program_pairs(const FlowArgs& a) {
   if (!a.frag || (a.D != 32 && a.D != 64) || a.nsteps < 2 || (a.nsteps & 1)) return 0;
   for (int s = 0; s < a.nsteps; ++s) {
@@ -602,6 +877,20 @@ int hj_program_pairs(const FlowArgs& a) {
     if (a.steps[s].op != want) return 0;
   }
   return a.nsteps / 2;
+}
+
+// one block of 16 waves per CU
+template <int D, int LM>
+static hipError_t launch_hjs(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
+  const size_t lds = hjs_lds_bytes(D, h.n);
+  const void* k = reinterpret_cast<const void*>(&flow_hjs_kernel<D, LM>);
+  hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  int64_t blocks = dev.num_cu;
+  const int64_t need = (h.N + (int64_t)HJLay<D, 8, 2>::TC * kHjsF - 1) / ((int64_t)HJLay<D, 8, 2>::TC * kHjsF);
+  if (blocks > need) blocks = need > 0 ? need : 1;
+  hipLaunchKernelGGL((flow_hjs_kernel<D, LM>), dim3((unsigned)blocks), dim3(1024), lds, st, h);
+  return hipGetLastError();
 }
 
 template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, int AS = 1, int VAR = 0>
@@ -629,6 +918,9 @@ static hipError_t launch_hj_as(int as, const HJArgs& a, hipStream_t st, const De
 template <int LM>
 static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, const DeviceInfo& dev) {
   (void)dbg;
+  // ENF_HJ_SPEC: 1 = the wave-specialised kernel (flow_hjs_kernel), 0 = flow_hj_kernel
+  static const int spec = ENF_KNOB("ENF_HJ_SPEC", kHjSpecDefault);
+  if (spec && dbg == 0) return D == 32 ? launch_hjs<32, LM>(a, st, dev) : launch_hjs<64, LM>(a, st, dev);
   if (D == 32) {
 #if ENF_DIAG
     if constexpr (LM == 1) {

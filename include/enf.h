@@ -106,9 +106,10 @@ enf_status enf_flow_apply(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
 /* Host-resident batch (optimize_whitening's VectorOfSimilarVectors /
  * flatview batches, src/optimize_whitening.jl:26,38, and N beyond device memory): the same
  * computation as enf_flow_apply with X, Y and ladj in HOST memory. Column chunks of chunk_cols
- * samples (0: ~256 MB per chunk) stream through a 3-slot device ring: host->device copy of chunk
+ * samples (0 or more than fit: as many as fill a 32 MB slot) stream through a 3-slot device ring: host->device copy of chunk
  * i+1, the fused flow on chunk i (on hip_stream) and device->host copy of chunk i-1 overlap.
- * Pageable host ranges are page-locked for the duration of the call. Layer parameters are device
+ * The caller's arrays are never page-locked: chunks pass through the ring's own pinned staging
+ * slots (threaded host copies overlap the device work). Layer parameters are device
  * pointers as in enf_flow_apply. Synchronous: returns when Y and ladj are in host memory.
  * Y may alias X exactly (ldx == ldy). */
 enf_status enf_flow_apply_host(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,

@@ -70,8 +70,11 @@ def main():
     ms = e0.elapsed_time(e1) / args.steps
     esz = 4 if args.dtype == "f32" else 8
     knobs = {k: v for k, v in os.environ.items() if k.startswith("ENF_")}
+    # bitwise fingerprint of the outputs (variants with identical arithmetic must agree exactly)
+    import hashlib
+    fp = hashlib.sha1(Y.cpu().numpy().tobytes() + ladj.cpu().numpy().tobytes()).hexdigest()[:16]
     print(json.dumps({"tag": args.tag, "lib": os.path.basename(lib.LIB_PATH), "knobs": knobs, "D": D, "N": N,
-                      "pairs": args.pairs, "pattern": args.pattern, "dtype": args.dtype, "kernel_ms": ms,
+                      "pairs": args.pairs, "pattern": args.pattern, "dtype": args.dtype, "kernel_ms": ms, "out_sha1": fp,
                       "samples_per_s": N / (ms * 1e-3),
                       "hbm_frac": N * (2 * D + 1) * esz / (ms * 1e-3) / 8e12}))
 
