@@ -595,6 +595,7 @@ __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   hj_stream<D, R, U, LM, DBG>(a, body);
 }
 
+#if ENF_DIAG
 // ---------------------------------------------------------------------------------------------------
 // Wave-specialised form of the same program (round 3): the transcendentals on waves of their own.
 //
@@ -612,6 +613,11 @@ __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
 // one slot's transcendentals the F wave works on the other slot. Steps are paced by one block barrier; a
 // step moves 16 values per lane each way. Identical arithmetic to flow_hj_kernel (AS = 1), so identical
 // results; the exact-range redo of a tile whose q product overflows is run by its F wave.
+// MEASURED AND REJECTED (diagnostics build only, ENF_HJ_SPEC=1): bit-identical outputs but 0.97 vs 0.78 ms at
+// D = 32 and 0.99 vs 0.80 ms at D = 64 (profiles/r03_hjs_spec_ab.jsonl) -- one block barrier per step puts all
+// F waves of a SIMD in the same phase, so the LDS round trips and the dot's DPP chain of each step are exposed
+// instead of hidden behind the other waves' work; the synthetic form of the same pacing
+// (tools/microbench23: 975 ns per step against 888 for the mixed stream) showed the same.
 constexpr int kHjSpecDefault = 0;         // product default of ENF_HJ_SPEC (dispatch_hj)
 constexpr int kHjsF = 8;                  // F waves per block; T waves kHjsF .. 2 kHjsF - 1
 constexpr int kHjsSlot = 64 * 16;         // floats of one slot: 16 values per lane
@@ -869,6 +875,7 @@ __global__ __launch_bounds__(1024, 1) void flow_hjs_kernel(HJArgs a) {
     body.template tile<true, 0>(c0, xt0, old);
   }
 }
+#endif  // ENF_DIAG
 
 int hj_program_pairs(const FlowArgs& a) {
   if (!a.frag || (a.D != 32 && a.D != 64) || a.nsteps < 2 || (a.nsteps & 1)) return 0;
@@ -879,6 +886,7 @@ int hj_program_pairs(const FlowArgs& a) {
   return a.nsteps / 2;
 }
 
+#if ENF_DIAG
 // one block of 16 waves per CU
 template <int D, int LM>
 static hipError_t launch_hjs(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
@@ -892,6 +900,7 @@ static hipError_t launch_hjs(const HJArgs& h, hipStream_t st, const DeviceInfo& 
   hipLaunchKernelGGL((flow_hjs_kernel<D, LM>), dim3((unsigned)blocks), dim3(1024), lds, st, h);
   return hipGetLastError();
 }
+#endif
 
 template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, int AS = 1, int VAR = 0>
 static hipError_t launch_hj(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
@@ -918,9 +927,11 @@ static hipError_t launch_hj_as(int as, const HJArgs& a, hipStream_t st, const De
 template <int LM>
 static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, const DeviceInfo& dev) {
   (void)dbg;
-  // ENF_HJ_SPEC: 1 = the wave-specialised kernel (flow_hjs_kernel), 0 = flow_hj_kernel
+  // ENF_HJ_SPEC (diagnostics build): 1 = the wave-specialised kernel (flow_hjs_kernel, rejected), 0 = flow_hj_kernel
+#if ENF_DIAG
   static const int spec = ENF_KNOB("ENF_HJ_SPEC", kHjSpecDefault);
   if (spec && dbg == 0) return D == 32 ? launch_hjs<32, LM>(a, st, dev) : launch_hjs<64, LM>(a, st, dev);
+#endif
   if (D == 32) {
 #if ENF_DIAG
     if constexpr (LM == 1) {
