@@ -84,9 +84,7 @@ void layer_block(const HostLayer& L, int64_t D, int64_t nc, T* Y, int64_t ld, T*
   const T* p3 = (const T*)L.p[3];
   switch (L.op) {
     case ENF_OP_SCALESHIFT: {
-      T s = T(0);
-      // sum(log.(abs.(f.a))) over a's own length (k = 1: a length-1 `a` broadcast to the D rows)
-      for (int64_t d = 0; d < (L.k == 1 ? std::min<int64_t>(D, 1) : D); ++d) s += std::log(std::fabs(p0[d]));
+      const T s = vv[0];  // sum(log.(abs.(f.a))), once per call (run_cpu)
       for (int64_t j = 0; j < nc; ++j) {
         T* y = Y + j * ld;
         for (int64_t d = 0; d < D; ++d) y[d] = std::fma(y[d], p0[d], p1[d]);
@@ -163,6 +161,15 @@ void run_cpu(int64_t D, int64_t N, const T* X, int64_t ldx, T* Y, int64_t ldy, T
   // v'v of every reflection vector once per call (the reference's _dot(v, v) per reflection)
   std::vector<std::vector<T>> vv(nl);
   for (int l = 0; l < nl; ++l) {
+    if (layers[l].op == ENF_OP_SCALESHIFT) {
+      // sum(log.(abs.(f.a))) over a's own length (k = 1: a length-1 `a` broadcast to the D rows), in the
+      // reference's order; one value per call instead of one per column block
+      const T* a = (const T*)layers[l].p[0];
+      T s = T(0);
+      for (int64_t d = 0; d < (layers[l].k == 1 ? std::min<int64_t>(D, 1) : D); ++d) s += std::log(std::fabs(a[d]));
+      vv[l].assign(1, s);
+      continue;
+    }
     if (layers[l].op != ENF_OP_HOUSEHOLDER) continue;
     vv[l].resize(layers[l].k);
     for (int c = 0; c < layers[l].k; ++c) {
@@ -182,8 +189,11 @@ void run_cpu(int64_t D, int64_t N, const T* X, int64_t ldx, T* Y, int64_t ldy, T
       const int64_t c0 = b * kBlock, nc = N - c0 < kBlock ? N - c0 : kBlock;
       T* Yb = Y + c0 * ldy;
       const T* Xb = X + c0 * ldx;
-      if (Yb != Xb)
-        for (int64_t j = 0; j < nc; ++j) std::memmove(Yb + j * ldy, Xb + j * ldx, (size_t)D * sizeof(T));
+      if (Yb != Xb) {
+        if (ldx == D && ldy == D) std::memmove(Yb, Xb, (size_t)(D * nc) * sizeof(T));  // dense: one copy
+        else
+          for (int64_t j = 0; j < nc; ++j) std::memmove(Yb + j * ldy, Xb + j * ldx, (size_t)D * sizeof(T));
+      }
       for (int l = 0; l < nl; ++l) layer_block<T>(layers[l], D, nc, Yb, ldy, lt.data() + (size_t)l * kBlock, vv[l]);
       if (ladj) {
         for (int64_t j = 0; j < nc; ++j) {
@@ -224,7 +234,7 @@ enf_status flow_apply_cpu(bool f64, int64_t D, int64_t N, const void* X, int64_t
   int nt = nthreads;
   if (nt <= 0) {  // all hardware threads, but at least ~2^16 element-steps per thread (a thread's start
                   // costs tens of microseconds: config 1's 1000 x 1 batch runs on the calling thread)
-    const unsigned h = std::thread::hardware_concurrency();
+    static const unsigned h = std::thread::hardware_concurrency();  // a system query: once per process
     int64_t steps = 0;
     for (int l = 0; l < nlayers; ++l) steps += layers[l].op == ENF_OP_HOUSEHOLDER ? 2 * (int64_t)layers[l].k : 1;
     const int64_t work = N * (D > 0 ? D : 1) * (steps > 0 ? steps : 1);

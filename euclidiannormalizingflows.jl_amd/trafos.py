@@ -512,11 +512,52 @@ def _apply_scalar(f, x, want_ladj: bool):
     return _apply(f, np.full(D, x, dtype=np_dt), want_ladj)
 
 
+def _apply_host_numpy(ts, X: np.ndarray, want_ladj: bool):
+    """Host fast path (config 1: a numpy (D, N) batch): one enf_flow_apply_cpu call on numpy buffers, no
+    torch tensors for X / Y / ladj. None when it does not apply (several promoted dtype runs, a vector
+    input, an empty flow); the general path then handles the call with identical results."""
+    if X.ndim != 2 or not ts or X.dtype not in (np.float32, np.float64):
+        return None
+    dt = _promote(_kind(X), *[_kind(p) for t in ts for p in t.params()])
+    npdt = np.float64 if dt == torch.float64 else np.float32
+    if X.dtype != npdt:
+        return None  # a promotion run: the general path converts
+    D, N = X.shape
+    if want_ladj:
+        for t in ts:
+            t._check_ladj_signature(False)
+    M = X if (X.flags.f_contiguous or N == 1 or D == 1) else np.asfortranarray(X)
+    ldx = max(D, 1) if N <= 1 else M.strides[1] // M.itemsize
+    if N > 1 and D > 1 and M.strides[0] != M.itemsize:
+        M, ldx = np.asfortranarray(M), D
+    Y = np.empty((D, N), dtype=npdt, order="F")
+    L = np.empty((1, N), dtype=npdt) if want_ladj else None
+    cpu = torch.device("cpu")
+    arr = (_lib.Layer * len(ts))()
+    keep = []
+    for i, t in enumerate(ts):
+        ps = t._device_params(cpu, dt, D)
+        keep.extend(ps)
+        arr[i].op = t.OP
+        arr[i].k = t._k()
+        for q, pt in enumerate(ps):
+            arr[i].p[q] = pt.data_ptr()
+    _lib.check(_lib.lib().enf_flow_apply_cpu(
+        _lib.ENF_F64 if dt == torch.float64 else _lib.ENF_F32, D, N, M.ctypes.data, ldx, Y.ctypes.data, max(D, 1),
+        L.ctypes.data if L is not None else None, 0, arr, len(ts), 0))
+    del keep
+    return Y, L
+
+
 def _apply(f, X, want_ladj: bool):
     if isinstance(X, (numbers.Real, np.generic)) and not isinstance(X, bool) or \
             (isinstance(X, np.ndarray) and X.ndim == 0):
         return _apply_scalar(f, X.item() if isinstance(X, np.ndarray) else X, want_ladj)
     ts = leaves(f)
+    if isinstance(X, np.ndarray):
+        r = _apply_host_numpy(ts, X, want_ladj)
+        if r is not None:
+            return r
     M, restore, is_vec = _to_matrix(X)
     if want_ladj:
         for t in ts:
