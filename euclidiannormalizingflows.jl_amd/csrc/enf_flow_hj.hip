@@ -54,7 +54,7 @@ struct HJArgs {
   void* ladj;
   int64_t N;
   int32_t n;        // pairs
-  int32_t pad_;
+  int32_t dreal;    // rows of the batch: D, or fewer on the padded layout (PAD: rows past dreal are inert)
   const float* v[kHjMaxPairs];  // reflection vector (column of V) of pair p
   const float* g[kHjMaxPairs];  // Johnson gamma, delta, xi, lambda of pair p
   const float* d[kHjMaxPairs];
@@ -106,18 +106,25 @@ __host__ __device__ constexpr bool hj_rotated(int q) { return q == HJ_DP || q ==
 // skip the stores (compute-only timing); cache policy A/B: 8 = nontemporal loads, 9 = plain stores.
 // The product loads X with plain loads (0.800 / 0.798 vs 0.808 / 0.805 ms with nontemporal loads,
 // profiles/r02_cache_policy_ab.jsonl) and writes Y with nontemporal stores (plain: 0.810 / 0.822).
-template <int D, int R, int U, bool TAIL, int DBG>
+// PAD (padded layout, round 3): D is the power-of-two layout, columns are a.dreal rows apart, and a
+// fragment whose rows start at or past a.dreal holds zeros and is neither loaded nor stored (a.dreal is
+// a multiple of 4, so a fragment is wholly inside or outside).
+template <int D, int R, int U, bool TAIL, int DBG, bool PAD = false>
 __device__ __forceinline__ void hj_load(const HJArgs& a, int64_t col0, float (&x)[U][R]) {
   using L = HJLay<D, R, U>;
   const int lane = threadIdx.x & 63;
   const float* __restrict__ X = (const float*)a.X;
+  const int64_t ld = PAD ? (int64_t)a.dreal : (int64_t)D;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t c = L::col(col0, u, lane);
 #pragma unroll
     for (int h = 0; h < L::NF; ++h) {
-      const int64_t off = c * D + L::row(h, lane);
-      if (DBG == 1 || DBG == 2) {
+      const int64_t off = c * ld + L::row(h, lane);
+      if (PAD && L::row(h, lane) >= a.dreal) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[u][4 * h + e] = 0.f;
+      } else if (DBG == 1 || DBG == 2) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) x[u][4 * h + e] = (float)(lane + 3 * u + 5 * h + e) * 0.03125f - 1.f;
       } else if (!TAIL) {
@@ -148,20 +155,23 @@ __device__ __forceinline__ void hj_load_old(const HJArgs& a, int64_t col0, float
 
 // Y fragments, then the ladj: column totals (group sums over the G lanes of a column) staged
 // through the wave's LDS slots and written by NLS full-wave coalesced stores.
-template <int D, int R, int U, int LM, bool TAIL, int DBG>
+template <int D, int R, int U, int LM, bool TAIL, int DBG, bool PAD = false>
 __device__ __forceinline__ void hj_store(const HJArgs& a, float ctot, int64_t col0, float (&x)[U][R],
                                          const float (&acc)[U], const float (&old)[HJLay<D, R, U>::NLS],
                                          float* __restrict__ stage) {
   using L = HJLay<D, R, U>;
   const int lane = threadIdx.x & 63;
   float* __restrict__ Y = (float*)a.Y;
+  const int64_t ld = PAD ? (int64_t)a.dreal : (int64_t)D;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t c = L::col(col0, u, lane);
 #pragma unroll
     for (int h = 0; h < L::NF; ++h) {
-      const int64_t off = c * D + L::row(h, lane);
-      if (DBG == 2) {
+      const int64_t off = c * ld + L::row(h, lane);
+      if (PAD && L::row(h, lane) >= a.dreal) {
+        continue;
+      } else if (DBG == 2) {
         if (x[u][4 * h] == 1234.5f) Y[off] = x[u][4 * h + 1];  // keeps the compute alive
       } else if (!TAIL) {
         u32x4 v4;
@@ -207,7 +217,7 @@ __device__ void build_hj_program(const HJArgs& a, int n, float* __restrict__ rec
   for (int p = wave; p < n; p += nw) {
     const float* v = a.v[p];
     double vv = 0.0, cl = 0.0;
-    for (int d = lane; d < D; d += 64) {
+    for (int d = lane; d < a.dreal; d += 64) {  // the batch's rows (padded rows: neutral records below)
       const double vd = v[d];
       vv += vd * vd;
       cl += log(fabs((double)a.d[p][d])) - log(fabs((double)a.lam[p][d]));
@@ -228,9 +238,13 @@ __device__ void build_hj_program(const HJArgs& a, int n, float* __restrict__ rec
     const int h = d / (D / NF), w = d % (D / NF), g = w / 4, e = w % 4;
     float* r = rec + (size_t)p * kHjW * D + g * kHjW * R + 4 * h;
     double q[kHjW] = {0, 0, 0, 0, 0, 0};
-    q[HJ_DP] = p > 0 ? (double)a.d[p - 1][d] * kLn2 : 1.0;
-    q[HJ_GP] = p > 0 ? (double)a.g[p - 1][d] : 0.0;
-    if (p < n) {
+    // a padded row (d >= dreal): vh = 0, 1/lambda = 1, -xi/lambda = 0, gamma = 0 -- its zeros stay zero,
+    // with q = 1 (ladj 0); its ladj constant is not in ctot (pass 1)
+    const bool real = d < a.dreal;
+    q[HJ_DP] = p > 0 && real ? (double)a.d[p - 1][d] * kLn2 : 1.0;
+    q[HJ_GP] = p > 0 && real ? (double)a.g[p - 1][d] : 0.0;
+    q[HJ_IL] = 1.0;
+    if (p < n && real) {
       const double vh = (double)a.v[p][d] * scr[2 * p];
       const double il = zs / (double)a.lam[p][d];
       q[HJ_VH] = vh;
@@ -504,7 +518,7 @@ __device__ __forceinline__ void hj_pair_exact(float (&x)[U][R], float (&acc)[U],
     for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_DP, e), prm.m(HJ_GP, e));
 }
 
-template <int D, int R, int U, int LM, int AS = 1, int VAR = 0>
+template <int D, int R, int U, int LM, int AS = 1, int VAR = 0, bool PAD = false>
 struct HJBody {
   const HJArgs& a;
   const float* rec;  // this lane's record group
@@ -529,7 +543,7 @@ struct HJBody {
     // column-uniform: the exact form's dot products read every lane of a column (DPP)
     m = group_max<HJLay<D, R, U>::G>(m);
     if (__builtin_expect(!(m <= FLT_MAX), 0)) {
-      hj_load<D, R, U, TAIL, DBG>(a, col0, x);
+      hj_load<D, R, U, TAIL, DBG, PAD>(a, col0, x);
 #pragma unroll
       for (int u = 0; u < U; ++u) acc[u] = 0.f;
       r = rec;
@@ -537,14 +551,14 @@ struct HJBody {
       for (int p = 0; p < n; ++p) hj_pair_exact<D, R, U, LADJ, AS>(x, acc, r, prm);
     }
     // (y_n = gamma_n + delta'_n L_n was formed at the end of the last pair)
-    hj_store<D, R, U, LM, TAIL, DBG>(a, ctot, col0, x, acc, old, stage);
+    hj_store<D, R, U, LM, TAIL, DBG, PAD>(a, ctot, col0, x, acc, old, stage);
   }
 };
 
 // Persistent, software-pipelined tile loop (as frag_stream in enf_frag.h, for the HJLay layout):
 // wave w processes tiles w, w + nwaves, ...; the next tile's loads are in flight while this tile
 // computes; the ragged last tile (N not a multiple of the tile) is processed by one wave.
-template <int D, int R, int U, int LM, int DBG, typename Body>
+template <int D, int R, int U, int LM, int DBG, bool PAD, typename Body>
 __device__ __forceinline__ void hj_stream(const HJArgs& a, Body& body) {
   using L = HJLay<D, R, U>;
   constexpr int64_t CT = L::TC;
@@ -555,33 +569,33 @@ __device__ __forceinline__ void hj_stream(const HJArgs& a, Body& body) {
   float xa[U][R], xb[U][R], old[L::NLS];
   const int64_t t = wave_id;
   if (t < ntiles_full) {
-    hj_load<D, R, U, false, DBG>(a, t * CT, xa);
+    hj_load<D, R, U, false, DBG, PAD>(a, t * CT, xa);
     int64_t t1 = t + nwaves;
     hj_load_old<D, R, U, LM>(a, t * CT, old, false);
-    hj_load<D, R, U, false, DBG>(a, (t1 < ntiles_full ? t1 : t) * CT, xb);
+    hj_load<D, R, U, false, DBG, PAD>(a, (t1 < ntiles_full ? t1 : t) * CT, xb);
     body.template tile<false, DBG>(t * CT, xa, old);
     while (t1 < ntiles_full) {
       const int64_t t2 = t1 + nwaves;
       hj_load_old<D, R, U, LM>(a, t1 * CT, old, false);
-      hj_load<D, R, U, false, DBG>(a, (t2 < ntiles_full ? t2 : t1) * CT, xa);
+      hj_load<D, R, U, false, DBG, PAD>(a, (t2 < ntiles_full ? t2 : t1) * CT, xa);
       body.template tile<false, DBG>(t1 * CT, xb, old);
       if (t2 >= ntiles_full) break;
       const int64_t t3 = t2 + nwaves;
       hj_load_old<D, R, U, LM>(a, t2 * CT, old, false);
-      hj_load<D, R, U, false, DBG>(a, (t3 < ntiles_full ? t3 : t2) * CT, xb);
+      hj_load<D, R, U, false, DBG, PAD>(a, (t3 < ntiles_full ? t3 : t2) * CT, xb);
       body.template tile<false, DBG>(t2 * CT, xa, old);
       t1 = t3;
     }
   }
   if (ntiles_full * CT < a.N && wave_id == ntiles_full % nwaves) {
     const int64_t c0 = ntiles_full * CT;
-    hj_load<D, R, U, true, 0>(a, c0, xa);
+    hj_load<D, R, U, true, 0, PAD>(a, c0, xa);
     hj_load_old<D, R, U, LM>(a, c0, old, true);
     body.template tile<true, 0>(c0, xa, old);
   }
 }
 
-template <int D, int R, int U, int LM, int OCC, int DBG, int AS = 1, int VAR = 0>
+template <int D, int R, int U, int LM, int OCC, int DBG, int AS = 1, int VAR = 0, bool PAD = false>
 __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   const int n = a.n;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -591,8 +605,8 @@ __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   float* rec = reinterpret_cast<float*>(smem + kHjHeader);
   build_hj_program<D, R, AS>(a, n, rec, scr, ctotp);
   constexpr int G = HJLay<D, R, U>::G;
-  HJBody<D, R, U, LM, AS, VAR> body{a, rec + ((threadIdx.x & 63) % G) * kHjW * R, *ctotp, stage, n};
-  hj_stream<D, R, U, LM, DBG>(a, body);
+  HJBody<D, R, U, LM, AS, VAR, PAD> body{a, rec + ((threadIdx.x & 63) % G) * kHjW * R, *ctotp, stage, n};
+  hj_stream<D, R, U, LM, DBG, PAD>(a, body);
 }
 
 #if ENF_DIAG
@@ -877,8 +891,19 @@ __global__ __launch_bounds__(1024, 1) void flow_hjs_kernel(HJArgs a) {
 }
 #endif  // ENF_DIAG
 
+// fp32: the layout D (a.dk on the padded fragment path, else a.D) 32, 64 or 128
+int hj_program_pairs_f32(const FlowArgs& a) {
+  const int dl = a.dk ? a.dk : a.D;
+  if (!a.frag || (dl != 32 && dl != 64 && dl != 128) || a.nsteps < 2 || (a.nsteps & 1)) return 0;
+  for (int s = 0; s < a.nsteps; ++s) {
+    const int want = (s & 1) ? OP_JOHNSON : OP_HOUSEHOLDER;
+    if (a.steps[s].op != want) return 0;
+  }
+  return a.nsteps / 2;
+}
+
 int hj_program_pairs(const FlowArgs& a) {
-  if (!a.frag || (a.D != 32 && a.D != 64) || a.nsteps < 2 || (a.nsteps & 1)) return 0;
+  if (!a.frag || a.dk || (a.D != 32 && a.D != 64) || a.nsteps < 2 || (a.nsteps & 1)) return 0;
   for (int s = 0; s < a.nsteps; ++s) {
     const int want = (s & 1) ? OP_JOHNSON : OP_HOUSEHOLDER;
     if (a.steps[s].op != want) return 0;
@@ -902,14 +927,14 @@ static hipError_t launch_hjs(const HJArgs& h, hipStream_t st, const DeviceInfo& 
 }
 #endif
 
-template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, int AS = 1, int VAR = 0>
+template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, int AS = 1, int VAR = 0, bool PAD = false>
 static hipError_t launch_hj(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
   const size_t lds = hj_lds_bytes(D, h.n);
-  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, AS, VAR>);
+  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, AS, VAR, PAD>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)HJLay<D, R, U>::TC * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, AS, VAR>), dim3((unsigned)blocks), dim3(256), lds, st, h);
+  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, AS, VAR, PAD>), dim3((unsigned)blocks), dim3(256), lds, st, h);
   return hipGetLastError();
 }
 
@@ -927,6 +952,13 @@ static hipError_t launch_hj_as(int as, const HJArgs& a, hipStream_t st, const De
 template <int LM>
 static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, const DeviceInfo& dev) {
   (void)dbg;
+  // padded layout (round 3): D = 24 / 100 / 36 ... on the next power of two, rows past a.dreal inert
+  if (a.dreal != D) {
+    if (D == 32) return launch_hj<32, 8, 2, LM, 4, 0, 1, 0, true>(a, st, dev);
+    if (D == 64) return launch_hj<64, 8, 2, LM, 4, 0, 1, 0, true>(a, st, dev);
+    return launch_hj<128, 8, 2, LM, 4, 0, 1, 0, true>(a, st, dev);
+  }
+  if (D == 128) return launch_hj<128, 8, 2, LM, 4>(a, st, dev);
   // ENF_HJ_SPEC (diagnostics build): 1 = the wave-specialised kernel (flow_hjs_kernel, rejected), 0 = flow_hj_kernel
 #if ENF_DIAG
   static const int spec = ENF_KNOB("ENF_HJ_SPEC", kHjSpecDefault);
@@ -956,8 +988,10 @@ static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, c
 }
 
 hipError_t launch_hj_program(const FlowArgs& a, int lm, int dbg, hipStream_t st, const DeviceInfo& dev) {
-  const int n = hj_program_pairs(a);
+  const int n = hj_program_pairs_f32(a);
   if (n < 1 || n > kHjMaxPairs) return hipErrorNotSupported;
+  const int dl = a.dk ? a.dk : a.D;
+  if (dl != a.D && dbg != 0) return hipErrorNotSupported;  // (diagnostics variants: unpadded only)
   HJArgs h;
   memset(&h, 0, sizeof h);
   h.X = a.X;
@@ -965,6 +999,7 @@ hipError_t launch_hj_program(const FlowArgs& a, int lm, int dbg, hipStream_t st,
   h.ladj = a.ladj;
   h.N = a.N;
   h.n = n;
+  h.dreal = a.D;
   for (int p = 0; p < n; ++p) {
     const Step& sh = a.steps[2 * p];
     const LayerDesc& J = a.layers[a.steps[2 * p + 1].layer];
@@ -974,9 +1009,9 @@ hipError_t launch_hj_program(const FlowArgs& a, int lm, int dbg, hipStream_t st,
     h.xi[p] = (const float*)J.p[2];
     h.lam[p] = (const float*)J.p[3];
   }
-  if (lm == 0) return dispatch_hj<0>(h, a.D, dbg, st, dev);
-  if (lm == 1) return dispatch_hj<1>(h, a.D, dbg, st, dev);
-  return dispatch_hj<2>(h, a.D, dbg, st, dev);
+  if (lm == 0) return dispatch_hj<0>(h, dl, dbg, st, dev);
+  if (lm == 1) return dispatch_hj<1>(h, dl, dbg, st, dev);
+  return dispatch_hj<2>(h, dl, dbg, st, dev);
 }
 
 }  // namespace enf

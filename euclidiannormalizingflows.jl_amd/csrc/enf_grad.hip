@@ -32,12 +32,12 @@
 #include <vector>
 
 #include "enf_grad_hj.h"
+#include "enf_grad_tail.h"
 #include "enf_internal.h"
 #include "enf_train.h"
 
 namespace enf {
 
-constexpr int kMaxGradSteps = 32;
 constexpr int kMaxGradLayers = 16;
 
 struct GradArgs {
@@ -426,27 +426,11 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
   }
 }
 
-// Sum the block partials (double, block order), project Householder direction gradients, add to out.
-struct ReduceArgs {
-  const double* partial;
-  int32_t nblocks;
-  int32_t nparams;
-  int32_t D;
-  int32_t nh;  // Householder columns
-  int32_t skip_loss;  // enf_flow_vjp: out has no loss slot (out[i - 1] += tot[i])
-  void* out;
-  double* tot;  // kSumSlices x (1 + nparams) slice totals (workspace tail); slice 0 = the total
-  // per Householder column: offset of its gradient vector and its device column pointer
-  int32_t hoff[kMaxGradSteps];
-  const void* hcol[kMaxGradSteps];
-};
-
 // Sum of the block partials in kSumSlices slices (blockIdx.y): slice s covers blocks
 // [s*bs, (s+1)*bs), summed in block order per wave (b = start + w, + 4, ...) with 8 independent
 // accumulators and then over the 4 waves, in double -> tot[s][i] for the loss (i = 0) and every
 // gradient entry. grad_finalize_kernel adds the slices in order: a fixed summation tree, so the
 // result is deterministic. 64 entries per block.
-constexpr int kSumSlices = 8;
 __global__ __launch_bounds__(256) void grad_sum_kernel(ReduceArgs r) {
   __shared__ double red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -469,101 +453,35 @@ __global__ __launch_bounds__(256) void grad_sum_kernel(ReduceArgs r) {
   if (w == 0 && i < n) r.tot[(int64_t)blockIdx.y * n + i] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
-// Slices -> total, then the Householder direction projection on tot (whole block; ends with a
-// barrier, tot[0 .. nparams] final).
+// grad_sum_kernel's slice sums and, in the block that finishes last, the rest of the reduction
+// (enf_grad_tail.h sum_tail): one launch instead of two.
 template <typename T>
-__device__ __forceinline__ void finalize_totals(const ReduceArgs& r) {
-  double* tot = r.tot;
-  const int64_t n = 1 + (int64_t)r.nparams;
+__global__ __launch_bounds__(256) void grad_sum_tail_kernel(TailCtl tc) {
+  __shared__ double red[4][64];
+  const ReduceArgs& r = tc.r;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  // Householder columns h = w, w + 4, ... of this wave: their first 64 entries (one per lane; D > 64
-  // adds entries lane + 64, lane + 128, ... below) loaded while the slices are summed (they do not
-  // depend on the totals)
-  constexpr int kPerWave = (kMaxGradSteps + 3) / 4;
-  double vh[kPerWave], nrm[kPerWave];
-#pragma unroll
-  for (int j = 0; j < kPerWave; ++j) {
-    const int h = w + 4 * j;
-    vh[j] = (h < r.nh && lane < r.D) ? (double)((const T*)r.hcol[h])[lane] : 0.0;
-  }
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {  // the slices in order, into slice 0
-    double t = tot[i];
-    for (int s = 1; s < kSumSlices; ++s) t += tot[s * n + i];
-    tot[i] = t;
-  }
-#pragma unroll
-  for (int j = 0; j < kPerWave; ++j) {
-    const int h = w + 4 * j;
-    double vv = vh[j] * vh[j];
-    if (h < r.nh)
-      for (int d = lane + 64; d < r.D; d += 64) {
-        const double v = (double)((const T*)r.hcol[h])[d];
-        vv += v * v;
-      }
-    for (int m = 32; m >= 1; m >>= 1) vv += __shfl_xor(vv, m);
-    nrm[j] = sqrt(vv);
-  }
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t n = 1 + (int64_t)r.nparams;
+  const int bs = (r.nblocks + kSumSlices - 1) / kSumSlices;
+  const int b0 = (int)blockIdx.y * bs;
+  const int b1 = b0 + bs < r.nblocks ? b0 + bs : r.nblocks;
+  red[w][lane] = slice_sum_entry(r, i, b0, b1 > b0 ? b1 : b0, w);
   __syncthreads();
-  // Householder: dS/dw = -sqrt2 * G;  dS/dv = (dS/dw - w (dS/dw . w)) / |v|  (householder_trafo.jl:32)
-#pragma unroll
-  for (int j = 0; j < kPerWave; ++j) {
-    const int h = w + 4 * j;
-    if (h >= r.nh) break;  // wave-uniform
-    double* gw = tot + 1 + r.hoff[h];
-    const T* vc = (const T*)r.hcol[h];
-    const double g = lane < r.D ? gw[lane] : 0.0;
-    const double wv = vh[j] / nrm[j];
-    double wd = -1.4142135623730951 * g * wv;
-    for (int d = lane + 64; d < r.D; d += 64) wd += -1.4142135623730951 * gw[d] * ((double)vc[d] / nrm[j]);
-    for (int m = 32; m >= 1; m >>= 1) wd += __shfl_xor(wd, m);
-    if (lane < r.D) gw[lane] = (-1.4142135623730951 * g - wv * wd) / nrm[j];
-    for (int d = lane + 64; d < r.D; d += 64)
-      gw[d] = (-1.4142135623730951 * gw[d] - ((double)vc[d] / nrm[j]) * wd) / nrm[j];
-  }
-  __syncthreads();
+  if (w == 0 && i < n) r.tot[(int64_t)blockIdx.y * n + i] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  sum_tail<T>(tc);
 }
 
 // Householder direction projection and accumulation into out (one block).
 template <typename T>
 __global__ __launch_bounds__(256) void grad_finalize_kernel(ReduceArgs r) {
-  finalize_totals<T>(r);
-  T* out = (T*)r.out;
-  if (r.skip_loss) {
-    for (int i = threadIdx.x; i < r.nparams; i += blockDim.x) out[i] += (T)r.tot[1 + i];
-  } else {
-    for (int i = threadIdx.x; i < 1 + r.nparams; i += blockDim.x) out[i] += (T)r.tot[i];
-  }
+  finalize_into_out<T>(r);
 }
 
-// The rest of a single-rank optimize_whitening step in the same block (enf_whitening_step):
-// loss/B (as the host computes out[0] / B in T), ADAGrad over the trainable runs with
-// g = (T)total (what enf_adagrad_step reads from a zeroed out), then the Householder
-// re-normalisation of every batch -- the operations and roundings of the unfused sequence.
-struct StepArgs {
-  void* theta;
-  void* acc;
-  double* loss_out;
-  double scale, eta, eps;
-  int64_t D, nsamp;
-  int32_t nruns, nhb;
-  int64_t runs[kMaxStepRuns][2];
-  int64_t hb[kMaxStepHB][3];  // offset, k, ldv
-};
-
+// The rest of a single-rank optimize_whitening step in one block (enf_whitening_step), when it does not
+// run at the end of the gradient kernel (enf_grad_tail.h whitening_tail_body).
 template <typename T>
 __global__ __launch_bounds__(256) void whitening_tail_kernel(ReduceArgs r, StepArgs a) {
-  finalize_totals<T>(r);
-  const double* tot = r.tot;
-  T* th = (T*)a.theta;
-  T* ac = (T*)a.acc;
-  if (threadIdx.x == 0) *a.loss_out = (double)((T)tot[0] / (T)a.nsamp);
-  for (int q = 0; q < a.nruns; ++q)
-    for (int64_t i = a.runs[q][0] + threadIdx.x; i < a.runs[q][1]; i += blockDim.x)
-      adagrad_update<T>(th[i], ac[i], (T)tot[1 + i], (T)a.scale, (T)a.eta, (T)a.eps);
-  __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int q = 0; q < a.nhb; ++q)
-    for (int64_t c = w; c < a.hb[q][1]; c += 4) normalize_column<T>(th + a.hb[q][0] + c * a.hb[q][2], a.D, lane);
+  whitening_tail_body<T>(r, a);
 }
 
 // The update half of a data-parallel step (enf_whitening_apply): the same loss / ADAGrad /
@@ -715,8 +633,13 @@ enf_status negll_grad_workspace(bool f64, int64_t D, int64_t N, const enf_layer*
 namespace {
 
 // The per-block partials (fused (J o H)^n kernel or the generic one) and their slice sums: tot of P.ra.
+// With a tail (mode != 0, enf_grad_tail.h) what follows the slice sums (finalisation into out, or the
+// whitening step's tail) runs in the slice-sum launch itself, in its last block: *fused is set, and the
+// caller launches nothing more.
 enf_status grad_parts(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
-                      int32_t nlayers, void* workspace, size_t workspace_bytes, hipStream_t st, Plan& P) {
+                      int32_t nlayers, void* workspace, size_t workspace_bytes, hipStream_t st, Plan& P,
+                      TailCtl* tail = nullptr, bool* fused = nullptr) {
+  if (fused) *fused = false;
   enf_status s = make_plan(f64, D, N, layers, nlayers, P);
   if (s != ENF_OK) return s;
   const size_t need = ((size_t)P.blocks + kSumSlices) * (1 + (size_t)P.ga.nparams) * sizeof(double);
@@ -728,18 +651,33 @@ enf_status grad_parts(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx
   P.ra.tot = (double*)workspace + (size_t)P.blocks * (1 + (size_t)P.ga.nparams);
   hipError_t e;
   static const int generic = ENF_KNOB("ENF_GRAD_GENERIC", 0);
+  // ENF_GRAD_FUSED_TAIL=1 (diagnostics build): the finalise / whitening tail in the slice-sum launch's last
+  // block (enf_grad_tail.h sum_tail) -- measured and rejected: 50.7 vs 44.7 us per config-5 step
+  // (profiles/r03_train_sum_tail_ab.txt); the product keeps the separate launches
+  static const int fuse_knob = ENF_KNOB("ENF_GRAD_FUSED_TAIL", 0);
+  const bool fuse = tail && tail->mode != 0 && fuse_knob;
   if (!f64 && !generic && hj_grad_eligible(D, ldx, X, layers, nlayers)) {
     e = launch_hj_grad(D, N, X, layers, nlayers, P.ga.nparams, (double*)workspace, P.blocks, st);
   } else {
     if (P.lds > kGradLdsMax) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: flow too large for LDS");
     e = f64 ? launch_grad<double>(P, st) : launch_grad<float>(P, st);
   }
-  if (e == hipSuccess) {
-    hipLaunchKernelGGL(grad_sum_kernel, dim3((unsigned)((1 + P.ra.nparams + 63) / 64), kSumSlices), dim3(256), 0, st,
-                       P.ra);
+  const dim3 sgrid((unsigned)((1 + P.ra.nparams + 63) / 64), kSumSlices);
+  if (e == hipSuccess && fuse) {
+    void* const out = tail->r.out;  // set by the caller (mode 1)
+    tail->r = P.ra;
+    tail->r.out = out;
+    // a ticket row per workspace (concurrent steps on other streams use other workspaces)
+    tail->slot = (int32_t)(((uintptr_t)workspace >> 8) % kTicketSlots);
+    if (f64) hipLaunchKernelGGL((grad_sum_tail_kernel<double>), sgrid, dim3(256), 0, st, *tail);
+    else hipLaunchKernelGGL((grad_sum_tail_kernel<float>), sgrid, dim3(256), 0, st, *tail);
+    e = hipGetLastError();
+  } else if (e == hipSuccess) {
+    hipLaunchKernelGGL(grad_sum_kernel, sgrid, dim3(256), 0, st, P.ra);
     e = hipGetLastError();
   }
   if (e != hipSuccess) return set_error(ENF_ERR_HIP, hipGetErrorString(e));
+  if (fused) *fused = fuse;
   return ENF_OK;
 }
 
@@ -748,8 +686,14 @@ enf_status grad_parts(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx
 enf_status negll_grad(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
                       int32_t nlayers, void* out, void* workspace, size_t workspace_bytes, hipStream_t st) {
   Plan P;
-  enf_status s = grad_parts(f64, D, N, X, ldx, layers, nlayers, workspace, workspace_bytes, st, P);
+  TailCtl tc;
+  std::memset(&tc, 0, sizeof tc);
+  tc.mode = 1;
+  tc.r.out = out;
+  bool fused = false;
+  enf_status s = grad_parts(f64, D, N, X, ldx, layers, nlayers, workspace, workspace_bytes, st, P, &tc, &fused);
   if (s != ENF_OK) return s;
+  if (fused) return ENF_OK;
   P.ra.out = out;
   if (f64) hipLaunchKernelGGL((grad_finalize_kernel<double>), dim3(1), dim3(256), 0, st, P.ra);
   else hipLaunchKernelGGL((grad_finalize_kernel<float>), dim3(1), dim3(256), 0, st, P.ra);
@@ -861,8 +805,30 @@ enf_status whitening_step(bool f64, int64_t D, int64_t N, const void* X, int64_t
     if (a.hb[i][0] < 0 || a.hb[i][1] < 0 || a.hb[i][2] < D ||
         (a.hb[i][1] > 0 && a.hb[i][0] + (a.hb[i][1] - 1) * a.hb[i][2] + D > P.ga.nparams))
       return set_error(ENF_ERR_INVALID, "enf_whitening_step: Householder batch outside theta");
-  s = grad_parts(f64, D, N, X, ldx, layers, nlayers, workspace, workspace_bytes, st, P);
+  // the tail at the end of the gradient kernel when the step fits TailStep (config 5: one run, one batch)
+  TailCtl tc;
+  std::memset(&tc, 0, sizeof tc);
+  bool fused = false;
+  if (nruns <= kTailRuns && nhb <= kTailHB) {
+    tc.mode = 2;
+    TailStep& ts = tc.s;
+    ts.theta = a.theta;
+    ts.acc = a.acc;
+    ts.loss_out = a.loss_out;
+    ts.scale = a.scale;
+    ts.eta = a.eta;
+    ts.eps = a.eps;
+    ts.D = a.D;
+    ts.nsamp = a.nsamp;
+    ts.nruns = a.nruns;
+    ts.nhb = a.nhb;
+    for (int i = 0; i < nruns; ++i) ts.runs[i][0] = a.runs[i][0], ts.runs[i][1] = a.runs[i][1];
+    for (int i = 0; i < nhb; ++i)
+      for (int q = 0; q < 3; ++q) ts.hb[i][q] = a.hb[i][q];
+  }
+  s = grad_parts(f64, D, N, X, ldx, layers, nlayers, workspace, workspace_bytes, st, P, &tc, &fused);
   if (s != ENF_OK) return s;
+  if (fused) return ENF_OK;
   if (f64) hipLaunchKernelGGL((whitening_tail_kernel<double>), dim3(1), dim3(256), 0, st, P.ra, a);
   else hipLaunchKernelGGL((whitening_tail_kernel<float>), dim3(1), dim3(256), 0, st, P.ra, a);
   hipError_t e = hipGetLastError();

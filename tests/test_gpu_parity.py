@@ -279,11 +279,12 @@ def _hj_layers(rng, D, pairs):
     return layers
 
 
-@pytest.mark.parametrize("D", [32, 64])
+@pytest.mark.parametrize("D", [32, 64, 128, 24, 36, 100])
 @pytest.mark.parametrize("pairs", [1, 2, 3, 4, 8, 9])
 def test_hj_program_pairs_vs_oracle(enf, gpu, oracle, D, pairs):
     """The compiled (J∘H)^n program (enf_flow_hj.hip; n <= 8, n = 9 runs on the interpreter):
-    forward + ladj, plain call f(X) and multi-tile waves (N > resident tiles) against the oracle."""
+    forward + ladj, plain call f(X) and multi-tile waves (N > resident tiles) against the oracle.
+    D = 24 / 36 / 100 run on the padded layout (32 / 64 / 128, rows past D inert; round 3)."""
     rng = np.random.default_rng(100 * D + pairs)
     layers = _hj_layers(rng, D, pairs)
     N = 300_007
@@ -294,12 +295,14 @@ def test_hj_program_pairs_vs_oracle(enf, gpu, oracle, D, pairs):
     assert np.array_equal(to_np(f(colmajor_cuda(X))), to_np(Y))
 
 
-def test_hj_program_accumulate_inplace(enf, gpu, oracle):
-    """accumulate_ladj = 1 and Y aliasing X through the raw C ABI on the compiled program."""
+@pytest.mark.parametrize("D", [32, 100])
+def test_hj_program_accumulate_inplace(enf, gpu, oracle, D):
+    """accumulate_ladj = 1 and Y aliasing X through the raw C ABI on the compiled program (D = 100: the
+    padded layout)."""
     import torch
 
     rng = np.random.default_rng(5)
-    D, N = 32, 50_001
+    N = 50_001
     layers = _hj_layers(rng, D, 4)
     X = np.asfortranarray(rng.standard_normal((D, N)).astype(np.float32))
     Yr, Lr = oracle.flow_apply(layers, X)
@@ -313,7 +316,7 @@ def test_hj_program_accumulate_inplace(enf, gpu, oracle):
     assert ladj_err(L0.cpu().numpy() - 3.25, Lr) < 1e-5
 
 
-@pytest.mark.parametrize("D", [32, 64])
+@pytest.mark.parametrize("D", [32, 64, 128, 24, 100])
 def test_hj_program_exact_redo_edge_values(enf, gpu, oracle, D):
     """Columns with huge, infinite and NaN entries inside the compiled program: the tile is redone
     with the exact-range form; everything else in the batch is unaffected."""
