@@ -373,20 +373,20 @@ static int flow_ops(const FlowArgs& a) {
 
 template <typename T, int LADJ>
 static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
-  if constexpr (std::is_same_v<T, float>) {
-    // the compiled (J o H)^n program: layout D 32 / 64 / 128, the padded layout included (round 3)
+  if (a.dk) {
+    // the compiled (J o H)^n programs on the padded layout (round 3; D = 24, 36, 100, ... on 32 / 64 / 128)
     static const int nospec = ENF_KNOB("ENF_NO_SPECIALIZE", 0);
-    static const int dbg = ENF_KNOB("ENF_DEBUG_MODE", 0);
-    if (!nospec && a.dk && hj_program_pairs_f32(a) > 0) {
-      hipError_t e = launch_hj_program(a, LADJ, 0, st, dev);
+    if (!nospec && hj_program_pairs(a) > 0) {
+      hipError_t e = std::is_same_v<T, float> ? launch_hj_program(a, LADJ, 0, st, dev)
+                                              : launch_hj64_program(a, LADJ, st, dev);
       if (e != hipErrorNotSupported) return e;
     }
+    return dispatch_pad<T, LADJ>(a, lds, st, dev);
   }
-  if (a.dk) return dispatch_pad<T, LADJ>(a, lds, st, dev);
   if constexpr (std::is_same_v<T, float>) {
     static const int nospec = ENF_KNOB("ENF_NO_SPECIALIZE", 0);
     static const int dbg = ENF_KNOB("ENF_DEBUG_MODE", 0);
-    if (!nospec && hj_program_pairs_f32(a) > 0) {
+    if (!nospec && hj_program_pairs(a) > 0) {
       hipError_t e = launch_hj_program(a, LADJ, dbg, st, dev);
       if (e != hipErrorNotSupported) return e;
     }

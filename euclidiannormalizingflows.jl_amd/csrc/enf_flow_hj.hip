@@ -891,8 +891,9 @@ __global__ __launch_bounds__(1024, 1) void flow_hjs_kernel(HJArgs a) {
 }
 #endif  // ENF_DIAG
 
-// fp32: the layout D (a.dk on the padded fragment path, else a.D) 32, 64 or 128
-int hj_program_pairs_f32(const FlowArgs& a) {
+// (J o H)^n flows for the compiled programs (fp32 enf_flow_hj.hip, fp64 enf_flow_hj64.hip): the layout D
+// (a.dk on the padded fragment path, else a.D) 32, 64 or 128
+int hj_program_pairs(const FlowArgs& a) {
   const int dl = a.dk ? a.dk : a.D;
   if (!a.frag || (dl != 32 && dl != 64 && dl != 128) || a.nsteps < 2 || (a.nsteps & 1)) return 0;
   for (int s = 0; s < a.nsteps; ++s) {
@@ -902,14 +903,6 @@ int hj_program_pairs_f32(const FlowArgs& a) {
   return a.nsteps / 2;
 }
 
-int hj_program_pairs(const FlowArgs& a) {
-  if (!a.frag || a.dk || (a.D != 32 && a.D != 64) || a.nsteps < 2 || (a.nsteps & 1)) return 0;
-  for (int s = 0; s < a.nsteps; ++s) {
-    const int want = (s & 1) ? OP_JOHNSON : OP_HOUSEHOLDER;
-    if (a.steps[s].op != want) return 0;
-  }
-  return a.nsteps / 2;
-}
 
 #if ENF_DIAG
 // one block of 16 waves per CU
@@ -988,7 +981,7 @@ static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, c
 }
 
 hipError_t launch_hj_program(const FlowArgs& a, int lm, int dbg, hipStream_t st, const DeviceInfo& dev) {
-  const int n = hj_program_pairs_f32(a);
+  const int n = hj_program_pairs(a);
   if (n < 1 || n > kHjMaxPairs) return hipErrorNotSupported;
   const int dl = a.dk ? a.dk : a.D;
   if (dl != a.D && dbg != 0) return hipErrorNotSupported;  // (diagnostics variants: unpadded only)

@@ -45,7 +45,7 @@ struct HJ64Args {
   double* ladj;
   int64_t N;
   int32_t n;  // pairs
-  int32_t pad_;
+  int32_t dreal;  // rows of the batch: D, or fewer on the padded layout (PAD: rows past dreal are inert)
   const double* v[kHj64MaxPairs];
   const double* g[kHj64MaxPairs];
   const double* d[kHj64MaxPairs];
@@ -77,17 +77,23 @@ struct H64Lay {
   }
 };
 
-template <int D, int U, bool TAIL>
+// PAD (padded layout, round 3): D is the power-of-two layout, columns are a.dreal rows apart; a fragment
+// (2 rows) at or past a.dreal holds zeros and is neither loaded nor stored (a.dreal is even).
+template <int D, int U, bool TAIL, bool PAD = false>
 __device__ __forceinline__ void h64_load(const HJ64Args& a, int64_t col0, double (&x)[U][8]) {
   using L = H64Lay<D, U>;
   const int lane = threadIdx.x & 63;
+  const int64_t ld = PAD ? (int64_t)a.dreal : (int64_t)D;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t c = L::col(col0, u, lane);
 #pragma unroll
     for (int h = 0; h < L::NF; ++h) {
-      const int64_t off = c * D + L::row(h, lane);
-      if (!TAIL) {
+      const int64_t off = c * ld + L::row(h, lane);
+      if (PAD && L::row(h, lane) >= a.dreal) {
+        x[u][2 * h] = 0.0;
+        x[u][2 * h + 1] = 0.0;
+      } else if (!TAIL) {
         if (ENF_INB(c < a.N, "hj64 load X", c, a.N)) {
           const u32x4 v4 = *reinterpret_cast<const u32x4*>(a.X + off);
           __builtin_memcpy(&x[u][2 * h], &v4, 16);
@@ -112,19 +118,22 @@ __device__ __forceinline__ void h64_load_old(const HJ64Args& a, int64_t col0, do
   }
 }
 
-template <int D, int U, int LM, bool TAIL>
+template <int D, int U, int LM, bool TAIL, bool PAD = false>
 __device__ __forceinline__ void h64_store(const HJ64Args& a, double ctot, int64_t col0, const double (&x)[U][8],
                                           const double (&acc)[U], const double (&old)[H64Lay<D, U>::NLS],
                                           double* __restrict__ stage) {
   using L = H64Lay<D, U>;
   const int lane = threadIdx.x & 63;
+  const int64_t ld = PAD ? (int64_t)a.dreal : (int64_t)D;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t c = L::col(col0, u, lane);
 #pragma unroll
     for (int h = 0; h < L::NF; ++h) {
-      const int64_t off = c * D + L::row(h, lane);
-      if (!TAIL) {
+      const int64_t off = c * ld + L::row(h, lane);
+      if (PAD && L::row(h, lane) >= a.dreal) {
+        continue;
+      } else if (!TAIL) {
         u32x4 v4;
         __builtin_memcpy(&v4, &x[u][2 * h], 16);
         if (!ENF_INB(c < a.N, "hj64 store Y", c, a.N)) continue;
@@ -161,7 +170,7 @@ __device__ void build_hj64_program(const HJ64Args& a, double* __restrict__ rec, 
   for (int i = threadIdx.x; i < 3 * kLogTabN; i += blockDim.x) tab[i] = kLogTab[i];
   for (int p = wave; p < n; p += nw) {
     double vv = 0.0, cl = 0.0;
-    for (int d = lane; d < D; d += 64) {
+    for (int d = lane; d < a.dreal; d += 64) {  // the batch's rows (padded rows: neutral records below)
       const double vd = a.v[p][d];
       vv += vd * vd;
       cl += log(fabs(a.d[p][d])) - log(fabs(a.lam[p][d]));  // johnson_trafo.jl:41
@@ -180,11 +189,13 @@ __device__ void build_hj64_program(const HJ64Args& a, double* __restrict__ rec, 
     const int p = i / D, d = i % D;
     const int h = d / (D / 4), w = d % (D / 4), g = w / 2, e = w % 2;
     double* r = rec + (size_t)p * kHj64W * D + g * kHj64W * 8 + 2 * h + e;
-    r[H64_VH * 8] = a.v[p][d] * scr[2 * p];
-    r[H64_XI * 8] = a.xi[p][d];
-    r[H64_IL * 8] = 1.0 / a.lam[p][d];  // one multiply per element instead of a division (interpreter)
-    r[H64_DL * 8] = a.d[p][d];
-    r[H64_GM * 8] = a.g[p][d];
+    // a padded row (d >= dreal): vh = 0, xi = 0, 1/lambda = 1, gamma = 0 -- its zeros stay zero with q = 1
+    const bool real = d < a.dreal;
+    r[H64_VH * 8] = real ? a.v[p][d] * scr[2 * p] : 0.0;
+    r[H64_XI * 8] = real ? a.xi[p][d] : 0.0;
+    r[H64_IL * 8] = real ? 1.0 / a.lam[p][d] : 1.0;  // one multiply per element instead of a division
+    r[H64_DL * 8] = real ? a.d[p][d] : 1.0;
+    r[H64_GM * 8] = real ? a.g[p][d] : 0.0;
   }
   if (threadIdx.x == 0) {
     double c = 0.0;
@@ -269,7 +280,7 @@ __device__ __forceinline__ void h64_pair(double (&x)[U][8], double (&acc)[U], co
   }
 }
 
-template <int D, int U, int LM, bool TAIL>
+template <int D, int U, int LM, bool TAIL, bool PAD>
 __device__ __forceinline__ void h64_tile(const HJ64Args& a, const double* __restrict__ rec, const double* tab,
                                          double ctot, double* stage, int64_t col0, double (&x)[U][8],
                                          const double (&old)[H64Lay<D, U>::NLS]) {
@@ -277,10 +288,10 @@ __device__ __forceinline__ void h64_tile(const HJ64Args& a, const double* __rest
 #pragma unroll
   for (int u = 0; u < U; ++u) acc[u] = 0.0;
   for (int p = 0; p < a.n; ++p) h64_pair<D, U, (LM > 0)>(x, acc, rec + (size_t)p * kHj64W * D, tab);
-  h64_store<D, U, LM, TAIL>(a, ctot, col0, x, acc, old, stage);
+  h64_store<D, U, LM, TAIL, PAD>(a, ctot, col0, x, acc, old, stage);
 }
 
-template <int D, int U, int LM>
+template <int D, int U, int LM, bool PAD = false>
 __global__ __launch_bounds__(256) void flow_hj64_kernel(HJ64Args a) {
   using L = H64Lay<D, U>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -300,13 +311,13 @@ __global__ __launch_bounds__(256) void flow_hj64_kernel(HJ64Args a) {
   double xa[U][8], xb[U][8], old[L::NLS];
   int64_t t = wave_id;
   if (t < ntiles_full) {
-    h64_load<D, U, false>(a, t * CT, xa);
+    h64_load<D, U, false, PAD>(a, t * CT, xa);
     h64_load_old<D, U, LM>(a, t * CT, old, false);
     for (;;) {
       const int64_t t1 = t + nwaves;
       const bool more = t1 < ntiles_full;
-      h64_load<D, U, false>(a, (more ? t1 : t) * CT, xb);  // prefetch (the current tile again at the end)
-      h64_tile<D, U, LM, false>(a, myrec, tab, ctot, stage, t * CT, xa, old);
+      h64_load<D, U, false, PAD>(a, (more ? t1 : t) * CT, xb);  // prefetch (the current tile again at the end)
+      h64_tile<D, U, LM, false, PAD>(a, myrec, tab, ctot, stage, t * CT, xa, old);
       if (!more) break;
       h64_load_old<D, U, LM>(a, t1 * CT, old, false);
 #pragma unroll
@@ -318,26 +329,34 @@ __global__ __launch_bounds__(256) void flow_hj64_kernel(HJ64Args a) {
   }
   if (ntiles_full * CT < a.N && wave_id == ntiles_full % nwaves) {
     const int64_t c0 = ntiles_full * CT;
-    h64_load<D, U, true>(a, c0, xa);
+    h64_load<D, U, true, PAD>(a, c0, xa);
     h64_load_old<D, U, LM>(a, c0, old, true);
-    h64_tile<D, U, LM, true>(a, myrec, tab, ctot, stage, c0, xa, old);
+    h64_tile<D, U, LM, true, PAD>(a, myrec, tab, ctot, stage, c0, xa, old);
   }
 }
 
-template <int D, int U, int LM>
+template <int D, int U, int LM, bool PAD = false>
 static hipError_t launch_hj64(const HJ64Args& h, hipStream_t st, const DeviceInfo& dev) {
   const size_t lds = hj64_lds_bytes(D, h.n);
-  const void* k = reinterpret_cast<const void*>(&flow_hj64_kernel<D, U, LM>);
+  const void* k = reinterpret_cast<const void*>(&flow_hj64_kernel<D, U, LM, PAD>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)H64Lay<D, U>::TC * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_hj64_kernel<D, U, LM>), dim3((unsigned)blocks), dim3(256), lds, st, h);
+  hipLaunchKernelGGL((flow_hj64_kernel<D, U, LM, PAD>), dim3((unsigned)blocks), dim3(256), lds, st, h);
   return hipGetLastError();
 }
 
+template <int D, bool PAD>
+static hipError_t launch_hj64_lm(const HJ64Args& h, int lm, hipStream_t st, const DeviceInfo& dev) {
+  if (lm == 0) return launch_hj64<D, 1, 0, PAD>(h, st, dev);
+  if (lm == 1) return launch_hj64<D, 1, 1, PAD>(h, st, dev);
+  return launch_hj64<D, 1, 2, PAD>(h, st, dev);
+}
+
 hipError_t launch_hj64_program(const FlowArgs& a, int lm, hipStream_t st, const DeviceInfo& dev) {
-  const int n = hj_program_pairs(a);
+  const int n = hj_program_pairs(a);  // layout 32 / 64 / 128, padded or not
   if (n < 1 || n > kHj64MaxPairs) return hipErrorNotSupported;
+  const int dl = a.dk ? a.dk : a.D;
   HJ64Args h;
   memset(&h, 0, sizeof h);
   h.X = (const double*)a.X;
@@ -345,6 +364,7 @@ hipError_t launch_hj64_program(const FlowArgs& a, int lm, hipStream_t st, const 
   h.ladj = (double*)a.ladj;
   h.N = a.N;
   h.n = n;
+  h.dreal = a.D;
   for (int p = 0; p < n; ++p) {
     const Step& sh = a.steps[2 * p];
     const LayerDesc& J = a.layers[a.steps[2 * p + 1].layer];
@@ -354,16 +374,10 @@ hipError_t launch_hj64_program(const FlowArgs& a, int lm, hipStream_t st, const 
     h.xi[p] = (const double*)J.p[2];
     h.lam[p] = (const double*)J.p[3];
   }
-  if (a.D == 32) {
-    if (lm == 0) return launch_hj64<32, 1, 0>(h, st, dev);
-    if (lm == 1) return launch_hj64<32, 1, 1>(h, st, dev);
-    return launch_hj64<32, 1, 2>(h, st, dev);
-  }
-  if (a.D == 64) {
-    if (lm == 0) return launch_hj64<64, 1, 0>(h, st, dev);
-    if (lm == 1) return launch_hj64<64, 1, 1>(h, st, dev);
-    return launch_hj64<64, 1, 2>(h, st, dev);
-  }
+  const bool pad = dl != a.D;
+  if (dl == 32) return pad ? launch_hj64_lm<32, true>(h, lm, st, dev) : launch_hj64_lm<32, false>(h, lm, st, dev);
+  if (dl == 64) return pad ? launch_hj64_lm<64, true>(h, lm, st, dev) : launch_hj64_lm<64, false>(h, lm, st, dev);
+  if (dl == 128) return pad ? launch_hj64_lm<128, true>(h, lm, st, dev) : launch_hj64_lm<128, false>(h, lm, st, dev);
   return hipErrorNotSupported;
 }
 

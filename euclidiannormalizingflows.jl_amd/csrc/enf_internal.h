@@ -175,8 +175,7 @@ hipError_t launch_jsu_sample(bool f64, int64_t n, void* out, const double (&prm)
 
 // Compiled (J o H)^n program (enf_flow_hj.hip): n if the fp32 step table is H, J, H, J, ... (one
 // reflection per H, Johnson forward) on the fragment path with D in {32, 64}, else 0.
-int hj_program_pairs(const FlowArgs& a);      // fp64 compiled program: D 32 / 64, unpadded
-int hj_program_pairs_f32(const FlowArgs& a);  // fp32: layout D 32 / 64 / 128, padded or not
+int hj_program_pairs(const FlowArgs& a);  // (J o H)^n at layout D 32 / 64 / 128, padded or not
 // lm: 0 no ladj, 1 write, 2 accumulate; dbg: ENF_DEBUG_MODE. hipErrorNotSupported: not a program.
 hipError_t launch_hj_program(const FlowArgs& a, int lm, int dbg, hipStream_t st, const DeviceInfo& dev);
 // the same program in fp64 (enf_flow_hj64.hip); hipErrorNotSupported: not a program

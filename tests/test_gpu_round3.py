@@ -204,12 +204,13 @@ def _hj64_layers(rng, D, pairs):
     return layers
 
 
-@pytest.mark.parametrize("D", [32, 64])
+@pytest.mark.parametrize("D", [32, 64, 128, 6, 24, 100])
 @pytest.mark.parametrize("pairs", [1, 2, 4, 8, 9])
 def test_hj64_program_vs_oracle(enf, gpu, oracle, D, pairs):
     """The compiled fp64 (J∘H)^n program (enf_flow_hj64.hip; n <= 8, n = 9 runs on the interpreter):
     forward + ladj at 1e-12 against the oracle (and the x87 evaluation), ragged tail, multi-tile waves,
-    the plain call f(X) equal to the Y of the ladj call."""
+    the plain call f(X) equal to the Y of the ladj call. D = 24 / 100 run on the padded layout (32 / 128,
+    rows past D inert; round 3); D = 6 (layout 8) stays on the padded interpreter."""
     rng = np.random.default_rng(7000 + 100 * D + pairs)
     layers = _hj64_layers(rng, D, pairs)
     N = 100_003
@@ -220,16 +221,18 @@ def test_hj64_program_vs_oracle(enf, gpu, oracle, D, pairs):
     assert np.array_equal(to_np(f(colmajor_cuda(X))), to_np(Y))
 
 
-def test_hj64_program_edge_values_accumulate_inplace(enf, gpu, oracle):
+@pytest.mark.parametrize("D", [32, 100])
+def test_hj64_program_edge_values_accumulate_inplace(enf, gpu, oracle, D):
     """fp64 program: huge (>= 2^26), infinite and NaN entries follow the reference (asinh64_tab's whole
-    range, logprod64_tab's Inf / NaN); accumulate_ladj and Y aliasing X through the raw C ABI."""
+    range, logprod64_tab's Inf / NaN); accumulate_ladj and Y aliasing X through the raw C ABI (D = 100:
+    the padded layout)."""
     import torch
 
     from parity import col_err, ladj_err
     from test_gpu_parity import _raw_apply
 
     rng = np.random.default_rng(64)
-    D, N = 32, 20_001
+    N = 20_001
     layers = _hj64_layers(rng, D, 4)
     X = rng.standard_normal((D, N))
     X[3, 7] = 3e30
