@@ -55,6 +55,7 @@ def build_flow(D, pairs, np_dtype, seed=42, pattern=None):
 # clock: full-rate f32 fma/mul/add/sub and bit ops 2, half-rate ops (v_cmp, v_cndmask, v_bfi, DPP,
 # v_max/min, any SGPR source or three source VGPRs in one bank) 4, transcendentals 7.5 (3.4 vs 1.0 ns)
 ISSUE_CYC_FAST, ISSUE_CYC_TRANS = 2.0, 7.5
+ISSUE_CYC_MIX_FAST, ISSUE_CYC_MIX_TRANS = 2.35, 12.1  # inside an FMA + transcendental mix (microbench21, round 3)
 
 
 def pmc_evidence(D, N, args):
@@ -87,10 +88,16 @@ def pmc_evidence(D, N, args):
             trans = c["SQ_INSTS_VALU_TRANS_F32"]
             cyc = (ISSUE_CYC_FAST * (c["SQ_INSTS_VALU"] - trans) + ISSUE_CYC_TRANS * trans) / 1024.0
             clk, dur = tr.get("effective_clock_ghz"), tr.get("median_duration_ns_profiled")
+            # the same instructions priced at what they cost inside the loop's mix (round 3,
+            # tools/microbench21: ~2.35 cycles per full-rate and ~12.1 per transcendental instruction when the
+            # two interleave): the fraction of the launch's cycles that this instruction stream explains
+            mix = (ISSUE_CYC_MIX_FAST * (c["SQ_INSTS_VALU"] - trans) + ISSUE_CYC_MIX_TRANS * trans) / 1024.0
             valu = {"insts_per_launch": c["SQ_INSTS_VALU"], "trans_insts_per_launch": trans,
+                    "insts_per_element_pair": c["SQ_INSTS_VALU"] / (N * D * args.pairs / 64.0),
                     "issue_cycle_floor_per_simd": cyc, "pmc_effective_clock_ghz": clk,
                     "pmc_kernel_ms": dur / 1e6 if dur else None,
                     "issue_floor_frac": cyc / (clk * dur) if clk and dur else None,
+                    "mix_cost_frac": mix / (clk * dur) if clk and dur else None,
                     "wait_inst_any_frac": tr.get("SQ_WAIT_INST_ANY_frac"),
                     "lds_insts_per_launch": c.get("SQ_INSTS_LDS"),
                     "source": f"{rel} (not this run)"}
