@@ -113,17 +113,19 @@ __device__ __forceinline__ double log1p64_ge0(double t) {
 // log64_tab(u, kadd) = log(u * 2^kadd) for u >= 1 finite: u = 2^k m, m in [1, 2); j = the top B
 // fraction bits of m rounded (0..2^B), c_j = 1 + j/2^B; r = fma(m, 1/c_j, -1) (|r| <= ~2^-(B+1), one
 // rounding); log m = -log(1/c_j) + log1p(r) with the table's -log(1/c_j) in hi + lo (enf_logtab.h,
-// exact to 2^-106 for the stored 1/c_j) and log1p(r) = r + r^2 P(r) (truncation < 2^-53 r). B = 5
-// (33 entries): few distinct LDS addresses per wave, so the per-lane lookups mostly broadcast
-// instead of conflicting in the LDS banks, at two FMAs more than B = 7;
+// exact to 2^-106 for the stored 1/c_j) and log1p(r) = r + r^2 P(r) (truncation < 2^-53 r). log64_tab:
+// B = 5 (33 entries) everywhere: few distinct LDS addresses per wave, so the per-lane lookups mostly
+// broadcast. B = 7 / 8 (kLogTabB7 / B8: two / three FMAs fewer per log) were measured in config 2's kernel
+// and lost that in LDS bank conflicts (profiles/r03_c2_table_bits_nt.txt);
 // j = 0 has 1/c = 1 exactly, so log(1 + tiny) keeps full relative accuracy. tab: the table in LDS
 // (3 doubles per entry), filled by the kernel prologue.
-__device__ __forceinline__ double log64_tab(double u, int kadd, const double* __restrict__ tab) {
+template <int B>
+__device__ __forceinline__ double log64_tab_b(double u, int kadd, const double* __restrict__ tab) {
   constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
   const uint64_t b = __builtin_bit_cast(uint64_t, u);
   const uint32_t hi = (uint32_t)(b >> 32), frac = hi & 0xFFFFFu;
   const int k = (int)(hi >> 20) - 1023 + kadd;
-  const uint32_t j = (frac + (1u << (19 - kLogTabBits))) >> (20 - kLogTabBits);
+  const uint32_t j = (frac + (1u << (19 - B))) >> (20 - B);
   const double m = __builtin_bit_cast(double, ((uint64_t)(frac | 0x3FF00000u) << 32) | (uint32_t)b);
   const double* t = tab + 3 * j;
   const double r = fma(m, t[0], -1.0);
@@ -131,11 +133,15 @@ __device__ __forceinline__ double log64_tab(double u, int kadd, const double* __
   const double lhi = fma(kd, ln2_hi, t[1]);
   const double llo = fma(kd, ln2_lo, t[2]);
   // log1p(r) = r + r^2 P(r), P to r^(NP-2): |r| <= 2^-(B+1), truncation r^NP/NP < 2^-53 r
-  constexpr int NP = kLogTabBits >= 7 ? 8 : kLogTabBits >= 5 ? 10 : 12;
+  constexpr int NP = B >= 8 ? 7 : B >= 7 ? 8 : B >= 5 ? 10 : 12;
   double p = ((NP - 1) & 1 ? 1.0 : -1.0) / (NP - 1);
 #pragma unroll
   for (int n = NP - 2; n >= 2; --n) p = fma(p, r, (n & 1 ? 1.0 : -1.0) / n);
   return lhi + (r + fma(r * r, p, llo));
+}
+
+__device__ __forceinline__ double log64_tab(double u, int kadd, const double* __restrict__ tab) {
+  return log64_tab_b<kLogTabBits>(u, kadd, tab);
 }
 
 // asinh(x) over the whole double range, odd, +-Inf -> +-Inf, NaN -> NaN, with the table log:
@@ -146,6 +152,7 @@ __device__ __forceinline__ double log64_tab(double u, int kadd, const double* __
 //     is exact; c itself carries the Goldschmidt step's error of s1, up to 2^-44 s). For small a this is
 //     msun's log1p form without the log1p: u = 1 + (the rounded part) and c the rest.
 //   a >= 2^26: asinh a = log(2a) + 1/(4a^2) - ... = log(a) + ln2 within 2^-54 (kadd = 1).
+template <int B = kLogTabBits>
 __device__ __forceinline__ double asinh64_tab(double x, const double* __restrict__ tab) {
   const double a = __builtin_fabs(x);
   const bool big = a >= 67108864.0;
@@ -160,7 +167,7 @@ __device__ __forceinline__ double asinh64_tab(double x, const double* __restrict
   const double u0 = a + g;
   const double c0 = (a - (u0 - g)) + corr;
   const double cu = c0 * ((g - a) + corr);  // 1/u = s - a: g - a is exact (Sterbenz), corr completes s
-  double r = log64_tab(big ? a : u0, big ? 1 : 0, tab);
+  double r = log64_tab_b<B>(big ? a : u0, big ? 1 : 0, tab);
   r += big ? 0.0 : cu;
   r = a < __builtin_huge_val() ? r : a;  // Inf stays Inf, NaN stays NaN
   return __builtin_copysign(r, x);
@@ -169,6 +176,7 @@ __device__ __forceinline__ double asinh64_tab(double x, const double* __restrict
 // asinh64_tab for |x| < 2^26 and finite only (no range selects): the fused kernels take it for a wave whose
 // arguments are all in that range (a wave-uniform vote), asinh64_tab otherwise. Same operations and
 // roundings as asinh64_tab's a < 2^26 branch, so the same results there.
+template <int B = kLogTabBits>
 __device__ __forceinline__ double asinh64_tab_fin(double x, const double* __restrict__ tab) {
   const double a = __builtin_fabs(x);
   const double q = fma(a, a, 1.0);
@@ -182,7 +190,7 @@ __device__ __forceinline__ double asinh64_tab_fin(double x, const double* __rest
   const double u0 = a + g;
   const double c0 = (a - (u0 - g)) + corr;
   const double cu = c0 * ((g - a) + corr);
-  return __builtin_copysign(log64_tab(u0, 0, tab) + cu, x);
+  return __builtin_copysign(log64_tab_b<B>(u0, 0, tab) + cu, x);
 }
 // true when asinh64_tab_fin applies to x (|x| < 2^26; false for Inf and NaN)
 __device__ __forceinline__ bool asinh64_fin_ok(double x) { return __builtin_fabs(x) < 67108864.0; }
@@ -190,7 +198,7 @@ __device__ __forceinline__ bool asinh64_fin_ok(double x) { return __builtin_fabs
 // log(q_1 q_2 ... q_n) for n values q_i >= 1 (a fragment column segment's 1 + z^2): the exponents
 // are summed as integers and the mantissas multiplied (< 2^n), so no product overflows; +Inf if a
 // factor is +Inf, NaN if one is NaN (the reference's log(1/sqrt(Inf)) = -Inf, NaN propagation).
-template <int NQ>
+template <int NQ, int B = kLogTabBits>
 __device__ __forceinline__ double logprod64_tab(const double (&q)[NQ], const double* __restrict__ tab) {
   int ks = 0;
   double mp = 1.0, qs = 0.0;
@@ -202,7 +210,7 @@ __device__ __forceinline__ double logprod64_tab(const double (&q)[NQ], const dou
     mp *= __builtin_bit_cast(double, ((uint64_t)((hi & 0xFFFFFu) | 0x3FF00000u) << 32) | (uint32_t)b);
     qs += q[i];
   }
-  const double l = log64_tab(mp, ks, tab);
+  const double l = log64_tab_b<B>(mp, ks, tab);
   return qs < __builtin_huge_val() ? l : qs;
 }
 

@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--tag", default="")
     ap.add_argument("--product", action="store_true", help="time the shipping libenf.so instead")
+    ap.add_argument("--flush-mb", type=int, default=0,
+                    help="write a buffer of this many MB before every call (evicts the L2s and the MALL: cold-cache "
+                         "kernel times under rocprofv3; the event time then includes the writes)")
     args = ap.parse_args()
     from enf_pkg import load
     import bench
@@ -54,7 +57,11 @@ def main():
     st = torch.cuda.current_stream(dev)
     dt = lib.ENF_F32 if args.dtype == "f32" else lib.ENF_F64
 
+    flush = torch.empty(args.flush_mb << 18, device=dev, dtype=torch.float32) if args.flush_mb else None
+
     def step():
+        if flush is not None:
+            flush.fill_(1.0)
         lib.check(L.enf_flow_apply(dt, D, N, X.data_ptr(), D, Y.data_ptr(), D, ladj.data_ptr(), 0, arr, len(layers),
                                    st.cuda_stream))
 
@@ -73,7 +80,7 @@ def main():
     # bitwise fingerprint of the outputs (variants with identical arithmetic must agree exactly)
     import hashlib
     fp = hashlib.sha1(Y.cpu().numpy().tobytes() + ladj.cpu().numpy().tobytes()).hexdigest()[:16]
-    print(json.dumps({"tag": args.tag, "lib": os.path.basename(lib.LIB_PATH), "knobs": knobs, "D": D, "N": N,
+    print(json.dumps({"tag": args.tag, "flush_mb": args.flush_mb, "lib": os.path.basename(lib.LIB_PATH), "knobs": knobs, "D": D, "N": N,
                       "pairs": args.pairs, "pattern": args.pattern, "dtype": args.dtype, "kernel_ms": ms, "out_sha1": fp,
                       "samples_per_s": N / (ms * 1e-3),
                       "hbm_frac": N * (2 * D + 1) * esz / (ms * 1e-3) / 8e12}))
