@@ -318,11 +318,14 @@ static hipError_t launch_d2_u(const D2Args& h, hipStream_t st, const DeviceInfo&
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)64 * U * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  // two blocks per CU (2 waves per SIMD, ~4 tiles per wave at N = 1e6): every wave pays the prologue,
-  // so fewer, longer waves beat full occupancy (11.2 vs 11.9 us; 1 block per CU: 12.6 us,
-  // profiles/r02_c2_d2_ab.txt; ENF_BLOCKS_PER_CU overrides in the diagnostics build)
+  // three blocks per CU (3 waves per SIMD, ~2.5 tiles per wave at N = 1e6): every wave pays the prologue,
+  // so fewer, longer waves beat full occupancy. Round 2 (prologue after the tiles) measured 2 blocks best
+  // (11.2 vs 11.9 us; 1 block per CU: 12.6 us, profiles/r02_c2_d2_ab.txt); with the round-3 prologue
+  // issued ahead of the tiles, 3 blocks: 10.63 / 10.65 vs 11.30 / 11.45 us warm for 2, 10.93 vs 10.89 cold;
+  // 4 / 5 blocks 11.4 / 11.4-11.9 (profiles/r03_c2_bpc_sweep.txt). ENF_BLOCKS_PER_CU overrides in the
+  // diagnostics build.
   static const int bpc_env = ENF_KNOB("ENF_BLOCKS_PER_CU", 0);
-  const int64_t cap = (int64_t)dev.num_cu * 2;
+  const int64_t cap = (int64_t)dev.num_cu * 3;
   if (bpc_env == 0 && blocks > cap) blocks = cap;
   hipLaunchKernelGGL((flow_d2_kernel<U, LM, DBG, P, PB, TB, NT>), dim3((unsigned)blocks), dim3(256), lds, st, h);
   return hipGetLastError();
