@@ -105,6 +105,100 @@ def pmc_evidence(D, N, args):
     return None, None
 
 
+PMC_PASSES = ("FETCH_SIZE SQ_WAVES", "WRITE_SIZE",
+              "SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE",
+              "SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_LDS")
+KERNEL_PAT = "flow_hj_kernel"
+
+
+def _run_group(cmd, timeout_s, log):
+    """Run cmd in its own process group; on timeout kill the whole group (rocprofv3 and the program it
+    runs). Returns the exit status (None on timeout)."""
+    import signal
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                        "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE", "TORCHELASTIC_RUN_ID")}
+    with open(log, "w") as lf:
+        p = subprocess.Popen(cmd, stdout=lf, stderr=subprocess.STDOUT, start_new_session=True, cwd=ROOT, env=env)
+        try:
+            return p.wait(timeout=timeout_s)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            return None
+
+
+def pmc_live(D, N, args):
+    """The same PMC evidence as pmc_evidence(), collected IN THIS RUN (one GPU): after the timed region,
+    rocprofv3 runs child processes of this bench (`--no-cpu --no-train --no-pmc --steps 3 --warmup 1`,
+    the same flow, sizes and library), one counter group per pass (`--kernel-trace --pmc` only, no other
+    trace domain; each pass in its own process group under a time limit), plus one `--kernel-trace
+    --stats` pass of 20 steps whose average duration of the headline kernel is reported beside the HIP-
+    event time. Summarised as tools/pmc_summary.py does (FETCH_SIZE doubled, MI355X_MICROARCH.md §HBM).
+    Returns (traffic, valu, rocprof) or None when rocprofv3 is absent or any pass fails (the caller then
+    falls back to the committed summary, labelled "not this run")."""
+    import csv
+    import shutil
+    import tempfile
+
+    prof = shutil.which("rocprofv3")
+    if prof is None or any(k.startswith("ROCPROF") for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        return None  # no profiler, or this bench already runs under one (never nest them)
+    base = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-train", "--no-pmc",
+            "--D", str(D), "--N", str(N), "--pairs", str(args.pairs), "--dtype", args.dtype]
+    work = tempfile.mkdtemp(prefix="enf_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    per, dur = {}, []
+    for i, grp in enumerate(PMC_PASSES):
+        d = os.path.join(work, f"p{i}")
+        rc = _run_group([prof, "--kernel-trace", "--pmc", *grp.split(), "--output-format", "csv", "-d", d, "-o", "run",
+                         "--", *base, "--steps", "3", "--warmup", "1"], 120, d + ".log")
+        if rc != 0:
+            return None
+        agg = {}
+        with open(os.path.join(d, "run_counter_collection.csv")) as f:
+            for r in csv.DictReader(f):
+                if KERNEL_PAT in r["Kernel_Name"]:
+                    key = (r["Dispatch_Id"], r["Counter_Name"])
+                    agg[key] = agg.get(key, 0.0) + float(r["Counter_Value"])
+        for (_, c), v in agg.items():
+            per.setdefault(c, []).append(v)
+        with open(os.path.join(d, "run_kernel_trace.csv")) as f:
+            dur += [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(f)
+                    if KERNEL_PAT in r["Kernel_Name"]]
+    c = {k: sorted(v)[len(v) // 2] for k, v in per.items()}
+    if not dur or not all(k in c for k in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "SQ_INSTS_VALU_TRANS_F32",
+                                           "GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY")):
+        return None
+    dmed = sorted(dur)[len(dur) // 2]
+    d = os.path.join(work, "stats")
+    if _run_group([prof, "--kernel-trace", "--stats", "--output-format", "csv", "-d", d, "-o", "run",
+                   "--", *base, "--steps", "20", "--warmup", "3"], 120, d + ".log") != 0:
+        return None
+    stats = None
+    with open(os.path.join(d, "run_kernel_stats.csv")) as f:
+        for r in csv.DictReader(f):
+            if KERNEL_PAT in r["Name"]:
+                stats = {"kernel": r["Name"], "calls": int(r["Calls"]), "average_ms": float(r["AverageNs"]) / 1e6,
+                         "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6}
+    shutil.rmtree(work, ignore_errors=True)
+    src = "this run: rocprofv3 --kernel-trace --pmc passes over child runs of this bench (same flow and sizes)"
+    hbm = c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024
+    traffic = {"bytes_per_launch": hbm, "source": src}
+    trans = c["SQ_INSTS_VALU_TRANS_F32"]
+    clk = c["GRBM_GUI_ACTIVE"] / 8 / dmed
+    cyc = (ISSUE_CYC_FAST * (c["SQ_INSTS_VALU"] - trans) + ISSUE_CYC_TRANS * trans) / 1024.0
+    mix = (ISSUE_CYC_MIX_FAST * (c["SQ_INSTS_VALU"] - trans) + ISSUE_CYC_MIX_TRANS * trans) / 1024.0
+    valu = {"insts_per_launch": c["SQ_INSTS_VALU"], "trans_insts_per_launch": trans,
+            "insts_per_element_pair": c["SQ_INSTS_VALU"] / (N * D * args.pairs / 64.0),
+            "issue_cycle_floor_per_simd": cyc, "pmc_effective_clock_ghz": clk, "pmc_kernel_ms": dmed / 1e6,
+            "issue_floor_frac": cyc / (clk * dmed), "mix_cost_frac": mix / (clk * dmed),
+            "wait_inst_any_frac": c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"],
+            "lds_insts_per_launch": c.get("SQ_INSTS_LDS"), "source": src}
+    return traffic, valu, stats
+
+
 def max_over_ranks(values, device, world):
     """Element-wise max over ranks of per-rank values (the timed region's wall time and kernel
     time): the whole job is as slow as its slowest GPU. torch.distributed all-reduce(MAX)
@@ -141,6 +235,8 @@ def main():
     ap.add_argument("--no-train", action="store_true", help="skip the config-5 training leg (`train` object)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of each CPU baseline leg")
     ap.add_argument("--pattern", default=None, help="diagnostic layer pattern, e.g. HHHHHHHH (overrides --pairs)")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the in-run rocprofv3 PMC passes (one GPU; report the committed summary instead)")
     ap.add_argument("--selftest-cpu", action="store_true",
                     help="CPU tests only: the launch / barrier / max-over-ranks harness on gloo with a CPU "
                          "stand-in step (measures nothing)")
@@ -241,7 +337,18 @@ def main():
 
     bytes_per_launch = N * (2 * D + 1) * esz  # read X, write Y, write ladj
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    traffic, valu = (None, None) if args.selftest_cpu else pmc_evidence(D, N, args)
+    traffic, valu, rocprof = None, None, None
+    if not args.selftest_cpu:
+        live = None
+        if world == 1 and not args.no_pmc and args.pattern is None and args.dtype == "f32" and D in (32, 64, 128):
+            try:
+                live = pmc_live(D, N, args)
+            except Exception:  # noqa: BLE001 -- the committed summary below, labelled "not this run"
+                live = None
+        if live is not None:
+            traffic, valu, rocprof = live
+        else:
+            traffic, valu = pmc_evidence(D, N, args)
     copy_gbs = None if args.selftest_cpu else copy_ceiling(X, Y, stream)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.selftest_cpu:
@@ -281,7 +388,8 @@ def main():
                          "traffic_source": traffic["source"] if traffic else None,
                          "kernel_ms": kern_ms, "kernel_ms_max_rank": kern_ms_max,
                          "algorithmic_bytes_per_launch": bytes_per_launch,
-                         "torch_copy_GBps": copy_gbs, "frac_of_torch_copy": achieved / copy_gbs if copy_gbs else None},
+                         "torch_copy_GBps": copy_gbs, "frac_of_torch_copy": achieved / copy_gbs if copy_gbs else None,
+                         "rocprof_kernel_stats": rocprof},
             "valu": valu,
             "cpu_baseline": cpu,
             "train": train,

@@ -12,7 +12,7 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smok
 timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --no-cpu --no-train --steps 20 > $OUT/prof_bench.json 2> $OUT/prof.err || { tail $OUT/prof.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --no-cpu --no-train --no-pmc --steps 20 > $OUT/prof_bench.json 2> $OUT/prof.err || { tail $OUT/prof.err; exit 1; }
 timeout -k 10 300 bash tools/configs.sh > $OUT/configs.log 2>&1 || { tail $OUT/configs.log; exit 1; }
 PASSES="FETCH_SIZE;WRITE_SIZE" timeout -k 10 300 bash tools/pmc.sh || exit 1
 echo done

@@ -17,7 +17,7 @@ timeout -k 10 600 python bench.py > $OUT/r02_bench_$V.json 2> $OUT/r02_bench_$V.
 rc=$?; cat $OUT/r02_bench_$V.json; [ $rc -eq 0 ] || { tail -5 $OUT/r02_bench_$V.err; exit $rc; }
 echo "== rocprofv3 kernel trace"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$V -o run -- python bench.py --no-cpu --no-train --steps 20 > $OUT/r02_prof_bench_$V.json 2> $OUT/r02_prof_$V.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$V -o run -- python bench.py --no-cpu --no-train --no-pmc --steps 20 > $OUT/r02_prof_bench_$V.json 2> $OUT/r02_prof_$V.err
 rc=$?; [ $rc -eq 0 ] || { tail -5 $OUT/r02_prof_$V.err; exit $rc; }
 find $OUT/prof_$V -name '*kernel_stats.csv' -exec cp {} $OUT/r02_kernel_stats_$V.csv \;
 cat $OUT/r02_kernel_stats_$V.csv | head -5
@@ -30,7 +30,7 @@ PMC_PASSES=("FETCH_SIZE SQ_WAVES" "WRITE_SIZE"
 i=0
 for grp in "${PMC_PASSES[@]}"; do
   i=$((i+1))
-  mkdir -p $OUT/pmc_$V; timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/pmc_$V/p$i -o run -- python bench.py --no-cpu --no-train --steps 3 --warmup 1 > $OUT/pmc_$V/p$i.log 2>&1
+  mkdir -p $OUT/pmc_$V; timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/pmc_$V/p$i -o run -- python bench.py --no-cpu --no-train --no-pmc --steps 3 --warmup 1 > $OUT/pmc_$V/p$i.log 2>&1
   rc=$?
   [ $rc -eq 0 ] || { echo "pmc pass $i ($grp) failed rc=$rc"; tail -5 $OUT/pmc_$V/p$i.log; exit $rc; }
   echo "pass $i ok"

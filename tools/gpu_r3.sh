@@ -18,6 +18,6 @@ echo "== bench"
 timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; cat $OUT/bench.json; tail -5 $OUT/bench.err; [ $rc -eq 0 ] || { echo "bench failed rc=$rc"; exit $rc; }
 echo "== rocprofv3 kernel trace"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --no-cpu --no-train --steps 20 ${BENCH_ARGS:-} > $OUT/prof_bench.json 2> $OUT/prof.err
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --no-cpu --no-train --no-pmc --steps 20 ${BENCH_ARGS:-} > $OUT/prof_bench.json 2> $OUT/prof.err
 rc=$?; tail -3 $OUT/prof.err; [ $rc -eq 0 ] || { echo "rocprof failed rc=$rc"; exit $rc; }
 find $OUT/prof -name '*kernel_stats.csv' -exec head -5 {} \;

@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 OUT=gpurun_out/pmc
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-ARGS="${BENCH_ARGS:---no-cpu --no-train --steps 3 --warmup 1}"
+ARGS="${BENCH_ARGS:---no-cpu --no-train --no-pmc --steps 3 --warmup 1}"
 if [ "${LIST:-0}" = "1" ]; then
   timeout -k 5 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 fi

@@ -17,7 +17,7 @@ echo "== bench"
 timeout -k 10 600 python bench.py > $OUT/r03_bench_final.json 2> $OUT/r03_bench_final.err
 rc=$?; cut -c1-400 $OUT/r03_bench_final.json; [ $rc -eq 0 ] || { tail -5 $OUT/r03_bench_final.err; exit $rc; }
 echo "== rocprofv3 kernel trace"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --no-cpu --no-train --steps 20 > $OUT/r03_prof_bench_final.json 2> $OUT/r03_prof_final.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --no-cpu --no-train --no-pmc --steps 20 > $OUT/r03_prof_bench_final.json 2> $OUT/r03_prof_final.err
 rc=$?; [ $rc -eq 0 ] || { tail -5 $OUT/r03_prof_final.err; exit $rc; }
 cp $OUT/prof/run_kernel_stats.csv $OUT/r03_kernel_stats_final.csv
 head -3 $OUT/r03_kernel_stats_final.csv | cut -c1-200
@@ -28,7 +28,7 @@ PMC_PASSES=("FETCH_SIZE SQ_WAVES" "WRITE_SIZE"
 i=0
 for grp in "${PMC_PASSES[@]}"; do
   i=$((i+1))
-  mkdir -p $OUT/pmc; timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/pmc/p$i -o run -- python bench.py --no-cpu --no-train --steps 3 --warmup 1 > $OUT/pmc/p$i.log 2>&1
+  mkdir -p $OUT/pmc; timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/pmc/p$i -o run -- python bench.py --no-cpu --no-train --no-pmc --steps 3 --warmup 1 > $OUT/pmc/p$i.log 2>&1
   rc=$?; [ $rc -eq 0 ] || { echo "pmc pass $i ($grp) failed rc=$rc"; tail -5 $OUT/pmc/p$i.log; exit $rc; }
   echo "pass $i ok"
 done
