@@ -451,21 +451,55 @@ def host_info():
         info["affinity_cpus"] = len(os.sched_getaffinity(0))
     except OSError:
         pass
+    q = cgroup_cpu_quota()
+    if q is not None:
+        info["cgroup_cpu_quota"] = q
+    if os.environ.get("OMP_NUM_THREADS"):
+        info["OMP_NUM_THREADS"] = os.environ["OMP_NUM_THREADS"]
     return info
+
+
+def cgroup_cpu_quota():
+    """CPUs this process may use per the cgroup CPU bandwidth limit (v2 cpu.max, v1 cfs quota / period),
+    rounded up; None when unlimited or unknown. nproc and the affinity mask show the whole machine on a
+    shared GPU box, so the CPU baseline sizes its thread count by this."""
+    import math
+
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            return max(1, math.ceil(int(quota) / int(period)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            quota = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            period = int(f.read())
+        return max(1, math.ceil(quota / period)) if quota > 0 else None
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_baseline(layers, D, np_dtype, seconds):
     """The oracle (CPU restatement of the reference algorithm; Julia is unavailable) timed on a bounded
     sample of the same workload on this host, in two legs of ~`seconds` each: reference-structured,
     1 thread (layer by layer, materialising Y and the D x N ladj temporaries as the Julia broadcasts
-    do), and the same arithmetic on all usable host cores (OpenMP column blocks). The sample size is
+    do), and the same arithmetic on all usable host cores (OpenMP column blocks; the affinity mask capped by
+    the cgroup CPU quota). The sample size is
     calibrated on a short probe so each leg runs about `seconds`."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # bench cpu_baseline leg only
 
     oracle.build()
     info = host_info()
+    # every CPU this process may actually use: the affinity mask, capped by the cgroup CPU quota (a shared
+    # GPU box shows the whole machine in nproc / the mask; threads beyond the quota only time-slice)
     ncores = info.get("affinity_cpus") or os.cpu_count() or 1
+    if info.get("cgroup_cpu_quota"):
+        ncores = min(ncores, info["cgroup_cpu_quota"])
     rng = np.random.default_rng(1)
     probe = np.asfortranarray(rng.standard_normal((D, 20_000)).astype(np_dtype))
     t0 = time.perf_counter()
