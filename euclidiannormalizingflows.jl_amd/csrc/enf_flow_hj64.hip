@@ -291,8 +291,10 @@ __device__ __forceinline__ void h64_tile(const HJ64Args& a, const double* __rest
   h64_store<D, U, LM, TAIL, PAD>(a, ctot, col0, x, acc, old, stage);
 }
 
-template <int D, int U, int LM, bool PAD = false>
-__global__ __launch_bounds__(256) void flow_hj64_kernel(HJ64Args a) {
+// OCC: minimum waves per SIMD the register allocation must allow (1: no constraint; the D = 32 / 64 program
+// takes 140 VGPRs, 3 waves per SIMD; OCC = 4 caps it at 128)
+template <int D, int U, int LM, bool PAD = false, int OCC = 1>
+__global__ __launch_bounds__(256, OCC) void flow_hj64_kernel(HJ64Args a) {
   using L = H64Lay<D, U>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* scr = reinterpret_cast<double*>(smem);
@@ -335,19 +337,24 @@ __global__ __launch_bounds__(256) void flow_hj64_kernel(HJ64Args a) {
   }
 }
 
-template <int D, int U, int LM, bool PAD = false>
+template <int D, int U, int LM, bool PAD = false, int OCC = 1>
 static hipError_t launch_hj64(const HJ64Args& h, hipStream_t st, const DeviceInfo& dev) {
   const size_t lds = hj64_lds_bytes(D, h.n);
-  const void* k = reinterpret_cast<const void*>(&flow_hj64_kernel<D, U, LM, PAD>);
+  const void* k = reinterpret_cast<const void*>(&flow_hj64_kernel<D, U, LM, PAD, OCC>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)H64Lay<D, U>::TC * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_hj64_kernel<D, U, LM, PAD>), dim3((unsigned)blocks), dim3(256), lds, st, h);
+  hipLaunchKernelGGL((flow_hj64_kernel<D, U, LM, PAD, OCC>), dim3((unsigned)blocks), dim3(256), lds, st, h);
   return hipGetLastError();
 }
 
 template <int D, bool PAD>
 static hipError_t launch_hj64_lm(const HJ64Args& h, int lm, hipStream_t st, const DeviceInfo& dev) {
+#if ENF_DIAG
+  // ENF_HJ64_OCC (diagnostics build): 4 = the register allocation capped for 4 waves per SIMD (A/B)
+  static const int occ = ENF_KNOB("ENF_HJ64_OCC", 1);
+  if (occ == 4 && lm == 1 && !PAD && D <= 64) return launch_hj64<D, 1, 1, false, 4>(h, st, dev);
+#endif
   if (lm == 0) return launch_hj64<D, 1, 0, PAD>(h, st, dev);
   if (lm == 1) return launch_hj64<D, 1, 1, PAD>(h, st, dev);
   return launch_hj64<D, 1, 2, PAD>(h, st, dev);
