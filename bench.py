@@ -139,7 +139,6 @@ def pmc_live(D, N, args):
     event time. Summarised as tools/pmc_summary.py does (FETCH_SIZE doubled, MI355X_MICROARCH.md §HBM).
     Returns (traffic, valu, rocprof) or None when rocprofv3 is absent or any pass fails (the caller then
     falls back to the committed summary, labelled "not this run")."""
-    import csv
     import shutil
     import tempfile
 
@@ -149,6 +148,16 @@ def pmc_live(D, N, args):
     base = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-train", "--no-pmc",
             "--D", str(D), "--N", str(N), "--pairs", str(args.pairs), "--dtype", args.dtype]
     work = tempfile.mkdtemp(prefix="enf_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        return _pmc_passes(prof, base, work, N, D, args)
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
+def _pmc_passes(prof, base, work, N, D, args):
+    """pmc_live's passes and summary, in the scratch directory `work`."""
+    import csv
+
     per, dur = {}, []
     for i, grp in enumerate(PMC_PASSES):
         d = os.path.join(work, f"p{i}")
@@ -182,7 +191,6 @@ def pmc_live(D, N, args):
             if KERNEL_PAT in r["Name"]:
                 stats = {"kernel": r["Name"], "calls": int(r["Calls"]), "average_ms": float(r["AverageNs"]) / 1e6,
                          "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6}
-    shutil.rmtree(work, ignore_errors=True)
     src = "this run: rocprofv3 --kernel-trace --pmc passes over child runs of this bench (same flow and sizes)"
     hbm = c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024
     traffic = {"bytes_per_launch": hbm, "source": src}
