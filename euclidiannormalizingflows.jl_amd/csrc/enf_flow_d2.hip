@@ -178,8 +178,10 @@ __device__ __forceinline__ void d2_rem(const D2Args& a, const D2Prog& P_, const 
 // PB (diagnostics A/B): the program constants computed once per block by one wave (wave b % 4 of block b, so
 // the four SIMDs share the work) and broadcast through LDS after an LDS-only barrier, and one log table per
 // block, instead of every wave computing its own. TB: the log table's index bits (enf_logtab.h). NT: bit 0
-// nontemporal X loads, bit 1 nontemporal Y stores.
-template <int U, int LM, int DBG, int P = 2, bool PB = false, int TB = 5, int NT = 3>
+// nontemporal X loads, bit 1 nontemporal Y stores. LO (diagnostics A/B): 1 = only the first tile's load
+// before the prologue, the other P - 1 after it (every wave's first tile ahead of the later ones in the
+// memory queues).
+template <int U, int LM, int DBG, int P = 2, bool PB = false, int TB = 5, int NT = 3, int LO = 0>
 __global__ __launch_bounds__(256, U == 1 ? 8 : 4) void flow_d2_kernel(D2Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
@@ -272,12 +274,19 @@ __global__ __launch_bounds__(256, U == 1 ? 8 : 4) void flow_d2_kernel(D2Args a) 
     // the first P tiles, unconditionally (d2_load: a tile past the wave's last reads one line), so the
     // prologue's waits count only its own loads
 #pragma unroll
-    for (int k = 0; k < P; ++k) {
+    for (int k = 0; k < (LO == 1 ? 1 : P); ++k) {
       const int64_t tk = wave_id + k * nwaves;
       d2_load<U, false, DBG, NT>(a, tk * CT, lane, xs[k], tk < ntiles_full);
     }
     __builtin_amdgcn_sched_barrier(0);
     prologue();
+    if constexpr (LO == 1) {
+#pragma unroll
+      for (int k = 1; k < P; ++k) {
+        const int64_t tk = wave_id + k * nwaves;
+        d2_load<U, false, DBG, NT>(a, tk * CT, lane, xs[k], tk < ntiles_full);
+      }
+    }
     // persistent loop over groups of P tiles, P tiles in flight: compute buffer k, then refill it with the
     // tile P strides ahead. No conditionals inside a group and the remainder nested (d2_rem), so every
     // path into a tile has issued the same loads and stores before it and the vmcnt waits stay static:
@@ -311,10 +320,10 @@ bool d2_program(const FlowArgs& a) {
   return a.frag && a.D == 2 && a.nsteps == 2 && a.steps[0].op == OP_HOUSEHOLDER && a.steps[1].op == OP_JOHNSON;
 }
 
-template <int U, int LM, int DBG, int P = 2, bool PB = false, int TB = 5, int NT = 3>
+template <int U, int LM, int DBG, int P = 2, bool PB = false, int TB = 5, int NT = 3, int LO = 0>
 static hipError_t launch_d2_u(const D2Args& h, hipStream_t st, const DeviceInfo& dev) {
   const size_t lds = 4 * d2_tab_doubles(TB) * sizeof(double) + 16 * sizeof(double);
-  const void* k = reinterpret_cast<const void*>(&flow_d2_kernel<U, LM, DBG, P, PB, TB, NT>);
+  const void* k = reinterpret_cast<const void*>(&flow_d2_kernel<U, LM, DBG, P, PB, TB, NT, LO>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)64 * U * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
@@ -327,7 +336,7 @@ static hipError_t launch_d2_u(const D2Args& h, hipStream_t st, const DeviceInfo&
   static const int bpc_env = ENF_KNOB("ENF_BLOCKS_PER_CU", 0);
   const int64_t cap = (int64_t)dev.num_cu * 3;
   if (bpc_env == 0 && blocks > cap) blocks = cap;
-  hipLaunchKernelGGL((flow_d2_kernel<U, LM, DBG, P, PB, TB, NT>), dim3((unsigned)blocks), dim3(256), lds, st, h);
+  hipLaunchKernelGGL((flow_d2_kernel<U, LM, DBG, P, PB, TB, NT, LO>), dim3((unsigned)blocks), dim3(256), lds, st, h);
   return hipGetLastError();
 }
 
@@ -343,6 +352,12 @@ static hipError_t launch_d2_lm(const D2Args& h, hipStream_t st, const DeviceInfo
   static const int pb = ENF_KNOB("ENF_D2_PB", 0);
   // ENF_D2_TABB: log table index bits (5, 7, 8)
   static const int tb = ENF_KNOB("ENF_D2_TABB", 5);
+  // ENF_D2_LO=1: the first tile before the prologue, the rest after it
+  static const int lo = ENF_KNOB("ENF_D2_LO", 0);
+  if (lo == 1 && dbg == 0 && u == 2 && pb == 0 && tb == 5) {
+    if (pf == 4) return launch_d2_u<2, LM, 0, 4, false, 5, 3, 1>(h, st, dev);
+    if (pf == 3) return launch_d2_u<2, LM, 0, 3, false, 5, 3, 1>(h, st, dev);
+  }
   if (dbg == 0 && u == 2 && pb == 0 && pf == 4 && tb == 7) return launch_d2_u<2, LM, 0, 4, false, 7>(h, st, dev);
   if (dbg == 0 && u == 2 && pb == 0 && pf == 4 && tb == 8) return launch_d2_u<2, LM, 0, 4, false, 8>(h, st, dev);
   if (dbg == 2 && tb == 8) return launch_d2_u<2, LM, 2, 4, false, 8>(h, st, dev);
