@@ -434,6 +434,15 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
 #pragma unroll
       for (int e = 0; e < R; ++e) msel[u][e] = asinh2_mask(q[u][e], csign);
   }
+  // Wave priority 3 while a wave issues its sqrt / log2 group, 0 otherwise (round 3, last session): the SIMD's
+  // arbiter then issues the transcendentals of the waves in that phase first and fills the transcendental
+  // pipe's busy cycles with the other waves' FMAs, instead of picking by age. 0.682 / 0.683 / 0.686 vs
+  // 0.725 / 0.721 / 0.723 ms streaming, 0.532 / 0.548 / 0.553 vs 0.614 / 0.609 / 0.597 ms compute-only
+  // (profiles/r03_setprio_ab.jsonl). VAR bit 4 (diagnostics A/B): the previous schedule without it; bit 8:
+  // the priorities the other way round (slower).
+  constexpr bool PRIO = (VAR & 4) == 0 && (VAR & 8) == 0;
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
+  if constexpr ((VAR & 8) != 0) __builtin_amdgcn_s_setprio(0);
   if constexpr (R == 8) {
 #pragma unroll
     for (int u = 0; u < U; ++u) sqrt8(t[u], q[u]);
@@ -443,6 +452,8 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
 #pragma unroll
       for (int e = 0; e < R; ++e) t[u][e] = hw_sqrt(q[u][e]);
   }
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  if constexpr ((VAR & 8) != 0) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
   for (int u = 0; u < U; ++u) pr[u] = prod_tree<R>(q[u]);
   if constexpr (AS > 0) {  // small |z|: the Taylor form (enf_frag.h) in place of q
@@ -456,6 +467,8 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) t[u][e] = fabsf(x[u][e]) + t[u][e];
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
+  if constexpr ((VAR & 8) != 0) __builtin_amdgcn_s_setprio(0);
   if constexpr (R == 8) {
 #pragma unroll
     for (int u = 0; u < U; ++u) log2_8_inplace(t[u]);
@@ -465,6 +478,8 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
 #pragma unroll
       for (int e = 0; e < R; ++e) t[u][e] = hw_log2(t[u][e]);
   }
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  if constexpr ((VAR & 8) != 0) __builtin_amdgcn_s_setprio(2);
   if (LADJ)
 #pragma unroll
     for (int u = 0; u < U; ++u) acc[u] = fmaf(-0.5f, hw_log2(pr[u]), acc[u]);
@@ -967,6 +982,11 @@ static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, c
       if (dbg == 0 && var == 1) return launch_hj<32, 8, 2, 1, 5, 0, 1, 1>(a, st, dev);
       if (dbg == 0 && var == 2) return launch_hj<32, 8, 2, 1, 4, 0, 1, 2>(a, st, dev);
       if (dbg == 0 && var == 3) return launch_hj<32, 8, 2, 1, 5, 0, 1, 3>(a, st, dev);
+      // 4: without the s_setprio around the transcendental groups (the schedule before), 8: priorities reversed
+      if (dbg == 0 && var == 4) return launch_hj<32, 8, 2, 1, 4, 0, 1, 4>(a, st, dev);
+      if (dbg == 0 && var == 8) return launch_hj<32, 8, 2, 1, 4, 0, 1, 8>(a, st, dev);
+      if (dbg == 2 && var == 4) return launch_hj<32, 8, 2, 1, 4, 2, 1, 4>(a, st, dev);
+      if (dbg == 2 && var == 8) return launch_hj<32, 8, 2, 1, 4, 2, 1, 8>(a, st, dev);
       if (dbg == 2 && var == 1) return launch_hj<32, 8, 2, 1, 5, 2, 1, 1>(a, st, dev);
       if (dbg == 1) return launch_hj_as<1, 1>(as, a, st, dev);
       if (dbg == 2) return launch_hj_as<2, 1>(as, a, st, dev);
