@@ -405,6 +405,9 @@ template <int D, int R, int U, bool LADJ, int AS = 1, int VAR = 0>
 __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U], const float*& r, HJParams<R>& prm,
                                               uint32_t csign) {
   constexpr bool RL = !(VAR & 2);
+  // VAR bit 128 (diagnostics A/B): priority 2 through the reflection (dot, DPP reduction, z), 3 for the
+  // transcendental groups, 0 for the rest
+  if constexpr ((VAR & 128) != 0) __builtin_amdgcn_s_setprio(2);
   hj_pair_z<D, R, U, RL>(x, r, prm);
   if constexpr ((VAR & 1) && AS == 1) {
     float pr1[U];
@@ -440,8 +443,11 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
   // 0.725 / 0.721 / 0.723 ms streaming, 0.532 / 0.548 / 0.553 vs 0.614 / 0.609 / 0.597 ms compute-only
   // (profiles/r03_setprio_ab.jsonl). VAR bit 4 (diagnostics A/B): the previous schedule without it; bit 8:
   // the priorities the other way round (slower).
+  // (bits 16 / 32: only around the sqrt / only around the log2 group; 64: also around the ladj's log2)
   constexpr bool PRIO = (VAR & 4) == 0 && (VAR & 8) == 0;
-  if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
+  constexpr bool PS = PRIO && (VAR & 32) == 0, PL = PRIO && (VAR & 16) == 0;
+  if constexpr ((VAR & 128) != 0) __builtin_amdgcn_s_setprio(0);
+  if constexpr (PS) __builtin_amdgcn_s_setprio(3);
   if constexpr ((VAR & 8) != 0) __builtin_amdgcn_s_setprio(0);
   if constexpr (R == 8) {
 #pragma unroll
@@ -452,7 +458,7 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
 #pragma unroll
       for (int e = 0; e < R; ++e) t[u][e] = hw_sqrt(q[u][e]);
   }
-  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  if constexpr (PS) __builtin_amdgcn_s_setprio(0);
   if constexpr ((VAR & 8) != 0) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
   for (int u = 0; u < U; ++u) pr[u] = prod_tree<R>(q[u]);
@@ -467,7 +473,7 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) t[u][e] = fabsf(x[u][e]) + t[u][e];
-  if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
+  if constexpr (PL) __builtin_amdgcn_s_setprio(3);
   if constexpr ((VAR & 8) != 0) __builtin_amdgcn_s_setprio(0);
   if constexpr (R == 8) {
 #pragma unroll
@@ -478,11 +484,12 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
 #pragma unroll
       for (int e = 0; e < R; ++e) t[u][e] = hw_log2(t[u][e]);
   }
-  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  if constexpr (PL && (VAR & 64) == 0) __builtin_amdgcn_s_setprio(0);
   if constexpr ((VAR & 8) != 0) __builtin_amdgcn_s_setprio(2);
   if (LADJ)
 #pragma unroll
     for (int u = 0; u < U; ++u) acc[u] = fmaf(-0.5f, hw_log2(pr[u]), acc[u]);
+  if constexpr (PL && (VAR & 64) != 0) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -985,6 +992,11 @@ static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, c
       // 4: without the s_setprio around the transcendental groups (the schedule before), 8: priorities reversed
       if (dbg == 0 && var == 4) return launch_hj<32, 8, 2, 1, 4, 0, 1, 4>(a, st, dev);
       if (dbg == 0 && var == 8) return launch_hj<32, 8, 2, 1, 4, 0, 1, 8>(a, st, dev);
+      if (dbg == 0 && var == 16) return launch_hj<32, 8, 2, 1, 4, 0, 1, 16>(a, st, dev);
+      if (dbg == 0 && var == 32) return launch_hj<32, 8, 2, 1, 4, 0, 1, 32>(a, st, dev);
+      if (dbg == 0 && var == 64) return launch_hj<32, 8, 2, 1, 4, 0, 1, 64>(a, st, dev);
+      if (dbg == 0 && var == 128) return launch_hj<32, 8, 2, 1, 4, 0, 1, 128>(a, st, dev);
+      if (dbg == 0 && var == 192) return launch_hj<32, 8, 2, 1, 4, 0, 1, 192>(a, st, dev);
       if (dbg == 2 && var == 4) return launch_hj<32, 8, 2, 1, 4, 2, 1, 4>(a, st, dev);
       if (dbg == 2 && var == 8) return launch_hj<32, 8, 2, 1, 4, 2, 1, 8>(a, st, dev);
       if (dbg == 2 && var == 1) return launch_hj<32, 8, 2, 1, 5, 2, 1, 1>(a, st, dev);
