@@ -375,23 +375,27 @@ __device__ __forceinline__ float hj_johnson_slab(float (&x)[R], float& acc, uint
   for (int e = 0; e < R; ++e) q[e] = fmaf(x[e], x[e], 1.0f);
 #pragma unroll
   for (int e = 0; e < R; ++e) msel[e] = asinh2_mask(q[e], csign);
+  __builtin_amdgcn_s_setprio(3);  // the wave-priority schedule of hj_pair_fast
   if constexpr (R == 8) {
     sqrt8(t, q);
   } else {
 #pragma unroll
     for (int e = 0; e < R; ++e) t[e] = hw_sqrt(q[e]);
   }
+  __builtin_amdgcn_s_setprio(0);
   const float pr = prod_tree<R>(q);
 #pragma unroll
   for (int e = 0; e < R; ++e) q[e] = asinh2_small(x[e], q[e]);
 #pragma unroll
   for (int e = 0; e < R; ++e) t[e] = fabsf(x[e]) + t[e];
+  __builtin_amdgcn_s_setprio(3);
   if constexpr (R == 8) {
     log2_8_inplace(t);
   } else {
 #pragma unroll
     for (int e = 0; e < R; ++e) t[e] = hw_log2(t[e]);
   }
+  __builtin_amdgcn_s_setprio(0);
   if (LADJ) acc = fmaf(-0.5f, hw_log2(pr), acc);
 #pragma unroll
   for (int e = 0; e < R; ++e) x[e] = asinh2_pick(q[e], t[e], msel[e]);
