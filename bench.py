@@ -109,6 +109,7 @@ PMC_PASSES = ("FETCH_SIZE SQ_WAVES", "WRITE_SIZE",
               "SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE",
               "SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_LDS")
 KERNEL_PAT = "flow_hj_kernel"
+PMC_BUDGET_S = 180.0  # all in-run profiler passes together (bench.py's default run stays within minutes)
 
 
 def _run_group(cmd, timeout_s, log):
@@ -155,14 +156,22 @@ def pmc_live(D, N, args):
 
 
 def _pmc_passes(prof, base, work, N, D, args):
-    """pmc_live's passes and summary, in the scratch directory `work`."""
+    """pmc_live's passes and summary, in the scratch directory `work`. All passes together get PMC_BUDGET_S
+    seconds (a good pass takes 5-10 s); each pass is killed at what is left of it."""
     import csv
+
+    deadline = time.monotonic() + PMC_BUDGET_S
+
+    def left():
+        return max(1.0, min(90.0, deadline - time.monotonic()))
 
     per, dur = {}, []
     for i, grp in enumerate(PMC_PASSES):
+        if time.monotonic() >= deadline:
+            return None
         d = os.path.join(work, f"p{i}")
         rc = _run_group([prof, "--kernel-trace", "--pmc", *grp.split(), "--output-format", "csv", "-d", d, "-o", "run",
-                         "--", *base, "--steps", "3", "--warmup", "1"], 120, d + ".log")
+                         "--", *base, "--steps", "3", "--warmup", "1"], left(), d + ".log")
         if rc != 0:
             return None
         agg = {}
@@ -182,8 +191,9 @@ def _pmc_passes(prof, base, work, N, D, args):
         return None
     dmed = sorted(dur)[len(dur) // 2]
     d = os.path.join(work, "stats")
-    if _run_group([prof, "--kernel-trace", "--stats", "--output-format", "csv", "-d", d, "-o", "run",
-                   "--", *base, "--steps", "20", "--warmup", "3"], 120, d + ".log") != 0:
+    if time.monotonic() >= deadline or _run_group([prof, "--kernel-trace", "--stats", "--output-format", "csv", "-d", d,
+                                                   "-o", "run", "--", *base, "--steps", "20", "--warmup", "3"],
+                                                  left(), d + ".log") != 0:
         return None
     stats = None
     with open(os.path.join(d, "run_kernel_stats.csv")) as f:

@@ -127,3 +127,17 @@ def test_cgroup_quota_parsing(monkeypatch, tmp_path):
     assert bench.cgroup_cpu_quota() == 2
     fake_open.text = "max 100000\n"
     assert bench.cgroup_cpu_quota() is None
+
+
+def test_pmc_live_time_budget(monkeypatch, rocprof_present, tmp_path):
+    """An exhausted budget starts no further pass (each pass is also killed at what is left of it)."""
+    monkeypatch.setenv("TMPDIR", str(tmp_path))
+    monkeypatch.setattr(bench, "PMC_BUDGET_S", 0.0)
+    monkeypatch.setattr(bench, "_run_group", lambda *a: pytest.fail("a pass started past the budget"))
+    assert bench.pmc_live(32, 10_000_000, _args()) is None
+    seen = []
+    monkeypatch.setattr(bench, "PMC_BUDGET_S", 1000.0)
+    run, _ = _fake_runner()
+    monkeypatch.setattr(bench, "_run_group", lambda cmd, t, log: (seen.append(t), run(cmd, t, log))[1])
+    assert bench.pmc_live(32, 10_000_000, _args()) is not None
+    assert seen and all(0 < t <= 90.0 for t in seen)
