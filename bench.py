@@ -34,20 +34,73 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICRO
 MFMA_NOTE = "elementwise/rank-1 maps: HBM roofline (SURVEY.md §8(d))"
 
 
+LETTERS = {"S": 0, "C": 1, "K": 2, "J": 3, "I": 4, "H": 5}
+
+
+def parse_pattern(pattern):
+    """Layer letters in application order (innermost first): S = ScaleShiftTrafo, C = CenterStretch,
+    K = CenterContract, J = JohnsonTrafo, I = JohnsonTrafoInv, H = one Householder reflection, H<k> = a
+    chained HouseholderTrafo of k reflections (e.g. "H4JH4J"). Returns [(op, k)]."""
+    import re
+
+    out, pos = [], 0
+    for m in re.finditer(r"([SCKJIH])(\d*)", pattern):
+        if m.start() != pos:
+            raise ValueError(f"unknown layer letter in pattern {pattern!r} at {pos}")
+        k = int(m.group(2)) if m.group(2) else 1
+        if m.group(2) and m.group(1) != "H":
+            raise ValueError(f"only H takes a column count ({m.group(0)!r})")
+        out.append((LETTERS[m.group(1)], k))
+        pos = m.end()
+    if pos != len(pattern) or not out:
+        raise ValueError(f"bad pattern {pattern!r}")
+    return out
+
+
 def build_flow(D, pairs, np_dtype, seed=42, pattern=None):
-    """Parameters from a host RNG with seed 42 in per-layer order.
-    pattern: layer letters applied in order (H = Householder, J = Johnson); default "HJ" * pairs."""
+    """Parameters from a host RNG with seed 42 in per-layer order (the Center and ScaleShift
+    distributions of tests/parity.py rand_params). pattern: see parse_pattern; default "HJ" * pairs."""
     rng = np.random.default_rng(seed)
+    u = lambda lo, hi: rng.uniform(lo, hi, D).astype(np_dtype)
     layers = []
-    for ch in (pattern or "HJ" * pairs):
-        if ch == "H":
-            layers.append((5, [rng.standard_normal(D).astype(np_dtype)]))
-        elif ch == "J":
-            layers.append((3, [rng.uniform(-1, 1, D).astype(np_dtype), rng.uniform(0.5, 2, D).astype(np_dtype),
-                               rng.uniform(-0.5, 0.5, D).astype(np_dtype), rng.uniform(0.5, 2, D).astype(np_dtype)]))
+    for op, k in parse_pattern(pattern or "HJ" * pairs):
+        if op == 5:
+            V = rng.standard_normal((D, k)).astype(np_dtype)
+            layers.append((5, [V[:, 0] if k == 1 else np.asfortranarray(V)]))
+        elif op in (3, 4):
+            layers.append((op, [u(-1, 1), u(0.5, 2), u(-0.5, 0.5), u(0.5, 2)]))
+        elif op in (1, 2):
+            layers.append((op, [u(0, 2), u(0.5, 2), u(-0.5, 0.5)]))
         else:
-            raise ValueError(f"unknown layer letter {ch!r}")
+            layers.append((0, [(np.where(rng.random(D) < 0.5, -1, 1) * rng.uniform(0.5, 2, D)).astype(np_dtype),
+                               rng.standard_normal(D).astype(np_dtype)]))
     return layers
+
+
+def invert_layers(layers):
+    """Layers (innermost first) of inverse(f_n o ... o f_1): reversed order, each layer inverted as the
+    reference's InverseFunctions.inverse methods do (scale_shift_trafo.jl:26-30: ScaleShift(1/a, -b/a);
+    center_stretch.jl:45,69: CenterStretch <-> CenterContract; johnson_trafo.jl:82,107: JohnsonTrafo <->
+    JohnsonTrafoInv; householder_trafo.jl:153-154: the reflection columns in reverse order)."""
+    out = []
+    for op, ps in reversed(layers):
+        if op == 0:
+            ai = (1 / ps[0]).astype(ps[0].dtype)
+            out.append((0, [ai, (-ai * ps[1]).astype(ps[1].dtype)]))
+        elif op in (1, 2):
+            out.append((3 - op, ps))
+        elif op in (3, 4):
+            out.append((7 - op, ps))
+        else:
+            V = np.asarray(ps[0])
+            out.append((5, [V if V.ndim == 1 else np.asfortranarray(V[:, ::-1])]))
+    return out
+
+
+def layer_letters(layers):
+    inv = {v: k for k, v in LETTERS.items()}
+    return "".join(inv[op] + (str(np.asarray(ps[0]).shape[1]) if op == 5 and np.asarray(ps[0]).ndim == 2 else "")
+                   for op, ps in layers)
 
 
 # Issue costs of gfx950 VALU wave-instructions at 4 waves per SIMD, measured on MI355X
@@ -108,7 +161,11 @@ def pmc_evidence(D, N, args):
 PMC_PASSES = ("FETCH_SIZE SQ_WAVES", "WRITE_SIZE",
               "SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE",
               "SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_LDS")
-KERNEL_PAT = "flow_hj_kernel"
+KERNEL_PAT = "flow_hj_kernel"  # the headline kernel; --inverse: flow_hji_kernel (kernel_pat())
+
+
+def kernel_pat(args):
+    return "flow_hji_kernel" if getattr(args, "inverse", False) else KERNEL_PAT
 PMC_BUDGET_S = 180.0  # all in-run profiler passes together (bench.py's default run stays within minutes)
 
 
@@ -148,6 +205,8 @@ def pmc_live(D, N, args):
         return None  # no profiler, or this bench already runs under one (never nest them)
     base = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu", "--no-train", "--no-pmc",
             "--D", str(D), "--N", str(N), "--pairs", str(args.pairs), "--dtype", args.dtype]
+    if getattr(args, "inverse", False):
+        base.append("--inverse")
     work = tempfile.mkdtemp(prefix="enf_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
         return _pmc_passes(prof, base, work, N, D, args)
@@ -177,14 +236,14 @@ def _pmc_passes(prof, base, work, N, D, args):
         agg = {}
         with open(os.path.join(d, "run_counter_collection.csv")) as f:
             for r in csv.DictReader(f):
-                if KERNEL_PAT in r["Kernel_Name"]:
+                if kernel_pat(args) in r["Kernel_Name"]:
                     key = (r["Dispatch_Id"], r["Counter_Name"])
                     agg[key] = agg.get(key, 0.0) + float(r["Counter_Value"])
         for (_, c), v in agg.items():
             per.setdefault(c, []).append(v)
         with open(os.path.join(d, "run_kernel_trace.csv")) as f:
             dur += [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(f)
-                    if KERNEL_PAT in r["Kernel_Name"]]
+                    if kernel_pat(args) in r["Kernel_Name"]]
     c = {k: sorted(v)[len(v) // 2] for k, v in per.items()}
     if not dur or not all(k in c for k in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "SQ_INSTS_VALU_TRANS_F32",
                                            "GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY")):
@@ -198,7 +257,7 @@ def _pmc_passes(prof, base, work, N, D, args):
     stats = None
     with open(os.path.join(d, "run_kernel_stats.csv")) as f:
         for r in csv.DictReader(f):
-            if KERNEL_PAT in r["Name"]:
+            if kernel_pat(args) in r["Name"]:
                 stats = {"kernel": r["Name"], "calls": int(r["Calls"]), "average_ms": float(r["AverageNs"]) / 1e6,
                          "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6}
     src = "this run: rocprofv3 --kernel-trace --pmc passes over child runs of this bench (same flow and sizes)"
@@ -252,7 +311,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-train", action="store_true", help="skip the config-5 training leg (`train` object)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of each CPU baseline leg")
-    ap.add_argument("--pattern", default=None, help="diagnostic layer pattern, e.g. HHHHHHHH (overrides --pairs)")
+    ap.add_argument("--pattern", default=None,
+                    help="layer letters in application order (S C K J I H, H<k> = k chained reflections), e.g. "
+                         "SHK or H4JH4J (overrides --pairs)")
+    ap.add_argument("--inverse", action="store_true",
+                    help="time inverse(flow) on the forward flow's outputs (what a round trip reads)")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the in-run rocprofv3 PMC passes (one GPU; report the committed summary instead)")
     ap.add_argument("--selftest-cpu", action="store_true",
@@ -284,7 +347,8 @@ def main():
     t_dtype = torch.float32 if args.dtype == "f32" else torch.float64
     esz = 4 if args.dtype == "f32" else 8
     D, N = args.D, args.N
-    layers = build_flow(D, args.pairs, np_dtype, pattern=args.pattern)
+    fwd_layers = build_flow(D, args.pairs, np_dtype, pattern=args.pattern)
+    layers = invert_layers(fwd_layers) if args.inverse else fwd_layers
 
     if args.selftest_cpu:
         Xs = np.ones((D, min(N, 4096)), dtype=np_dtype)
@@ -309,15 +373,29 @@ def main():
         X = torch.randn((N, D), generator=g, device=dev, dtype=t_dtype)  # row-major N x D == column-major D x N
         Y = torch.empty_like(X)
         ladj = torch.empty(N, device=dev, dtype=t_dtype)
-        dparams = [[torch.from_numpy(np.ascontiguousarray(np.asarray(p))).to(dev) for p in ps] for _, ps in layers]
-        arr = (lib.Layer * len(layers))()
-        for i, ((op, ps), dp) in enumerate(zip(layers, dparams)):
-            arr[i].op, arr[i].k = op, 1 if op == 5 else 0
-            for q, t in enumerate(dp):
-                arr[i].p[q] = t.data_ptr()
+        def layer_array(lays):
+            # column-major parameter arrays (a chained Householder V: D x k, Fortran order)
+            dps = [[torch.from_numpy(np.ascontiguousarray(np.asarray(p).T)).to(dev) for p in ps] for _, ps in lays]
+            a = (lib.Layer * len(lays))()
+            for i, ((op, ps), dp) in enumerate(zip(lays, dps)):
+                a[i].op = op
+                a[i].k = (np.asarray(ps[0]).shape[1] if np.asarray(ps[0]).ndim == 2 else 1) if op == 5 else 0
+                for q, t in enumerate(dp):
+                    a[i].p[q] = t.data_ptr()
+            return a, dps
+
+        arr, dparams = layer_array(layers)
         stream = torch.cuda.current_stream(dev)
         sh = stream.cuda_stream
         dt_code = lib.ENF_F32 if args.dtype == "f32" else lib.ENF_F64
+        if args.inverse:
+            # the inverse's input is the forward flow's output (untimed): X <- forward(X); each timed step then
+            # writes inverse(X) into Y
+            farr, fdp = layer_array(fwd_layers)
+            lib.check(L.enf_flow_apply(dt_code, D, N, X.data_ptr(), D, Y.data_ptr(), D, ladj.data_ptr(), 0,
+                                       farr, len(fwd_layers), sh))
+            X, Y = Y, X
+            torch.cuda.synchronize()
 
         def step():
             lib.check(L.enf_flow_apply(dt_code, D, N, X.data_ptr(), D, Y.data_ptr(), D, ladj.data_ptr(), 0,
@@ -332,21 +410,27 @@ def main():
         torch.distributed.barrier()
     sync()
     if stream is not None:
-        # HIP events on the launch stream (torch.cuda.Event on the stream the kernel is launched on)
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        # HIP events on the launch stream (torch.cuda.Event on the stream the kernel is launched on), one
+        # between consecutive launches: the per-launch spread besides the mean
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        ev0, ev1 = evs[0], evs[-1]
     t0 = time.perf_counter()
     if stream is not None:
         ev0.record(stream)
-    for _ in range(args.steps):
+    for i in range(args.steps):
         step()
-    if stream is not None:
-        ev1.record(stream)
+        if stream is not None:
+            evs[i + 1].record(stream)
     sync()
     if world > 1:
         torch.distributed.barrier()
     sync()
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps if stream is not None else wall / args.steps * 1e3
+    per_launch = None
+    if stream is not None:
+        pl = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+        per_launch = {"min": pl[0], "median": pl[len(pl) // 2], "max": pl[-1], "launches": len(pl)}
     t_local, kern_ms_max = max_over_ranks([wall, kern_ms], dev, world)
     per_rank_kernel_ms = gather_ranks(kern_ms, dev, world, rank)
     ms_per_step = t_local / args.steps * 1e3
@@ -365,14 +449,14 @@ def main():
                 live = None
         if live is not None:
             traffic, valu, rocprof = live
-        else:
+        elif not args.inverse:
             traffic, valu = pmc_evidence(D, N, args)
     copy_gbs = None if args.selftest_cpu else copy_ceiling(X, Y, stream)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and not args.selftest_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and not args.selftest_cpu and not args.inverse:
         cpu = cpu_baseline(layers, D, np_dtype, args.cpu_seconds)
     train = None
-    headline = (D, N, args.pairs, args.dtype, args.pattern) == (32, 10_000_000, 4, "f32", None)
+    headline = (D, N, args.pairs, args.dtype, args.pattern, args.inverse) == (32, 10_000_000, 4, "f32", None, False)
     if args.selftest_cpu and not args.no_train:  # the config-5 leg's rank plumbing on gloo
         import bench_train
 
@@ -394,8 +478,11 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": ("selftest (CPU stand-in step, measures nothing)" if args.selftest_cpu else
-                     "synthetic: X ~ N(0,1) (torch Philox, seed 0x5EED+rank); params seed 42"),
-            "config": {"workload": f"{'∘'.join(reversed(args.pattern or 'HJ' * args.pairs))} composed flow "
+                     "synthetic: X ~ N(0,1) (torch Philox, seed 0x5EED+rank); params seed 42"
+                     + ("; the inverse reads forward(X)" if args.inverse else "")),
+            "config": {"workload": (f"inverse of {'∘'.join(reversed(layer_letters(fwd_layers)))} = "
+                                    if args.inverse else "")
+                                   + f"{'∘'.join(reversed(layer_letters(layers)))} composed flow "
                                    f"fwd+ladj, D={D}, N={N} per GPU",
                        "D": D, "N_per_gpu": N, "layers": len(layers), "parallelism": f"sample-shard x{world}"},
             "distributed": {"world_size": world, "backend": backend if world > 1 else None,
@@ -405,6 +492,7 @@ def main():
                          "traffic": traffic["bytes_per_launch"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
                          "kernel_ms": kern_ms, "kernel_ms_max_rank": kern_ms_max,
+                         "kernel_ms_per_launch": per_launch,
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          "torch_copy_GBps": copy_gbs, "frac_of_torch_copy": achieved / copy_gbs if copy_gbs else None,
                          "rocprof_kernel_stats": rocprof},

@@ -94,6 +94,7 @@ enf_status validate_layers(int64_t D, const enf_layer* layers, int32_t nlayers) 
 
 namespace enf {
 // enf_cpu.cpp (host-only translation unit)
+int usable_cpus();
 enf_status flow_apply_cpu(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, void* Y, int64_t ldy,
                           void* ladj, int32_t accumulate, const enf_layer* layers, int32_t nlayers, int32_t nthreads);
 // shared with enf_train.hip
@@ -359,7 +360,12 @@ struct Ring {
   RingBufs& b = lk.owns_lock() ? g_ring_cache : own;
   hipEvent_t h2d[kSlots] = {}, comp[kSlots] = {}, d2h[kSlots] = {};
   hipStream_t up = nullptr, down = nullptr;
+  hipStream_t caller = nullptr;  // set once the ring has queued work on the caller's stream
+  bool queued = false;
   ~Ring() {
+    // an error exit may leave flow kernels queued on the caller's stream that still use the slots: they
+    // finish before the slots are released or handed to the next call
+    if (queued) (void)hipStreamSynchronize(caller);
     if (up) (void)hipStreamSynchronize(up);
     if (down) (void)hipStreamSynchronize(down);
     for (int s = 0; s < kSlots; ++s) {
@@ -385,8 +391,8 @@ void host_copy_cols(char* dst, size_t ds, const char* src, size_t ss, size_t wid
     }
   };
   int nt = (int)std::min<size_t>(8, bytes >> 22);  // one thread per 4 MiB, at most 8
-  const unsigned hc = std::thread::hardware_concurrency();
-  if (hc > 0 && nt > (int)hc) nt = (int)hc;
+  const int hc = enf::usable_cpus();
+  if (nt > hc) nt = hc;
   if (nt <= 1 || cols < nt) {
     part(0, cols);
     return;
@@ -441,9 +447,11 @@ enf_status enf_flow_apply_host(enf_dtype dtype, int64_t D, int64_t N, const void
   if ((e = hipStreamCreateWithFlags(&r.up, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipStreamCreateWithFlags(&r.down, hipStreamNonBlocking)) != hipSuccess)
     return hip_fail(e, "hipStreamCreate");
-  // the ring starts after everything already queued on the caller's stream
+  // the ring starts after everything already queued on the caller's stream: the host copies out of X and
+  // into Y / ladj are not stream-ordered, so the host waits for that work (e.g. an async copy into X) first
   if ((e = hipEventRecord(r.comp[0], st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
-  if ((e = hipStreamWaitEvent(r.up, r.comp[0], 0)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
+  if ((e = hipEventSynchronize(r.comp[0])) != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+  r.caller = st;
   const char* Xc = (const char*)X;
   char* Yc = (char*)Y;
   char* Lc = (char*)ladj;
@@ -477,6 +485,7 @@ enf_status enf_flow_apply_host(enf_dtype dtype, int64_t D, int64_t N, const void
     if (e == hipSuccess) e = hipEventRecord(r.h2d[s], r.up);
     if (e == hipSuccess) e = hipStreamWaitEvent(st, r.h2d[s], 0);
     if (e != hipSuccess) return hip_fail(e, "ingest H2D");
+    r.queued = true;
     enf_status fs = enf_flow_apply(dtype, D, cols, dX, D, dX, D, ladj ? dL : nullptr, accumulate_ladj, layers,
                                    nlayers, st);
     if (fs != ENF_OK) return fs;

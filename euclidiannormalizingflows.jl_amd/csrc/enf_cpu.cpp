@@ -22,8 +22,11 @@
 //
 // Execution: column blocks of kBlock samples, each block through all layers while it sits in cache;
 // blocks are shared by worker threads (std::thread, static round-robin).
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -35,6 +38,44 @@
 namespace enf {
 
 enf_status set_error(enf_status st, const char* msg);
+
+// CPUs this process may actually use: the affinity set, capped by the cgroup CPU quota (cgroup v2 cpu.max,
+// or v1 cpu.cfs_quota_us / cpu.cfs_period_us) rounded up. std::thread::hardware_concurrency() counts every
+// hardware thread of the machine (256 on the GPU box, whose cgroup grants 16): a pool that size time-slices
+// on the quota. Queried once per process.
+int usable_cpus() {
+  static const int n = [] {
+    int cpus = 0;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = CPU_COUNT(&set);
+    if (cpus <= 0) cpus = (int)std::thread::hardware_concurrency();
+    if (cpus <= 0) cpus = 1;
+    double quota = -1.0;
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      long long period = 0;
+      if (std::fscanf(f, "%31s %lld", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0)
+        quota = std::atof(q) / (double)period;
+      std::fclose(f);
+    } else if (FILE* fq = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+      long long q = -1, period = 0;
+      if (std::fscanf(fq, "%lld", &q) != 1) q = -1;
+      std::fclose(fq);
+      if (FILE* fp = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+        if (std::fscanf(fp, "%lld", &period) != 1) period = 0;
+        std::fclose(fp);
+      }
+      if (q > 0 && period > 0) quota = (double)q / (double)period;
+    }
+    if (quota > 0.0) {
+      const int qc = std::max(1, (int)std::ceil(quota - 1e-9));
+      if (qc < cpus) cpus = qc;
+    }
+    return cpus;
+  }();
+  return n;
+}
 
 namespace {
 
@@ -232,14 +273,15 @@ enf_status flow_apply_cpu(bool f64, int64_t D, int64_t N, const void* X, int64_t
     for (int q = 0; q < 4; ++q) hl[l].p[q] = layers[l].p[q];
   }
   int nt = nthreads;
-  if (nt <= 0) {  // all hardware threads, but at least ~2^16 element-steps per thread (a thread's start
-                  // costs tens of microseconds: config 1's 1000 x 1 batch runs on the calling thread)
-    static const unsigned h = std::thread::hardware_concurrency();  // a system query: once per process
+  if (nt <= 0) {  // every CPU the process may use (usable_cpus: affinity and cgroup quota), but at least
+                  // ~2^16 element-steps per thread (a thread's start costs tens of microseconds: config 1's
+                  // 1000 x 1 batch runs on the calling thread)
+    const int h = usable_cpus();
     int64_t steps = 0;
     for (int l = 0; l < nlayers; ++l) steps += layers[l].op == ENF_OP_HOUSEHOLDER ? 2 * (int64_t)layers[l].k : 1;
     const int64_t work = N * (D > 0 ? D : 1) * (steps > 0 ? steps : 1);
     const int64_t want = 1 + work / (1 << 16);
-    nt = h > 0 ? (int)h : 1;
+    nt = h > 0 ? h : 1;
     if (want < nt) nt = (int)want;
   }
   const int64_t nblocks = (N + kBlock - 1) / kBlock;

@@ -381,6 +381,12 @@ static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, cons
                                               : launch_hj64_program(a, LADJ, st, dev);
       if (e != hipErrorNotSupported) return e;
     }
+    if constexpr (std::is_same_v<T, float>) {
+      if (!nospec && hji_program_pairs(a) > 0) {
+        hipError_t e = launch_hji_program(a, LADJ, st, dev);
+        if (e != hipErrorNotSupported) return e;
+      }
+    }
     return dispatch_pad<T, LADJ>(a, lds, st, dev);
   }
   if constexpr (std::is_same_v<T, float>) {
@@ -388,6 +394,11 @@ static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, cons
     static const int dbg = ENF_KNOB("ENF_DEBUG_MODE", 0);
     if (!nospec && hj_program_pairs(a) > 0) {
       hipError_t e = launch_hj_program(a, LADJ, dbg, st, dev);
+      if (e != hipErrorNotSupported) return e;
+    }
+    // the compiled inverse program (J^-1, H)^n (round 4)
+    if (!nospec && hji_program_pairs(a) > 0) {
+      hipError_t e = launch_hji_program(a, LADJ, st, dev);
       if (e != hipErrorNotSupported) return e;
     }
 #if ENF_DIAG

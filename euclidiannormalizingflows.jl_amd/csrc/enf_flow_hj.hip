@@ -282,18 +282,19 @@ struct HJParams {
 
 // Householder dot of every column of the tile: two independent partial chains per column (even
 // and odd rows) over the lane's R rows, then log2(G) DPP stages across the G lanes of the column.
-template <int D, int R, int U>
-__device__ __forceinline__ void hj_dots(const float (&y)[U][R], const HJParams<R>& prm, float (&dot)[U]) {
+// (Q: the record slot of vh in the parameter set P)
+template <int D, int R, int U, int Q = HJ_VH, typename P = HJParams<R>>
+__device__ __forceinline__ void hj_dots(const float (&y)[U][R], const P& prm, float (&dot)[U]) {
   constexpr int G = HJLay<D, R, U>::G;
   float d2[U][2];
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int c = 0; c < 2; ++c) d2[u][c] = prm.m(HJ_VH, c) * y[u][c];
+    for (int c = 0; c < 2; ++c) d2[u][c] = prm.m(Q, c) * y[u][c];
 #pragma unroll
   for (int e = 2; e < R; ++e)
 #pragma unroll
-    for (int u = 0; u < U; ++u) d2[u][e & 1] = fmaf(prm.m(HJ_VH, e), y[u][e], d2[u][e & 1]);
+    for (int u = 0; u < U; ++u) d2[u][e & 1] = fmaf(prm.m(Q, e), y[u][e], d2[u][e & 1]);
 #pragma unroll
   for (int u = 0; u < U; ++u) dot[u] = d2[u][0] + d2[u][1];
   if constexpr (G >= 2) {
@@ -633,6 +634,240 @@ __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   constexpr int G = HJLay<D, R, U>::G;
   HJBody<D, R, U, LM, AS, VAR, PAD> body{a, rec + ((threadIdx.x & 63) % G) * kHjW * R, *ctotp, stage, n};
   hj_stream<D, R, U, LM, DBG, PAD>(a, body);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// The inverse program (round 4): inverse(J_n o H_n o ... o J_1 o H_1) = H_1 o J_1^-1 o ... o H_n o J_n^-1
+// (src/johnson_trafo.jl:82 inverse(JohnsonTrafo) = JohnsonTrafoInv, src/householder_trafo.jl:153-154 a single
+// reflection is its own inverse), i.e. the layers J^-1, H, J^-1, H, ... applied in this order, fp32, the
+// layouts of the forward program (D = 32 / 64 / 128, padded or not), fused in one launch. Per pair p:
+//   w   = (y - gamma)/delta                  as fma(y, 1/delta, -gamma/delta)       (johnson_trafo.jl:36)
+//   sh  = sinh(w): |w| < 1/2: w (1 + w^2/6 + w^4/120 + w^6/5040) (truncation < 1e-8 relative),
+//         else (E - 1/E)/2, E = exp2(w log2 e) -- both odd in w, merged branch-free by a mask from w^2
+//   x   = lambda sh + xi                      the JohnsonTrafoInv output              (johnson_trafo.jl:36)
+//   ladj += -log|delta/lambda| + log(1 + sh^2)/2: the reference's -johnsontrafo_ladj of the output
+//         (johnson_trafo.jl:103-104), whose (x - xi)/lambda is sh up to the rounding of x; the constant part
+//         once per column (ctot), +1/2 log2 of the product of the q = 1 + sh^2 of a lane's 8 rows
+//   dot = vh'x, x -= dot vh                   householder_trafo! (householder_trafo.jl:8-11)
+// Records per pair and row {1/delta, -gamma/delta, lambda, xi, vh} (built in double); the multipliers of tile
+// registers one slot rotated (hj_rot). A tile whose q product overflows (|sh| ~ 2^16 on every row, Inf, NaN)
+// is redone from X elementwise (exact-range sinh, log2 per element: ladj +Inf where the reference's fp32
+// 1 + z^2 overflows).
+constexpr int kHjiW = 5;
+enum : int { HI_ID = 0, HI_NG = 1, HI_LM = 2, HI_XI = 3, HI_VH = 4 };
+__host__ __device__ constexpr bool hi_rotated(int q) { return q == HI_ID || q == HI_LM || q == HI_VH; }
+static size_t hji_lds_bytes(int D, int n) { return kHjHeader + (size_t)n * kHjiW * D * sizeof(float); }
+
+template <int R>
+struct HJIParams {
+  float v[kHjiW][R];
+  __device__ __forceinline__ void load(const float* r) {
+#pragma unroll
+    for (int k = 0; k < kHjiW; ++k)
+#pragma unroll
+      for (int h = 0; h < R / 4; ++h) lds_vec<float, 4>(r + k * R + 4 * h, *reinterpret_cast<float(*)[4]>(&v[k][4 * h]));
+  }
+  __device__ __forceinline__ float m(int k, int e) const { return v[k][hi_rotated(k) ? hj_rot(e) : e]; }
+};
+
+template <int D, int R>
+__device__ void build_hji_program(const HJArgs& a, int n, float* __restrict__ rec, double* __restrict__ scr,
+                                  float* ctot) {
+  constexpr int NF = R / 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int p = wave; p < n; p += nw) {  // v'v and sum_d log|delta/lambda| (johnson_trafo.jl:41) in double
+    const float* v = a.v[p];
+    double vv = 0.0, cl = 0.0;
+    for (int d = lane; d < a.dreal; d += 64) {
+      const double vd = v[d];
+      vv += vd * vd;
+      cl += log(fabs((double)a.d[p][d])) - log(fabs((double)a.lam[p][d]));
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+      vv += __shfl_xor(vv, m);
+      cl += __shfl_xor(cl, m);
+    }
+    if (lane == 0) {
+      scr[2 * p] = sqrt(2.0 / vv);
+      scr[2 * p + 1] = cl;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n * D; i += blockDim.x) {
+    const int p = i / D, d = i % D;
+    const int h = d / (D / NF), w = d % (D / NF), g = w / 4, e = w % 4;
+    float* r = rec + (size_t)p * kHjiW * D + g * kHjiW * R + 4 * h;
+    // a padded row (d >= dreal): w = 0, sh = 0, x = 0, vh = 0 -- its zeros stay zero with q = 1 (ladj 0)
+    double q[kHjiW] = {1.0, 0.0, 1.0, 0.0, 0.0};
+    if (d < a.dreal) {
+      const double id = 1.0 / (double)a.d[p][d];
+      q[HI_ID] = id;
+      q[HI_NG] = -(double)a.g[p][d] * id;
+      q[HI_LM] = (double)a.lam[p][d];
+      q[HI_XI] = (double)a.xi[p][d];
+      q[HI_VH] = (double)a.v[p][d] * scr[2 * p];
+    }
+#pragma unroll
+    for (int k = 0; k < kHjiW; ++k) r[k * R + (hi_rotated(k) ? hj_rot(e) : e)] = (float)q[k];
+  }
+  if (threadIdx.x == 0) {
+    double c = 0.0;
+    for (int p = 0; p < n; ++p) c -= scr[2 * p + 1];  // -johnsontrafo_ladj: -log|delta/lambda|
+    *ctot = (float)c;
+  }
+  __syncthreads();
+}
+
+// sinh(w) for |w| < 1/2 (the Taylor form) and w^2 < 1/4 as an all-ones mask (the integer difference of the
+// bit patterns of w^2 and 1/4 is negative exactly when w^2 < 1/4)
+__device__ __forceinline__ float sinh_small(float w, float w2) {
+  return w * fmaf(w2, fmaf(w2, fmaf(w2, 1.0f / 5040.0f, 1.0f / 120.0f), 1.0f / 6.0f), 1.0f);
+}
+__device__ __forceinline__ uint32_t sinh_small_mask(float w2) {
+  return (uint32_t)((int32_t)(__builtin_bit_cast(uint32_t, w2) - 0x3E800000u) >> 31);
+}
+
+// One pair (J^-1, H) on the register tile, fast form: returns the largest q product of a lane's rows.
+template <int D, int R, int U, bool LADJ>
+__device__ __forceinline__ float hji_pair_fast(float (&x)[U][R], float (&acc)[U], const float*& r) {
+  HJIParams<R> prm;
+  prm.load(r);
+  r += kHjiW * D;
+  float w[U][R], E[U][R], rE[U][R], pr[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < R; ++e) {
+      w[u][e] = fmaf(x[u][e], prm.m(HI_ID, e), prm.m(HI_NG, e));
+      E[u][e] = w[u][e] * (float)kLog2e;
+    }
+  // wave priority 3 around the transcendental groups, as in hj_pair_fast
+  __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if constexpr (R == 8) {
+      float t[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[e] = E[u][e];
+      exp2_8(E[u], t);
+    } else {
+#pragma unroll
+      for (int e = 0; e < R; ++e) E[u][e] = hw_exp2(E[u][e]);
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+  uint32_t msk[U][R];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < R; ++e) {
+      const float w2 = w[u][e] * w[u][e];
+      msk[u][e] = sinh_small_mask(w2);
+      w[u][e] = sinh_small(w[u][e], w2);
+    }
+  __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if constexpr (R == 8) {
+      rcp8(rE[u], E[u]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < R; ++e) rE[u][e] = hw_rcp(E[u][e]);
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+  float q[U][R];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+#pragma unroll
+    for (int e = 0; e < R; ++e) {
+      const float sh = asinh2_pick(w[u][e], (E[u][e] - rE[u][e]) * 0.5f, msk[u][e]);
+      q[u][e] = fmaf(sh, sh, 1.0f);
+      x[u][e] = fmaf(prm.m(HI_LM, e), sh, prm.m(HI_XI, e));
+    }
+    pr[u] = prod_tree<R>(q[u]);
+    if (LADJ) acc[u] = fmaf(0.5f, hw_log2(pr[u]), acc[u]);
+  }
+  float dot[U];
+  hj_dots<D, R, U, HI_VH>(x, prm, dot);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(-dot[u], prm.m(HI_VH, e), x[u][e]);
+  float m = pr[0];
+#pragma unroll
+  for (int u = 1; u < U; ++u) m = fmaxf(m, pr[u]);
+  return m;
+}
+
+// The same pair elementwise over the whole fp32 range: sinh finite up to |w| ~ 89.4 (E/2 formed as
+// exp2(|w| log2 e - 1)), the ladj's log2 per element (+Inf where 1 + sh^2 overflows, as the reference's).
+template <int D, int R, int U, bool LADJ>
+__device__ __forceinline__ void hji_pair_exact(float (&x)[U][R], float (&acc)[U], const float*& r) {
+  HJIParams<R> prm;
+  prm.load(r);
+  r += kHjiW * D;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < R; ++e) {
+      const float w = fmaf(x[u][e], prm.m(HI_ID, e), prm.m(HI_NG, e));
+      const float aw = fabsf(w);
+      const float h = hw_exp2(fmaf(aw, (float)kLog2e, -1.0f));
+      const float big = copysignf(fmaf(-0.25f, hw_rcp(h), h), w);
+      const float sh = aw < 0.5f ? sinh_small(w, w * w) : big;
+      x[u][e] = fmaf(prm.m(HI_LM, e), sh, prm.m(HI_XI, e));
+      if (LADJ) acc[u] += 0.5f * hw_log2(fmaf(sh, sh, 1.0f));
+    }
+  float dot[U];
+  hj_dots<D, R, U, HI_VH>(x, prm, dot);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(-dot[u], prm.m(HI_VH, e), x[u][e]);
+}
+
+template <int D, int R, int U, int LM, bool PAD>
+struct HJIBody {
+  const HJArgs& a;
+  const float* rec;
+  float ctot;
+  float* stage;
+  int n;
+
+  template <bool TAIL, int DBG>
+  __device__ __forceinline__ void tile(int64_t col0, float (&x)[U][R], const float (&old)[HJLay<D, R, U>::NLS]) {
+    constexpr bool LADJ = LM > 0;
+    float acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = 0.f;
+    const float* r = rec;
+    float m = 0.f;
+    for (int p = 0; p < n; ++p) m = fmaxf(m, hji_pair_fast<D, R, U, LADJ>(x, acc, r));
+    m = group_max<HJLay<D, R, U>::G>(m);
+    if (__builtin_expect(!(m <= FLT_MAX), 0)) {
+      hj_load<D, R, U, TAIL, DBG, PAD>(a, col0, x);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] = 0.f;
+      r = rec;
+      for (int p = 0; p < n; ++p) hji_pair_exact<D, R, U, LADJ>(x, acc, r);
+    }
+    hj_store<D, R, U, LM, TAIL, DBG, PAD>(a, ctot, col0, x, acc, old, stage);
+  }
+};
+
+template <int D, int R, int U, int LM, bool PAD>
+__global__ __launch_bounds__(256, 4) void flow_hji_kernel(HJArgs a) {
+  const int n = a.n;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* scr = reinterpret_cast<double*>(smem);
+  float* ctotp = reinterpret_cast<float*>(scr + 2 * kHjMaxPairs);
+  float* stage = reinterpret_cast<float*>(smem + kHjScratch) + (threadIdx.x >> 6) * kStagePerWave;
+  float* rec = reinterpret_cast<float*>(smem + kHjHeader);
+  build_hji_program<D, R>(a, n, rec, scr, ctotp);
+  constexpr int G = HJLay<D, R, U>::G;
+  HJIBody<D, R, U, LM, PAD> body{a, rec + ((threadIdx.x & 63) % G) * kHjiW * R, *ctotp, stage, n};
+  hj_stream<D, R, U, LM, 0, PAD>(a, body);
 }
 
 #if ENF_DIAG
@@ -1014,6 +1249,67 @@ static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, c
     return launch_hj<32, 8, 2, LM, 4>(a, st, dev);
   }
   return launch_hj<64, 8, 2, LM, 4>(a, st, dev);
+}
+
+// (J^-1, H)^n flows -- inverse((J o H)^n) -- for the compiled inverse program (fp32)
+int hji_program_pairs(const FlowArgs& a) {
+  const int dl = a.dk ? a.dk : a.D;
+  if (!a.frag || (dl != 32 && dl != 64 && dl != 128) || a.nsteps < 2 || (a.nsteps & 1)) return 0;
+  for (int s = 0; s < a.nsteps; ++s) {
+    const int want = (s & 1) ? OP_HOUSEHOLDER : OP_JOHNSON_INV;
+    if (a.steps[s].op != want) return 0;
+  }
+  return a.nsteps / 2;
+}
+
+template <int D, int LM, bool PAD>
+static hipError_t launch_hji(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
+  constexpr int R = 8, U = 2;
+  const size_t lds = hji_lds_bytes(D, h.n);
+  const void* k = reinterpret_cast<const void*>(&flow_hji_kernel<D, R, U, LM, PAD>);
+  int64_t blocks = 0;
+  hipError_t e = frag_grid(k, h.N, (int64_t)HJLay<D, R, U>::TC * 4, lds, dev, &blocks);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((flow_hji_kernel<D, R, U, LM, PAD>), dim3((unsigned)blocks), dim3(256), lds, st, h);
+  return hipGetLastError();
+}
+
+template <int LM>
+static hipError_t dispatch_hji(const HJArgs& h, int D, hipStream_t st, const DeviceInfo& dev) {
+  if (h.dreal != D) {
+    if (D == 32) return launch_hji<32, LM, true>(h, st, dev);
+    if (D == 64) return launch_hji<64, LM, true>(h, st, dev);
+    return launch_hji<128, LM, true>(h, st, dev);
+  }
+  if (D == 32) return launch_hji<32, LM, false>(h, st, dev);
+  if (D == 64) return launch_hji<64, LM, false>(h, st, dev);
+  return launch_hji<128, LM, false>(h, st, dev);
+}
+
+hipError_t launch_hji_program(const FlowArgs& a, int lm, hipStream_t st, const DeviceInfo& dev) {
+  const int n = hji_program_pairs(a);
+  if (n < 1 || n > kHjMaxPairs) return hipErrorNotSupported;
+  HJArgs h;
+  memset(&h, 0, sizeof h);
+  h.X = a.X;
+  h.Y = a.Y;
+  h.ladj = a.ladj;
+  h.N = a.N;
+  h.n = n;
+  h.dreal = a.D;
+  for (int p = 0; p < n; ++p) {
+    const LayerDesc& J = a.layers[a.steps[2 * p].layer];
+    const Step& sh = a.steps[2 * p + 1];
+    h.v[p] = (const float*)a.layers[sh.layer].p[0] + (int64_t)sh.col * a.D;
+    h.g[p] = (const float*)J.p[0];
+    h.d[p] = (const float*)J.p[1];
+    h.xi[p] = (const float*)J.p[2];
+    h.lam[p] = (const float*)J.p[3];
+  }
+  const int dl = a.dk ? a.dk : a.D;
+  if (lm == 0) return dispatch_hji<0>(h, dl, st, dev);
+  if (lm == 1) return dispatch_hji<1>(h, dl, st, dev);
+  return dispatch_hji<2>(h, dl, st, dev);
 }
 
 hipError_t launch_hj_program(const FlowArgs& a, int lm, int dbg, hipStream_t st, const DeviceInfo& dev) {

@@ -38,6 +38,8 @@ __device__ __forceinline__ float hw_rcp(float x) { return __builtin_amdgcn_rcpf(
       : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]), "=&v"(o[6]), "=&v"(o[7]) \
       : "v"(i[0]), "v"(i[1]), "v"(i[2]), "v"(i[3]), "v"(i[4]), "v"(i[5]), "v"(i[6]), "v"(i[7]))
 __device__ __forceinline__ void sqrt8(float (&o)[8], const float (&i)[8]) { ENF_TRANS8("v_sqrt_f32", o, i); }
+__device__ __forceinline__ void exp2_8(float (&o)[8], const float (&i)[8]) { ENF_TRANS8("v_exp_f32", o, i); }
+__device__ __forceinline__ void rcp8(float (&o)[8], const float (&i)[8]) { ENF_TRANS8("v_rcp_f32", o, i); }
 __device__ __forceinline__ void log2_8_inplace(float (&x)[8]) {
   asm("v_log_f32 %0, %0\nv_log_f32 %1, %1\nv_log_f32 %2, %2\nv_log_f32 %3, %3\nv_log_f32 %4, %4\n"
       "v_log_f32 %5, %5\nv_log_f32 %6, %6\nv_log_f32 %7, %7\ns_nop 0"

@@ -453,24 +453,6 @@ __global__ __launch_bounds__(256) void grad_sum_kernel(ReduceArgs r) {
   if (w == 0 && i < n) r.tot[(int64_t)blockIdx.y * n + i] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
-// grad_sum_kernel's slice sums and, in the block that finishes last, the rest of the reduction
-// (enf_grad_tail.h sum_tail): one launch instead of two.
-template <typename T>
-__global__ __launch_bounds__(256) void grad_sum_tail_kernel(TailCtl tc) {
-  __shared__ double red[4][64];
-  const ReduceArgs& r = tc.r;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
-  const int64_t n = 1 + (int64_t)r.nparams;
-  const int bs = (r.nblocks + kSumSlices - 1) / kSumSlices;
-  const int b0 = (int)blockIdx.y * bs;
-  const int b1 = b0 + bs < r.nblocks ? b0 + bs : r.nblocks;
-  red[w][lane] = slice_sum_entry(r, i, b0, b1 > b0 ? b1 : b0, w);
-  __syncthreads();
-  if (w == 0 && i < n) r.tot[(int64_t)blockIdx.y * n + i] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-  sum_tail<T>(tc);
-}
-
 // Householder direction projection and accumulation into out (one block).
 template <typename T>
 __global__ __launch_bounds__(256) void grad_finalize_kernel(ReduceArgs r) {
@@ -633,13 +615,8 @@ enf_status negll_grad_workspace(bool f64, int64_t D, int64_t N, const enf_layer*
 namespace {
 
 // The per-block partials (fused (J o H)^n kernel or the generic one) and their slice sums: tot of P.ra.
-// With a tail (mode != 0, enf_grad_tail.h) what follows the slice sums (finalisation into out, or the
-// whitening step's tail) runs in the slice-sum launch itself, in its last block: *fused is set, and the
-// caller launches nothing more.
 enf_status grad_parts(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
-                      int32_t nlayers, void* workspace, size_t workspace_bytes, hipStream_t st, Plan& P,
-                      TailCtl* tail = nullptr, bool* fused = nullptr) {
-  if (fused) *fused = false;
+                      int32_t nlayers, void* workspace, size_t workspace_bytes, hipStream_t st, Plan& P) {
   enf_status s = make_plan(f64, D, N, layers, nlayers, P);
   if (s != ENF_OK) return s;
   const size_t need = ((size_t)P.blocks + kSumSlices) * (1 + (size_t)P.ga.nparams) * sizeof(double);
@@ -651,33 +628,18 @@ enf_status grad_parts(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx
   P.ra.tot = (double*)workspace + (size_t)P.blocks * (1 + (size_t)P.ga.nparams);
   hipError_t e;
   static const int generic = ENF_KNOB("ENF_GRAD_GENERIC", 0);
-  // ENF_GRAD_FUSED_TAIL=1 (diagnostics build): the finalise / whitening tail in the slice-sum launch's last
-  // block (enf_grad_tail.h sum_tail) -- measured and rejected: 50.7 vs 44.7 us per config-5 step
-  // (profiles/r03_train_sum_tail_ab.txt); the product keeps the separate launches
-  static const int fuse_knob = ENF_KNOB("ENF_GRAD_FUSED_TAIL", 0);
-  const bool fuse = tail && tail->mode != 0 && fuse_knob;
   if (!f64 && !generic && hj_grad_eligible(D, ldx, X, layers, nlayers)) {
     e = launch_hj_grad(D, N, X, layers, nlayers, P.ga.nparams, (double*)workspace, P.blocks, st);
   } else {
     if (P.lds > kGradLdsMax) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: flow too large for LDS");
     e = f64 ? launch_grad<double>(P, st) : launch_grad<float>(P, st);
   }
-  const dim3 sgrid((unsigned)((1 + P.ra.nparams + 63) / 64), kSumSlices);
-  if (e == hipSuccess && fuse) {
-    void* const out = tail->r.out;  // set by the caller (mode 1)
-    tail->r = P.ra;
-    tail->r.out = out;
-    // a ticket row per workspace (concurrent steps on other streams use other workspaces)
-    tail->slot = (int32_t)(((uintptr_t)workspace >> 8) % kTicketSlots);
-    if (f64) hipLaunchKernelGGL((grad_sum_tail_kernel<double>), sgrid, dim3(256), 0, st, *tail);
-    else hipLaunchKernelGGL((grad_sum_tail_kernel<float>), sgrid, dim3(256), 0, st, *tail);
-    e = hipGetLastError();
-  } else if (e == hipSuccess) {
-    hipLaunchKernelGGL(grad_sum_kernel, sgrid, dim3(256), 0, st, P.ra);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(grad_sum_kernel, dim3((unsigned)((1 + P.ra.nparams + 63) / 64), kSumSlices), dim3(256), 0, st,
+                       P.ra);
     e = hipGetLastError();
   }
   if (e != hipSuccess) return set_error(ENF_ERR_HIP, hipGetErrorString(e));
-  if (fused) *fused = fuse;
   return ENF_OK;
 }
 
@@ -686,14 +648,8 @@ enf_status grad_parts(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx
 enf_status negll_grad(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
                       int32_t nlayers, void* out, void* workspace, size_t workspace_bytes, hipStream_t st) {
   Plan P;
-  TailCtl tc;
-  std::memset(&tc, 0, sizeof tc);
-  tc.mode = 1;
-  tc.r.out = out;
-  bool fused = false;
-  enf_status s = grad_parts(f64, D, N, X, ldx, layers, nlayers, workspace, workspace_bytes, st, P, &tc, &fused);
+  enf_status s = grad_parts(f64, D, N, X, ldx, layers, nlayers, workspace, workspace_bytes, st, P);
   if (s != ENF_OK) return s;
-  if (fused) return ENF_OK;
   P.ra.out = out;
   if (f64) hipLaunchKernelGGL((grad_finalize_kernel<double>), dim3(1), dim3(256), 0, st, P.ra);
   else hipLaunchKernelGGL((grad_finalize_kernel<float>), dim3(1), dim3(256), 0, st, P.ra);
@@ -805,30 +761,8 @@ enf_status whitening_step(bool f64, int64_t D, int64_t N, const void* X, int64_t
     if (a.hb[i][0] < 0 || a.hb[i][1] < 0 || a.hb[i][2] < D ||
         (a.hb[i][1] > 0 && a.hb[i][0] + (a.hb[i][1] - 1) * a.hb[i][2] + D > P.ga.nparams))
       return set_error(ENF_ERR_INVALID, "enf_whitening_step: Householder batch outside theta");
-  // the tail at the end of the gradient kernel when the step fits TailStep (config 5: one run, one batch)
-  TailCtl tc;
-  std::memset(&tc, 0, sizeof tc);
-  bool fused = false;
-  if (nruns <= kTailRuns && nhb <= kTailHB) {
-    tc.mode = 2;
-    TailStep& ts = tc.s;
-    ts.theta = a.theta;
-    ts.acc = a.acc;
-    ts.loss_out = a.loss_out;
-    ts.scale = a.scale;
-    ts.eta = a.eta;
-    ts.eps = a.eps;
-    ts.D = a.D;
-    ts.nsamp = a.nsamp;
-    ts.nruns = a.nruns;
-    ts.nhb = a.nhb;
-    for (int i = 0; i < nruns; ++i) ts.runs[i][0] = a.runs[i][0], ts.runs[i][1] = a.runs[i][1];
-    for (int i = 0; i < nhb; ++i)
-      for (int q = 0; q < 3; ++q) ts.hb[i][q] = a.hb[i][q];
-  }
-  s = grad_parts(f64, D, N, X, ldx, layers, nlayers, workspace, workspace_bytes, st, P, &tc, &fused);
+  s = grad_parts(f64, D, N, X, ldx, layers, nlayers, workspace, workspace_bytes, st, P);
   if (s != ENF_OK) return s;
-  if (fused) return ENF_OK;
   if (f64) hipLaunchKernelGGL((whitening_tail_kernel<double>), dim3(1), dim3(256), 0, st, P.ra, a);
   else hipLaunchKernelGGL((whitening_tail_kernel<float>), dim3(1), dim3(256), 0, st, P.ra, a);
   hipError_t e = hipGetLastError();

@@ -7,21 +7,11 @@
 // fused single-rank optimize_whitening step, the loss / ADAGrad / re-normalisation
 // (optimize_whitening.jl:36-42).
 //
-// Round 3, MEASURED AND REJECTED (diagnostics build, ENF_GRAD_FUSED_TAIL=1; the product launches the
-// slice sums and the finalisation / tail separately): 50.7 vs 44.7 us per config-5 step
-// (profiles/r03_train_sum_tail_ab.txt) -- on gfx950 a device-scope fence writes back and invalidates the
-// XCD's whole L2, and 88 slice-sum blocks fencing before their tickets cost more than the launch they
-// save. The mechanism: the finalisation / whitening tail runs in the slice-sum launch (grad_sum_tail_kernel): every
-// block writes its slice totals and takes a ticket (a device-scope atomic after a device-scope fence); the
-// block that takes the last ticket runs the rest. Same operations in the same order as the separate
-// kernels, so the same bits (tests/test_gpu_train.py). The tickets live in a zero-initialised device array
-// (one row per slot; the host picks the slot from the workspace address) and the last block resets its
-// row, so a launch leaves it zero for the next one and nothing has to clear it (graph replays included).
-// Measured and dropped: taking the tickets in the GRADIENT kernel (its 512 blocks each fencing, the last
-// block of each slice summing that slice): 98.7 vs 44.5 us per config-5 step
-// (profiles/r03_train_fused_tail_in_gradient_ab.txt) -- every device-scope fence writes back and
-// invalidates the XCD's L2 under the still-running gradient blocks, and one block per slice sums 64
-// partials of 641 entries alone.
+// Round 3 measured running the finalisation / whitening tail inside the slice-sum launch (a ticket taken
+// after a device-scope fence, the last block runs the rest): 50.7 vs 44.7 us per config-5 step, and in the
+// gradient kernel 98.7 vs 44.5 us -- on gfx950 each device-scope fence writes back and invalidates the XCD's
+// L2 (profiles/r03_train_sum_tail_ab.txt, r03_train_fused_tail_in_gradient_ab.txt). Rejected; round 4
+// removed that code path, so the product always launches the slice sums and the tail separately.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -63,48 +53,6 @@ struct StepArgs {
   int64_t runs[kMaxStepRuns][2];
   int64_t hb[kMaxStepHB][3];  // offset, k, ldv
 };
-
-// The fused tail's copy of StepArgs, small enough for the slice-sum kernel's arguments (config 5 has one
-// parameter run and one Householder batch); larger steps keep the separate tail kernel.
-constexpr int kTailRuns = 8, kTailHB = 4;
-struct TailStep {
-  void* theta;
-  void* acc;
-  double* loss_out;
-  double scale, eta, eps;
-  int64_t D, nsamp;
-  int32_t nruns, nhb;
-  int64_t runs[kTailRuns][2];
-  int64_t hb[kTailHB][3];
-};
-
-// mode 0: slice sums only (separate finalise / tail kernel); 1: the slice-sum launch's last block
-// finalises into r.out (enf_flow_negll_grad); 2: it runs the whitening step's tail with s
-// (enf_whitening_step).
-struct TailCtl {
-  int32_t mode;
-  int32_t slot;
-  ReduceArgs r;
-  TailStep s;
-};
-constexpr int kTicketSlots = 64;
-// zero at module load; every launch that uses a row leaves it zero
-static __device__ unsigned int g_grad_tickets[kTicketSlots][kSumSlices + 1];
-
-// grad_sum_kernel's sum of slice `slice` for the entries [c0, c0 + 64): per wave w (of 4) the blocks
-// b0 + w, b0 + w + 4, ... with 8 independent accumulators, then the 4 waves in order.
-__device__ __forceinline__ double slice_sum_entry(const ReduceArgs& r, int64_t i, int b0, int b1, int w) {
-  const int64_t n = 1 + (int64_t)r.nparams;
-  double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (i < n) {
-    int b = b0 + w;
-    for (; b + 28 < b1; b += 32)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) s8[k] += r.partial[(int64_t)(b + 4 * k) * n + i];
-    for (; b < b1; b += 4) s8[0] += r.partial[(int64_t)b * n + i];
-  }
-  return ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
-}
 
 // Slices -> total, then the Householder direction projection on tot (whole block of 4 waves; ends
 // with a barrier, tot[0 .. nparams] final).
@@ -172,7 +120,7 @@ __device__ __forceinline__ void finalize_into_out(const ReduceArgs& r) {
   }
 }
 
-// whitening_tail_kernel's work (S: StepArgs or TailStep): loss/B (as the host computes out[0] / B in T),
+// whitening_tail_kernel's work (S: StepArgs): loss/B (as the host computes out[0] / B in T),
 // ADAGrad over the trainable runs with g = (T)total (what enf_adagrad_step reads from a zeroed out), then
 // the Householder re-normalisation of every batch -- the operations and roundings of the unfused sequence.
 template <typename T, typename S>
@@ -189,24 +137,6 @@ __device__ __forceinline__ void whitening_tail_body(const ReduceArgs& r, const S
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int q = 0; q < a.nhb; ++q)
     for (int64_t c = w; c < a.hb[q][1]; c += 4) normalize_column<T>(th + a.hb[q][0] + c * a.hb[q][2], a.D, lane);
-}
-
-// Called by every thread of every slice-sum block after its slice totals are written (mode != 0): the
-// block that takes the launch's last ticket runs the rest of the reduction.
-template <typename T>
-__device__ __forceinline__ void sum_tail(const TailCtl& tc) {
-  if (tc.mode == 0) return;
-  __shared__ int s_last;
-  unsigned int* tk = g_grad_tickets[tc.slot];
-  __threadfence();  // this block's totals, device-wide, before its ticket
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&tk[0], 1u) == gridDim.x * gridDim.y - 1;
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();  // the other blocks' totals
-  if (threadIdx.x == 0) atomicExch(&tk[0], 0u);
-  if (tc.mode == 1) finalize_into_out<T>(tc.r);
-  else whitening_tail_body<T>(tc.r, tc.s);
 }
 
 }  // namespace enf

@@ -178,6 +178,8 @@ hipError_t launch_jsu_sample(bool f64, int64_t n, void* out, const double (&prm)
 int hj_program_pairs(const FlowArgs& a);  // (J o H)^n at layout D 32 / 64 / 128, padded or not
 // lm: 0 no ladj, 1 write, 2 accumulate; dbg: ENF_DEBUG_MODE. hipErrorNotSupported: not a program.
 hipError_t launch_hj_program(const FlowArgs& a, int lm, int dbg, hipStream_t st, const DeviceInfo& dev);
+int hji_program_pairs(const FlowArgs& a);  // (J^-1, H)^n -- the inverse of (J o H)^n -- at layout D 32 / 64 / 128
+hipError_t launch_hji_program(const FlowArgs& a, int lm, hipStream_t st, const DeviceInfo& dev);
 // the same program in fp64 (enf_flow_hj64.hip); hipErrorNotSupported: not a program
 hipError_t launch_hj64_program(const FlowArgs& a, int lm, hipStream_t st, const DeviceInfo& dev);
 // config 2 (J o H, D = 2, fp64): enf_flow_d2.hip
