@@ -28,6 +28,9 @@
 #include "enf_frag.h"
 #include "enf_internal.h"
 #include "enf_logtab.h"
+#if ENF_DIAG
+#include "enf_logtab_b78.h"  // the rejected B = 7 / 8 tables (ENF_D2_TABB A/B)
+#endif
 #include "enf_math64.h"
 
 namespace enf {
@@ -48,9 +51,14 @@ struct D2Args {
 constexpr int d2_tab_doubles(int B) { return 3 * ((1 << B) + 1); }
 template <int B>
 __device__ __forceinline__ const double* d2_tab_src() {
+#if ENF_DIAG
   if constexpr (B == 8) return kLogTabB8;
   else if constexpr (B == 7) return kLogTabB7;
   else return kLogTab;
+#else
+  static_assert(B == kLogTabBits, "the product build has the B = 5 table only");
+  return kLogTab;
+#endif
 }
 
 __device__ __forceinline__ double d2_readlane(double v, int l) {

@@ -48,10 +48,11 @@ def main():
     X = torch.randn((N, D), generator=g, device=dev, dtype=td)
     Y = torch.empty_like(X)
     ladj = torch.empty(N, device=dev, dtype=td)
-    dparams = [[torch.from_numpy(np.ascontiguousarray(p)).to(dev) for p in ps] for _, ps in layers]
+    dparams = [[torch.from_numpy(np.ascontiguousarray(np.asarray(p).T)).to(dev) for p in ps] for _, ps in layers]
     arr = (lib.Layer * len(layers))()
     for i, ((op, ps), dp) in enumerate(zip(layers, dparams)):
-        arr[i].op, arr[i].k = op, 1 if op == 5 else 0
+        arr[i].op = op
+        arr[i].k = (np.asarray(ps[0]).shape[1] if np.asarray(ps[0]).ndim == 2 else 1) if op == 5 else 0
         for q, t in enumerate(dp):
             arr[i].p[q] = t.data_ptr()
     st = torch.cuda.current_stream(dev)
@@ -80,8 +81,10 @@ def main():
     # bitwise fingerprint of the outputs (variants with identical arithmetic must agree exactly)
     import hashlib
     fp = hashlib.sha1(Y.cpu().numpy().tobytes() + ladj.cpu().numpy().tobytes()).hexdigest()[:16]
+    # the mailbox kernel's error word (diagnostics library: 1 = some wave ran out of polls)
+    mberr = L.enf_diag_mailbox_error() if hasattr(L, "enf_diag_mailbox_error") else None
     print(json.dumps({"tag": args.tag, "flush_mb": args.flush_mb, "lib": os.path.basename(lib.LIB_PATH), "knobs": knobs, "D": D, "N": N,
-                      "pairs": args.pairs, "pattern": args.pattern, "dtype": args.dtype, "kernel_ms": ms, "out_sha1": fp,
+                      "pairs": args.pairs, "pattern": args.pattern, "dtype": args.dtype, "kernel_ms": ms, "out_sha1": fp, "mailbox_err": mberr,
                       "samples_per_s": N / (ms * 1e-3),
                       "hbm_frac": N * (2 * D + 1) * esz / (ms * 1e-3) / 8e12}))
 
