@@ -517,9 +517,18 @@ def train_leg(dev, world, rank):
     import bench_train
 
     try:
-        return bench_train.train_leg(dev, world, rank, graph=True, comm_kind="enf")
+        res = bench_train.train_leg(dev, world, rank, graph=True, comm_kind="enf", breakdown=True)
     except Exception as e:  # noqa: BLE001 -- the headline line is printed regardless
         return {"error": f"{type(e).__name__}: {e}"}
+    if world == 1:
+        # one rank's data-parallel step at the 8-GPU share (B/8 = 12 500 columns per step): gradient, single-rank
+        # RCCL all-reduce and update, graph-captured, plus its eager per-phase breakdown
+        try:
+            s8 = bench_train.train_leg(dev, 1, 0, graph=True, comm_kind="enf", emulate_world=8, breakdown=True)
+            res["rank_share_of_8"] = {k: s8[k] for k in ("value", "ms_per_step", "step", "launch", "phases", "config")}
+        except Exception as e:  # noqa: BLE001
+            res["rank_share_of_8"] = {"error": f"{type(e).__name__}: {e}"}
+    return res
 
 
 def copy_ceiling(X, Y, stream, reps=10):

@@ -141,10 +141,16 @@ def main():
 
 
 def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps=100, warmup=5, graph=True,
-              comm_kind="enf", history=""):
+              comm_kind="enf", history="", emulate_world=None, breakdown=False):
     """Config 5 on this process's GPU as one rank of `world` (torch.distributed initialised by the
     caller when world > 1): returns the result record (the same on every rank; rank 0 prints it).
-    Also run by bench.py after its headline measurement (`train` object of its JSON line)."""
+    Also run by bench.py after its headline measurement (`train` object of its JSON line).
+    emulate_world=W (one process only): the data-parallel step of rank 0 of W ranks -- its share B/W of each
+    minibatch, the gradient, a single-rank EnfComm all-reduce and enf_whitening_apply normalised by the whole
+    minibatch B -- i.e. one rank's step at that world size without the cross-GPU transfer (the update differs
+    from a real W-rank run, which sums every share; the timing is the rank's local work).
+    breakdown=True: after the timed steps, `steps` eager steps with HIP events between the phases (gradient
+    launches, all-reduce, update; or the fused call) -> their per-phase medians."""
     import torch
 
     from enf_pkg import load
@@ -168,7 +174,9 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
     Z = torch.randn((N, D), generator=g, device=dev, dtype=torch.float32).t()
     X = enf.inverse(f_true)(Z)
     del Z
-    plan = enf.minibatch_plan(N, nbatches, rank, world)
+    if emulate_world and world != 1:
+        raise ValueError("emulate_world runs in a single process")
+    plan = enf.minibatch_plan(N, nbatches, 0 if emulate_world else rank, emulate_world or world)
     state = FlowState(f0, D, torch.float32, dev, enf.ADAGrad())
     out = torch.zeros(1 + state.nparams, dtype=torch.float32, device=dev)
     ws = _workspace(state, max(B for B, _, _ in plan))
@@ -181,7 +189,7 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
     opt = enf.ADAGrad()
     hist = []
 
-    fused = world == 1 and os.environ.get("BENCH_UNFUSED", "0") != "1"
+    fused = world == 1 and not emulate_world and os.environ.get("BENCH_UNFUSED", "0") != "1"
     comm = None
     if not fused and comm_kind == "enf":
         comm = enf.EnfComm.from_process_group() if world > 1 else enf.EnfComm.single()
@@ -189,8 +197,12 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
     hbs = np.ascontiguousarray(np.array(hbatches, dtype=np.int64).reshape(-1))
     hdev = torch.zeros(warmup + steps, dtype=torch.float64, device=dev)
 
-    def step(i, ev=None, sh=sh):
+    def step(i, ev=None, sh=sh, ph=None):
+        # ev: events around the gradient launches (the timed eager steps); ph: [e0, e1, e2, e3] around the
+        # gradient, the all-reduce and the update (breakdown)
         B, lo, hi = plan[i % len(plan)]
+        if ph is not None:
+            ph[0].record(stream)
         if fused:  # enf_whitening_step: gradient, loss, ADAGrad, re-normalisation (3 launches)
             if ev is not None:
                 ev[0].record(stream)
@@ -200,6 +212,8 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
                                            opt.epsilon, hdev[i:].data_ptr(), ws.data_ptr(), ws.numel() * 8, sh))
             if ev is not None:
                 ev[1].record(stream)
+            if ph is not None:
+                ph[3].record(stream)
             return hdev[i:i + 1]
         out.zero_()
         if ev is not None:
@@ -209,14 +223,20 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
                                             len(state.trafos), out.data_ptr(), ws.data_ptr(), ws.numel() * 8, sh))
         if ev is not None:
             ev[1].record(stream)
+        if ph is not None:
+            ph[1].record(stream)
         if comm is not None:
             comm.allreduce_sum_(out, sh)  # RCCL on the kernels' stream
         else:
             enf.allreduce_sum_(out, world)
+        if ph is not None:
+            ph[2].record(stream)
         # loss, ADAGrad and re-normalisation on every rank in one launch
         lib.check(L.enf_whitening_apply(lib.ENF_F32, D, state.nparams, out.data_ptr(), B, state.theta.data_ptr(),
                                         state.acc.data_ptr(), runs.ctypes.data, len(segs), hbs.ctypes.data,
                                         len(hbatches), opt.eta, opt.epsilon, hdev[i:].data_ptr(), sh))
+        if ph is not None:
+            ph[3].record(stream)
         return hdev[i:i + 1]
 
     for i in range(warmup):
@@ -258,7 +278,27 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
     per_rank_ms = gather_ranks(wall / steps * 1e3, dev, world, rank)
     wall, grad_ms_max = max_over_ranks([wall, grad_ms], dev, world)
     samples = sum(plan[(warmup + i) % len(plan)][0] for i in range(steps))
-    negll = [float(h) for h in torch.cat(hist).cpu()]
+    hist_vals = torch.cat(hist).cpu()  # (before the breakdown's steps overwrite the device history)
+    phases = None
+    if breakdown:
+        # eager steps with events between the phases (after the timed region; advances the optimizer further)
+        evp = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+        for i in range(steps):
+            step(warmup + i, None, sh, evp[i])
+        torch.cuda.synchronize()
+        med = lambda xs: float(np.median(xs))
+        if fused:
+            phases = {"fused_step_ms": med([e[0].elapsed_time(e[3]) for e in evp]),
+                      "launches": "enf_whitening_step: gradient kernel + slice sums + tail (3 launches)"}
+        else:
+            phases = {"gradient_ms": med([e[0].elapsed_time(e[1]) for e in evp]),
+                      "allreduce_ms": med([e[1].elapsed_time(e[2]) for e in evp]),
+                      "update_ms": med([e[2].elapsed_time(e[3]) for e in evp]),
+                      "step_ms": med([e[0].elapsed_time(e[3]) for e in evp]),
+                      "launches": "gradient: out.zero_ + gradient kernel + slice sums + finalize; all-reduce: RCCL; "
+                                  "update: enf_whitening_apply (1 launch)"}
+        phases["mode"] = "eager, HIP events between the phases (median over the steps)"
+    negll = [float(h) for h in hist_vals]
     if history and rank == 0:
         with open(history, "w") as f:
             json.dump(negll, f)
@@ -274,7 +314,9 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
         "data": "synthetic: X = f_true^-1(Z), Z ~ N(0,1) (torch Philox 0x5EED), f_true seed 7, init seed 42",
         "config": {"workload": f"optimize_whitening D={D}, N={N}, nbatches={nbatches} "
                                f"(B={plan[0][0]}), {pairs}x(J∘H), ADAGrad(0.1)",
-                   "per_rank_share": plan[0][2] - plan[0][1], "parallelism": f"dp{world}"},
+                   "per_rank_share": plan[0][2] - plan[0][1], "parallelism": f"dp{world}",
+                   "emulated_world": emulate_world},
+        "phases": phases,
         "negll_first": negll[0], "negll_last": negll[-1],
     }
     if graph:
