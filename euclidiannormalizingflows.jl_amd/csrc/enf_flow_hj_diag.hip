@@ -355,21 +355,22 @@ __device__ __forceinline__ int mb_load(mb_flag* f) {
   return __builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
 // returns the flag value once (v >> sh) >= want (wave-uniform), or after kMbSpinMax polls with *err set
+template <int SLEEP>
 __device__ __forceinline__ int mb_wait(mb_flag* f, int want, int sh, mb_flag* err, int lane) {
   int v = mb_load(f);
   for (int i = 0; (v >> sh) < want; ++i) {
-    if (i >= kMbSpinMax) {
+    if (i >= (SLEEP ? kMbSpinMax : 64 * kMbSpinMax)) {
       if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       break;
     }
-    __builtin_amdgcn_s_sleep(1);
+    if constexpr (SLEEP) __builtin_amdgcn_s_sleep(1);
     v = mb_load(f);
   }
   asm volatile("" ::: "memory");
   return v;
 }
 
-template <int D, int LM, int NOWAIT>
+template <int D, int LM, int NOWAIT, int SLEEP = 1>
 __global__ __launch_bounds__(512, 4) void flow_hjm_kernel(HJArgs a, int* errp) {
   constexpr int R = 8, U = 2;
   using L = HJLay<D, R, U>;
@@ -457,11 +458,12 @@ __global__ __launch_bounds__(512, 4) void flow_hjm_kernel(HJArgs a, int* errp) {
       const int p = (int)(s - k * n);
       const float* rp = recl + p * kHjW * D;
       if (p == 0) {
-        if (k > 0) finish(SC, k - 1, mb_wait(tf + S, (int)s - 1, 1, err, lane));
-        (void)mb_wait(xf + S, (int)k, 0, err, lane);
+        if (k > 0) finish(SC, k - 1, mb_wait<SLEEP>(tf + S, (int)s - 1, 1, err, lane));
+        (void)mb_wait<SLEEP>(xf + S, (int)k, 0, err, lane);
         slot_read<R, U>(xb(S), lane, x[S]);
+        prm.template load<0, HJ_IL>(rp);  // (vh of pair 0: hj_pair_z reads the other slots)
       } else {
-        (void)mb_wait(tf + S, (int)s - 1, 1, err, lane);
+        (void)mb_wait<SLEEP>(tf + S, (int)s - 1, 1, err, lane);
         float t[U][R];
         slot_read<R, U>(zt(S), lane, t);
         prm.template load<0, HJ_IL>(rp);
@@ -475,8 +477,8 @@ __global__ __launch_bounds__(512, 4) void flow_hjm_kernel(HJArgs a, int* errp) {
       if (s < stA) phase(std::integral_constant<int, 0>{}, s);
       if (s < stB) phase(std::integral_constant<int, 1>{}, s);
     }
-    if (KA > 0) finish(std::integral_constant<int, 0>{}, KA - 1, mb_wait(tf, (int)stA - 1, 1, err, lane));
-    if (KB > 0) finish(std::integral_constant<int, 1>{}, KB - 1, mb_wait(tf + 1, (int)stB - 1, 1, err, lane));
+    if (KA > 0) finish(std::integral_constant<int, 0>{}, KA - 1, mb_wait<SLEEP>(tf, (int)stA - 1, 1, err, lane));
+    if (KB > 0) finish(std::integral_constant<int, 1>{}, KB - 1, mb_wait<SLEEP>(tf + 1, (int)stB - 1, 1, err, lane));
   } else {
     float acc[2][U], mx[2];
 #pragma unroll
@@ -489,7 +491,7 @@ __global__ __launch_bounds__(512, 4) void flow_hjm_kernel(HJArgs a, int* errp) {
       constexpr int S = decltype(SC)::value;
       const int64_t k = s / n;
       const int p = (int)(s - k * n);
-      (void)mb_wait(zf + S, (int)s, 0, err, lane);
+      (void)mb_wait<SLEEP>(zf + S, (int)s, 0, err, lane);
       float z[U][R], t[U][R];
       slot_read<R, U>(zt(S), lane, z);
       if (p == 0 && k + 1 < KS(S)) {
@@ -561,7 +563,7 @@ __global__ __launch_bounds__(512, 4) void flow_hjm_kernel(HJArgs a, int* errp) {
 
 static int* g_mb_err = nullptr;  // device error word of the mailbox kernel (diagnostics: read by tools)
 
-template <int D, int LM, int NOWAIT>
+template <int D, int LM, int NOWAIT, int SLEEP = 1>
 static hipError_t launch_hjm(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
   if (!g_mb_err) {
     hipError_t e = hipMalloc(&g_mb_err, sizeof(int));
@@ -570,7 +572,7 @@ static hipError_t launch_hjm(const HJArgs& h, hipStream_t st, const DeviceInfo& 
     if (e != hipSuccess) return e;
   }
   const size_t lds = hjm_lds_bytes(D, h.n);
-  const void* k = reinterpret_cast<const void*>(&flow_hjm_kernel<D, LM, NOWAIT>);
+  const void* k = reinterpret_cast<const void*>(&flow_hjm_kernel<D, LM, NOWAIT, SLEEP>);
   hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   int per_cu = 0;
@@ -582,12 +584,13 @@ static hipError_t launch_hjm(const HJArgs& h, hipStream_t st, const DeviceInfo& 
   int64_t blocks = (int64_t)dev.num_cu * per_cu;
   const int64_t need = (h.N + (int64_t)HJLay<D, 8, 2>::TC * kMbF - 1) / ((int64_t)HJLay<D, 8, 2>::TC * kMbF);
   if (blocks > need) blocks = need > 0 ? need : 1;
-  hipLaunchKernelGGL((flow_hjm_kernel<D, LM, NOWAIT>), dim3((unsigned)blocks), dim3(512), lds, st, h, g_mb_err);
+  hipLaunchKernelGGL((flow_hjm_kernel<D, LM, NOWAIT, SLEEP>), dim3((unsigned)blocks), dim3(512), lds, st, h, g_mb_err);
   return hipGetLastError();
 }
 
 template <int LM>
 static hipError_t launch_hjm_d(int D, int nowait, const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
+  if (D == 32 && nowait == 2) return launch_hjm<32, LM, 1, 0>(h, st, dev);  // busy polling, no s_sleep
   if (D == 32) return nowait ? launch_hjm<32, LM, 1>(h, st, dev) : launch_hjm<32, LM, 0>(h, st, dev);
   return nowait ? launch_hjm<64, LM, 1>(h, st, dev) : launch_hjm<64, LM, 0>(h, st, dev);
 }
@@ -609,12 +612,14 @@ hipError_t diag_dispatch_hj(const HJArgs& a, int D, int lm, int dbg, hipStream_t
     if (lm == 1) return D == 32 ? launch_hjs<32, 1>(a, st, dev) : launch_hjs<64, 1>(a, st, dev);
     return D == 32 ? launch_hjs<32, 2>(a, st, dev) : launch_hjs<64, 2>(a, st, dev);
   }
-  // ENF_HJ_MBOX: 1 = the mailbox kernel flow_hjm_kernel, 2 = the same without the lgkmcnt wait before a flag
+  // ENF_HJ_MBOX: 1 = the mailbox kernel flow_hjm_kernel, 2 = the same without the lgkmcnt wait before a flag,
+  // 3 = that and busy polling (no s_sleep)
   static const int mbox = ENF_KNOB("ENF_HJ_MBOX", 0);
   if (mbox && dbg == 0 && (D == 32 || D == 64)) {
-    if (lm == 0) return launch_hjm_d<0>(D, mbox == 2, a, st, dev);
-    if (lm == 1) return launch_hjm_d<1>(D, mbox == 2, a, st, dev);
-    return launch_hjm_d<2>(D, mbox == 2, a, st, dev);
+    const int v = mbox == 3 ? 2 : mbox == 2 ? 1 : 0;
+    if (lm == 0) return launch_hjm_d<0>(D, v, a, st, dev);
+    if (lm == 1) return launch_hjm_d<1>(D, v, a, st, dev);
+    return launch_hjm_d<2>(D, v, a, st, dev);
   }
   if (D != 32 || lm != 1) return hipErrorNotSupported;
   static const int as = ENF_KNOB("ENF_HJ_ASINH", 1);

@@ -18,6 +18,11 @@ enf_status negll_grad_workspace(bool f64, int64_t D, int64_t N, const enf_layer*
 enf_status negll_grad(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
                       int32_t nlayers, void* out, void* workspace, size_t workspace_bytes, hipStream_t st);
 enf_status negll_loss_workspace(bool f64, int64_t D, int64_t N, size_t* bytes);
+// enf_loss.hip: the loss reduction of N columns (Y: D x N contiguous, L: N) into *total (double; first: set,
+// else added), and *total added into out[0] (T)
+enf_status negll_reduce(bool f64, int64_t D, int64_t N, const void* Y, const void* L, double* part, double* total,
+                        bool first, hipStream_t st);
+enf_status negll_add_total(bool f64, const double* total, void* out, hipStream_t st);
 enf_status negll_loss(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
                       int32_t nlayers, void* out, void* workspace, size_t workspace_bytes, hipStream_t st);
 enf_status flow_vjp(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const void* dY, int64_t lddy,

@@ -342,14 +342,14 @@ function flow_vjp(f::_Supported, X::HipMatrix{T}, dY::HipMatrix{T}, dladj::Union
     dX = HipMatrix{T}(X.D, X.N)
     np = params ? _param_count(layers, X.D) : 0
     dp = params ? HipMatrix(zeros(T, np, 1)) : nothing
-    ws = params ? _grad_workspace(T, X.D, X.N, layers) : nothing
+    ws = _grad_workspace(T, X.D, X.N, layers)  # (a flow beyond one gradient launch's bounds: checkpoints)
     GC.@preserve X dY dladj layers keep dX dp ws begin
         check(ccall((:enf_flow_vjp, libenf), Cint,
                     (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Ptr{EnfLayer}, Int32,
                      Ptr{Cvoid}, Int64, Ptr{Cvoid}, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
                     _dt(T), X.D, X.N, X.buf.ptr, X.D, dY.buf.ptr, X.D, dladj === nothing ? C_NULL : dladj.buf.ptr,
                     layers, length(layers), dX.buf.ptr, X.D, params ? dp.buf.ptr : C_NULL,
-                    params ? ws.ptr : C_NULL, params ? ws.bytes : 0, C_NULL))
+                    ws.ptr, ws.bytes, C_NULL))
     end
     params || return dX, nothing
     g = vcat(zero(T), Array(dp)[:, 1])

@@ -270,7 +270,7 @@ def flow_vjp(trafo, X, dY, dladj=None, param_grads: bool = False):
     state = FlowState(trafo, D, dtype, M.device)
     dX = torch.empty((N, D), dtype=dtype, device=M.device).t()  # column-major D x N
     dp = torch.zeros(state.nparams, dtype=dtype, device=M.device) if param_grads else None
-    ws = _workspace(state, N) if param_grads else None
+    ws = _workspace(state, N)  # (a flow beyond one gradient launch's bounds needs it for its checkpoints)
     with torch.cuda.device(M.device):
         _lib.check(_lib.lib().enf_flow_vjp(
             _lib.ENF_F64 if dtype == torch.float64 else _lib.ENF_F32, D, N, M.data_ptr(), _ld(M), G.data_ptr(), _ld(G),

@@ -139,7 +139,10 @@ enf_status enf_flow_param_count(int64_t D, const enf_layer* layers, int32_t nlay
  * out has 1 + param_count entries and is ACCUMULATED into (zero it first). Divide by the
  * global batch size after the cross-GPU sum to obtain negll and its gradient.
  * workspace: device scratch of enf_flow_negll_grad_workspace() bytes.
- * Limits: D <= 256 (fp32) / 128 (fp64), at most 16 layers / 32 steps (ENF_ERR_UNSUPPORTED otherwise). */
+ * Limits: D <= 1024. A flow beyond one gradient launch's bounds (more than 16 layers or 32 steps, or
+ * parameter accumulators that do not fit the LDS, as at large D) runs as consecutive chunks of layers with
+ * a checkpoint (D x N) of each chunk's input in the workspace (round 4; ENF_ERR_UNSUPPORTED only when a
+ * single transform exceeds the kernel's bounds). */
 enf_status enf_flow_negll_grad_workspace(enf_dtype dtype, int64_t D, int64_t N,
                                          const enf_layer* layers, int32_t nlayers,
                                          size_t* bytes);
@@ -164,8 +167,9 @@ enf_status enf_flow_negll(enf_dtype dtype, int64_t D, int64_t N, const void* X, 
  * for every sample j (J_j = dY[:, j]/dX[:, j]). dX may alias dY exactly (lddx == lddy), not X.
  * When dparams != NULL it also ACCUMULATES the parameter VJP summed over the samples into dparams
  * (enf_flow_param_count entries, the layout of enf_flow_negll_grad's out[1:]); workspace is then
- * required (enf_flow_negll_grad_workspace bytes), otherwise it may be NULL. The accurate library
- * arithmetic of enf_flow_negll_grad's generic kernel; limits as enf_flow_negll_grad. */
+ * required (enf_flow_negll_grad_workspace bytes), otherwise it may be NULL -- except for a chunked flow
+ * (enf_flow_negll_grad), which always needs it (its checkpoints). The accurate library arithmetic of
+ * enf_flow_negll_grad's generic kernel; limits as enf_flow_negll_grad. */
 enf_status enf_flow_vjp(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx, const void* dY,
                         int64_t lddy, const void* dladj, const enf_layer* layers, int32_t nlayers, void* dX,
                         int64_t lddx, void* dparams, void* workspace, size_t workspace_bytes,
