@@ -108,6 +108,9 @@ def main():
     ap.add_argument("--comm", default="enf", choices=["enf", "torch"],
                     help="world > 1: RCCL through libenf on the kernels' stream (enf; graph-capturable) or "
                          "torch.distributed.all_reduce (torch; eager only)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="one process: rank 0's data-parallel step at this world size (its share of each minibatch)")
+    ap.add_argument("--breakdown", action="store_true", help="per-phase event times of eager steps after the timed ones")
     args = ap.parse_args()
 
     # N > 1 started by hand: start the N ranks as child processes before anything touches a GPU
@@ -133,7 +136,8 @@ def main():
 
         load()._lib.use_diagnostics_library()
     res = train_leg(dev, world, rank, D=args.D, N=args.N, nbatches=args.nbatches, pairs=args.pairs, steps=args.steps,
-                    warmup=args.warmup, graph=bool(args.graph), comm_kind=args.comm, history=args.history)
+                    warmup=args.warmup, graph=bool(args.graph), comm_kind=args.comm, history=args.history,
+                    emulate_world=args.emulate_world or None, breakdown=args.breakdown)
     if rank == 0:
         print(json.dumps(res))
     if world > 1:

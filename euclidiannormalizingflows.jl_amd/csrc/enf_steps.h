@@ -29,7 +29,7 @@ static __shared__ double g_logtab[3 * kLogTabN];
 //  SCALESHIFT   W=2 {a, b}                           same
 //  JOHNSON      W=4 {gamma, delta*ln2, xi, 1/lambda} {gamma, delta, xi, 1/lambda}
 //  JOHNSON_INV  W=4 {gamma, 1/delta, xi, lambda}     {gamma, 1/delta, xi, lambda}
-//  CENTER_*     W=8 {b*log2e, c, ln2/b, exp(b*a),    {a, b, c, 0, ...}
+//  CENTER_*     W=8 {b*log2e, c, ln2/b, exp(b*a),    {a, b, c, exp(b*a), exp(2*b*a), 0, ...}
 //                    exp(2*b*a), b*a*log2e, a, b}
 // Layout: [group g][param q][element e] with RV elements per group; element (g, e) is row
 // g*RV + e (D >= RV) or e % D (D < RV). The fragment kernel uses RV = V = 16/sizeof(T), so a
@@ -76,7 +76,11 @@ __device__ __forceinline__ void param_values(int op, const LayerDesc& L, int col
       out[0] = av;
       out[1] = bv;
       out[2] = cv;
-      for (int q = 3; q < 8; ++q) out[q] = 0.0;
+      // the row constants of center_stretch.jl:7, once per row instead of per element (round 4): the same
+      // double operations as the per-element expressions they replace, so the same values
+      out[3] = exp(bv * av);
+      out[4] = exp(2.0 * bv * av);
+      for (int q = 5; q < 8; ++q) out[q] = 0.0;
     }
   }
 }
@@ -110,8 +114,10 @@ __device__ __forceinline__ void neutral_values(int op, T (&out)[8]) {
       out[3] = 1.0f;
       out[4] = 1.0f;
       out[7] = 1.0f;
-    } else {  // {a, b, c}
+    } else {  // {a, b, c, exp(ba), exp(2ba)}
       out[1] = 1.0;
+      out[3] = 1.0;
+      out[4] = 1.0;
     }
   }
 }
@@ -360,11 +366,11 @@ __device__ __forceinline__ void step_center_stretch(Tile<T, D, U>& x, Acc<T, D, 
               acc[u][e / SEG] -= hw_log2(fabsf(dy));
             }
           } else {
-            const double av = rr[0][e], bv = rr[1][e], c = rr[2][e];
+            const double av = rr[0][e], bv = rr[1][e], c = rr[2][e], E1 = rr[3][e], E2 = rr[4][e];
             const double xv = x[u][e];
             const double ex = exp(fabs(bv * xv));
             const double ome = 1.0 - ex;
-            const double inner = (sqrt(ome * ome * exp(2.0 * bv * av) + 4.0 * ex) - ome * exp(bv * av)) / 2.0;
+            const double inner = (sqrt(ome * ome * E2 + 4.0 * ex) - ome * E1) / 2.0;
             const double sg = xv > 0. ? 1. : (xv < 0. ? -1. : xv);
             const double y = sg * log(inner) / bv + c;
             x[u][e] = y;
