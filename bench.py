@@ -526,6 +526,10 @@ def train_leg(dev, world, rank):
         try:
             s8 = bench_train.train_leg(dev, 1, 0, graph=True, comm_kind="enf", emulate_world=8, breakdown=True)
             res["rank_share_of_8"] = {k: s8[k] for k in ("value", "ms_per_step", "step", "launch", "phases", "config")}
+            # the same step as three calls (gradient, all-reduce, enf_whitening_apply), with its per-phase breakdown
+            u8 = bench_train.train_leg(dev, 1, 0, graph=True, comm_kind="enf", emulate_world=8, breakdown=True,
+                                       dp_fused=False)
+            res["rank_share_of_8"]["separate_calls"] = {k: u8[k] for k in ("value", "ms_per_step", "step", "phases")}
         except Exception as e:  # noqa: BLE001
             res["rank_share_of_8"] = {"error": f"{type(e).__name__}: {e}"}
     return res

@@ -67,10 +67,13 @@ def train_leg_selftest(world, rank, N=10_000_000, nbatches=100, steps=100):
             "config": {"parallelism": f"dp{world}", "B": plan[0][0]}}
 
 
-def step_description(fused, world, comm_kind, graph):
+def step_description(fused, world, comm_kind, graph, dp_fused=False):
     """What one timed config-5 step runs (the `step` / `launch` fields of the record)."""
     if fused:
         return "enf_whitening_step (fused, 1 rank)"
+    if dp_fused:
+        return ("enf_whitening_step_dp (gradient, RCCL sum of the slice totals over xGMI on the kernels' stream"
+                + (", captured in the HIP graph" if graph else "") + ", one tail launch)")
     comm = ("libenf EnfComm (RCCL over xGMI on the kernels' stream" + (", captured in the HIP graph)" if graph else ")")
             if comm_kind == "enf" else "torch.distributed all_reduce (eager)")
     return f"enf_flow_negll_grad + {comm} + enf_whitening_apply"
@@ -145,7 +148,7 @@ def main():
 
 
 def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps=100, warmup=5, graph=True,
-              comm_kind="enf", history="", emulate_world=None, breakdown=False):
+              comm_kind="enf", history="", emulate_world=None, breakdown=False, dp_fused=True):
     """Config 5 on this process's GPU as one rank of `world` (torch.distributed initialised by the
     caller when world > 1): returns the result record (the same on every rank; rank 0 prints it).
     Also run by bench.py after its headline measurement (`train` object of its JSON line).
@@ -154,7 +157,9 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
     minibatch B -- i.e. one rank's step at that world size without the cross-GPU transfer (the update differs
     from a real W-rank run, which sums every share; the timing is the rank's local work).
     breakdown=True: after the timed steps, `steps` eager steps with HIP events between the phases (gradient
-    launches, all-reduce, update; or the fused call) -> their per-phase medians."""
+    launches, all-reduce, update; or the fused call) -> their per-phase medians.
+    dp_fused: the data-parallel step with an EnfComm as ONE call, enf_whitening_step_dp (gradient, RCCL sum of the
+    double slice totals, one tail launch; round 4), else enf_flow_negll_grad + all-reduce + enf_whitening_apply."""
     import torch
 
     from enf_pkg import load
@@ -214,6 +219,19 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
                                            len(state.trafos), state.theta.data_ptr(), state.acc.data_ptr(),
                                            runs.ctypes.data, len(segs), hbs.ctypes.data, len(hbatches), opt.eta,
                                            opt.epsilon, hdev[i:].data_ptr(), ws.data_ptr(), ws.numel() * 8, sh))
+            if ev is not None:
+                ev[1].record(stream)
+            if ph is not None:
+                ph[3].record(stream)
+            return hdev[i:i + 1]
+        if dp_fused and comm is not None:  # enf_whitening_step_dp: gradient, RCCL sum, tail
+            if ev is not None:
+                ev[0].record(stream)
+            lib.check(L.enf_whitening_step_dp(lib.ENF_F32, D, hi - lo, X[:, lo:hi].data_ptr(), ldx, state.layers(),
+                                              len(state.trafos), state.theta.data_ptr(), state.acc.data_ptr(),
+                                              runs.ctypes.data, len(segs), hbs.ctypes.data, len(hbatches), opt.eta,
+                                              opt.epsilon, B, hdev[i:].data_ptr(), comm.handle, ws.data_ptr(),
+                                              ws.numel() * 8, sh))
             if ev is not None:
                 ev[1].record(stream)
             if ph is not None:
@@ -291,9 +309,10 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
             step(warmup + i, None, sh, evp[i])
         torch.cuda.synchronize()
         med = lambda xs: float(np.median(xs))
-        if fused:
+        if fused or (dp_fused and comm is not None):
             phases = {"fused_step_ms": med([e[0].elapsed_time(e[3]) for e in evp]),
-                      "launches": "enf_whitening_step: gradient kernel + slice sums + tail (3 launches)"}
+                      "launches": "enf_whitening_step: gradient kernel + slice sums + tail (3 launches)" if fused else
+                                  "enf_whitening_step_dp: gradient kernel + slice sums + RCCL all-reduce + tail"}
         else:
             phases = {"gradient_ms": med([e[0].elapsed_time(e[1]) for e in evp]),
                       "allreduce_ms": med([e[1].elapsed_time(e[2]) for e in evp]),
@@ -313,7 +332,8 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
         "grad_kernel_ms_median" if not fused else "fused_step_ms_median": grad_ms,
         "grad_kernel_ms_max_rank" if not fused else "fused_step_ms_max_rank": grad_ms_max, "dtype": "f32",
         "launch": "HIP graph of the timed steps (torch.cuda.CUDAGraph), replayed" if graph else "eager",
-        "step": step_description(fused, world, "enf" if comm is not None else "torch", graph),
+        "step": step_description(fused, world, "enf" if comm is not None else "torch", graph,
+                                 dp_fused and comm is not None),
         "per_rank_ms_per_step": per_rank_ms,
         "data": "synthetic: X = f_true^-1(Z), Z ~ N(0,1) (torch Philox 0x5EED), f_true seed 7, init seed 42",
         "config": {"workload": f"optimize_whitening D={D}, N={N}, nbatches={nbatches} "

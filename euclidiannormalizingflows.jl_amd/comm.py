@@ -53,6 +53,11 @@ class EnfComm:
         dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
         return cls(world, rank, obj[0])
 
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        """The enf_comm handle (for enf_whitening_step_dp)."""
+        return self._h
+
     def allreduce_sum_(self, buf: torch.Tensor, stream: Optional[int] = None) -> torch.Tensor:
         """In-place sum over the ranks of a contiguous device tensor (fp32 / fp64), asynchronous on
         `stream` (default: torch's current stream of buf's device)."""

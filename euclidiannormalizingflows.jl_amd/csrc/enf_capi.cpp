@@ -778,4 +778,30 @@ enf_status enf_allreduce_sum(enf_comm comm, void* buf, int64_t count, enf_dtype 
   ENF_CATCH
 }
 
+// ------------------------------------------------------------- data-parallel training step ----
+static enf_status rccl_allreduce(void* ctx, void* buf, int64_t count, bool f64, hipStream_t st) {
+  const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, f64 ? ncclFloat64 : ncclFloat32, ncclSum,
+                                       static_cast<enf_comm_s*>(ctx)->comm, st);
+  return r == ncclSuccess ? ENF_OK : fail(ENF_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+}
+
+enf_status enf_whitening_step_dp(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
+                                 const enf_layer* layers, int32_t nlayers, void* theta, void* acc, const int64_t* runs,
+                                 int32_t nruns, const int64_t* hbatches, int32_t nhb, double eta, double epsilon,
+                                 int64_t B, double* loss_out, enf_comm comm, void* workspace, size_t workspace_bytes,
+                                 void* hip_stream) {
+  ENF_TRY
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
+  if (D < 1 || N < 0 || B < 1 || N > B) return fail(ENF_ERR_INVALID, "D and B must be >= 1, 0 <= N <= B");
+  if (ldx < D) return fail(ENF_ERR_INVALID, "ldx < D");
+  enf_status vs = validate_layers(D, layers, nlayers);
+  if (vs != ENF_OK) return vs;
+  if ((N > 0 && !X) || !theta || !acc || !loss_out) return fail(ENF_ERR_INVALID, "X, theta, acc or loss_out is NULL");
+  if ((nruns > 0 && !runs) || (nhb > 0 && !hbatches)) return fail(ENF_ERR_INVALID, "runs or hbatches is NULL");
+  return enf::whitening_step_dp(dtype == ENF_F64, D, N, X, ldx, layers, nlayers, theta, acc, runs, nruns, hbatches, nhb,
+                                eta, epsilon, B, loss_out, comm ? rccl_allreduce : nullptr, comm, workspace,
+                                workspace_bytes, (hipStream_t)hip_stream);
+  ENF_CATCH
+}
+
 }  // extern "C"

@@ -17,7 +17,7 @@ hipError_t diag_dispatch_hj(const HJArgs& a, int D, int lm, int dbg, hipStream_t
 // layouts of the forward program (D = 32 / 64 / 128, padded or not), fused in one launch. Per pair p:
 //   w   = (y - gamma)/delta                  as fma(y, 1/delta, -gamma/delta)       (johnson_trafo.jl:36)
 //   sh  = sinh(w): |w| < 1/2: w (1 + w^2/6 + w^4/120 + w^6/5040) (truncation < 1e-8 relative),
-//         else (E - 1/E)/2, E = exp2(w log2 e) -- both odd in w, merged branch-free by a mask from w^2
+//         else H - 1/(4H), H = E/2 = exp2(w log2 e - 1) -- both odd in w, merged branch-free by a mask from w^2
 //   x   = lambda sh + xi                      the JohnsonTrafoInv output              (johnson_trafo.jl:36)
 //   ladj += -log|delta/lambda| + log(1 + sh^2)/2: the reference's -johnsontrafo_ladj of the output
 //         (johnson_trafo.jl:103-104), whose (x - xi)/lambda is sh up to the rounding of x; the constant part
@@ -113,7 +113,7 @@ __device__ __forceinline__ float hji_pair_fast(float (&x)[U][R], float (&acc)[U]
 #pragma unroll
     for (int e = 0; e < R; ++e) {
       w[u][e] = fmaf(x[u][e], prm.m(HI_ID, e), prm.m(HI_NG, e));
-      E[u][e] = w[u][e] * (float)kLog2e;
+      E[u][e] = fmaf(w[u][e], (float)kLog2e, -1.0f);  // exp2 of this is E/2
     }
   // wave priority 3 around the transcendental groups, as in hj_pair_fast
   __builtin_amdgcn_s_setprio(3);
@@ -155,7 +155,8 @@ __device__ __forceinline__ float hji_pair_fast(float (&x)[U][R], float (&acc)[U]
   for (int u = 0; u < U; ++u) {
 #pragma unroll
     for (int e = 0; e < R; ++e) {
-      const float sh = asinh2_pick(w[u][e], (E[u][e] - rE[u][e]) * 0.5f, msk[u][e]);
+      // (E - 1/E)/2 = E/2 - 1/(4 E/2): one fma on the halved exponential and its reciprocal
+      const float sh = asinh2_pick(w[u][e], fmaf(-0.25f, rE[u][e], E[u][e]), msk[u][e]);
       q[u][e] = fmaf(sh, sh, 1.0f);
       x[u][e] = fmaf(prm.m(HI_LM, e), sh, prm.m(HI_XI, e));
     }

@@ -736,10 +736,13 @@ enf_status whitening_apply(bool f64, int64_t D, int64_t nparams, const void* g, 
 }
 
 namespace {
+// B: the global batch size the update normalises by (N on one rank); ar: the cross-rank sum of the 8 slice
+// totals (double) between the gradient and the tail (enf_whitening_step_dp), or none
 enf_status whitening_step_single(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
                                  int32_t nlayers, void* theta, void* acc, const int64_t* runs, int32_t nruns,
                                  const int64_t* hb, int32_t nhb, double eta, double epsilon, double* loss_out,
-                                 void* workspace, size_t workspace_bytes, hipStream_t st) {
+                                 void* workspace, size_t workspace_bytes, hipStream_t st, int64_t B, AllreduceFn ar,
+                                 void* ar_ctx) {
   if (nruns < 0 || nruns > kMaxStepRuns || nhb < 0 || nhb > kMaxStepHB)
     return set_error(ENF_ERR_UNSUPPORTED, "enf_whitening_step: too many parameter runs or Householder batches");
   StepArgs a;
@@ -747,11 +750,11 @@ enf_status whitening_step_single(bool f64, int64_t D, int64_t N, const void* X, 
   a.theta = theta;
   a.acc = acc;
   a.loss_out = loss_out;
-  a.scale = 1.0 / (double)N;
+  a.scale = 1.0 / (double)B;
   a.eta = eta;
   a.eps = epsilon;
   a.D = D;
-  a.nsamp = N;
+  a.nsamp = B;
   a.nruns = nruns;
   a.nhb = nhb;
   for (int i = 0; i < nruns; ++i) {
@@ -761,7 +764,7 @@ enf_status whitening_step_single(bool f64, int64_t D, int64_t N, const void* X, 
   for (int i = 0; i < nhb; ++i)
     for (int q = 0; q < 3; ++q) a.hb[i][q] = hb[3 * i + q];
   Plan P;
-  enf_status s = make_plan(f64, D, N, layers, nlayers, P);
+  enf_status s = make_plan(f64, D, N > 0 ? N : 1, layers, nlayers, P);
   if (s != ENF_OK) return s;
   for (int i = 0; i < nruns; ++i)
     if (a.runs[i][0] < 0 || a.runs[i][1] < a.runs[i][0] || a.runs[i][1] > P.ga.nparams)
@@ -770,8 +773,22 @@ enf_status whitening_step_single(bool f64, int64_t D, int64_t N, const void* X, 
     if (a.hb[i][0] < 0 || a.hb[i][1] < 0 || a.hb[i][2] < D ||
         (a.hb[i][1] > 0 && a.hb[i][0] + (a.hb[i][1] - 1) * a.hb[i][2] + D > P.ga.nparams))
       return set_error(ENF_ERR_INVALID, "enf_whitening_step: Householder batch outside theta");
-  s = grad_parts(f64, D, N, X, ldx, layers, nlayers, workspace, workspace_bytes, st, P);
-  if (s != ENF_OK) return s;
+  const size_t ntot = (size_t)kSumSlices * (1 + (size_t)P.ga.nparams);
+  if (N > 0) {
+    s = grad_parts(f64, D, N, X, ldx, layers, nlayers, workspace, workspace_bytes, st, P);
+    if (s != ENF_OK) return s;
+  } else {  // an empty share (a rank without columns in this minibatch): zero slice totals
+    const size_t need = ((size_t)P.blocks + kSumSlices) * (1 + (size_t)P.ga.nparams) * sizeof(double);
+    if (!workspace || workspace_bytes < need) return set_error(ENF_ERR_INVALID, "enf_whitening_step: workspace too small");
+    P.ra.partial = (const double*)workspace;
+    P.ra.tot = (double*)workspace + (size_t)P.blocks * (1 + (size_t)P.ga.nparams);
+    if (hipMemsetAsync(P.ra.tot, 0, ntot * sizeof(double), st) != hipSuccess)
+      return set_error(ENF_ERR_HIP, "hipMemsetAsync");
+  }
+  if (ar) {  // the cross-rank sum of the slice totals, in double, before the tail sums the slices
+    s = ar(ar_ctx, P.ra.tot, (int64_t)ntot, true, st);
+    if (s != ENF_OK) return s;
+  }
   if (f64) hipLaunchKernelGGL((whitening_tail_kernel<double>), dim3(1), dim3(256), 0, st, P.ra, a);
   else hipLaunchKernelGGL((whitening_tail_kernel<float>), dim3(1), dim3(256), 0, st, P.ra, a);
   hipError_t e = hipGetLastError();
@@ -1024,9 +1041,17 @@ enf_status whitening_step(bool f64, int64_t D, int64_t N, const void* X, int64_t
                           int32_t nlayers, void* theta, void* acc, const int64_t* runs, int32_t nruns,
                           const int64_t* hb, int32_t nhb, double eta, double epsilon, double* loss_out,
                           void* workspace, size_t workspace_bytes, hipStream_t st) {
+  return whitening_step_dp(f64, D, N, X, ldx, layers, nlayers, theta, acc, runs, nruns, hb, nhb, eta, epsilon, N,
+                           loss_out, nullptr, nullptr, workspace, workspace_bytes, st);
+}
+
+enf_status whitening_step_dp(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
+                             int32_t nlayers, void* theta, void* acc, const int64_t* runs, int32_t nruns,
+                             const int64_t* hb, int32_t nhb, double eta, double epsilon, int64_t B, double* loss_out,
+                             AllreduceFn ar, void* ar_ctx, void* workspace, size_t workspace_bytes, hipStream_t st) {
   if (fits_one_launch(f64, D, N, layers, nlayers))
     return whitening_step_single(f64, D, N, X, ldx, layers, nlayers, theta, acc, runs, nruns, hb, nhb, eta, epsilon,
-                                 loss_out, workspace, workspace_bytes, st);
+                                 loss_out, workspace, workspace_bytes, st, B, ar, ar_ctx);
   std::vector<GradChunk> ch;
   ChunkWs w;
   enf_status s = chunked_setup(f64, D, N, layers, nlayers, workspace, workspace_bytes, ch, w, "enf_whitening_step");
@@ -1036,9 +1061,15 @@ enf_status whitening_step(bool f64, int64_t D, int64_t N, const void* X, int64_t
   const int64_t np = total_params(D, layers, nlayers);
   if (hipMemsetAsync(ws + w.g, 0, (size_t)(1 + np) * (f64 ? 8 : 4), st) != hipSuccess)
     return set_error(ENF_ERR_HIP, "hipMemsetAsync");
-  s = negll_grad_chunked(f64, D, N, X, ldx, ch, ws + w.g, ws, w, st);
-  if (s != ENF_OK) return s;
-  return whitening_apply(f64, D, np, ws + w.g, N, theta, acc, runs, nruns, hb, nhb, eta, epsilon, loss_out, st);
+  if (N > 0) {
+    s = negll_grad_chunked(f64, D, N, X, ldx, ch, ws + w.g, ws, w, st);
+    if (s != ENF_OK) return s;
+  }
+  if (ar) {
+    s = ar(ar_ctx, ws + w.g, 1 + np, f64, st);
+    if (s != ENF_OK) return s;
+  }
+  return whitening_apply(f64, D, np, ws + w.g, B, theta, acc, runs, nruns, hb, nhb, eta, epsilon, loss_out, st);
 }
 
 }  // namespace enf

@@ -193,33 +193,58 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
 
 // Block prologue shared by both kernels: per pair v'v and the constant ladj part sum log|delta/lambda|
 // (double, scr), then the records [pair][group][param][4] in rec. Returns ctot = sum of the constants.
+// LDS-only block barrier: global loads issued before it (a wave's first tile) stay in flight
+__device__ __forceinline__ void gh_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Block prologue: the per-row records of every pair in ONE round of global loads (round 4; round 3 read the
+// parameters twice, once per pass): thread i of the first n*D handles row d = i % D of pair p = i / D, loads its
+// five parameters, and the per-pair sums v'v and sum_d log|delta/lambda| (johnson_trafo.jl:41) are reduced over
+// the D adjacent lanes that hold pair p (D <= 64: within one wave); after one LDS barrier each thread writes its
+// row's records with the pair's reflection scale sqrt(2/v'v) (householder_trafo.jl:9-10). Double arithmetic as
+// before, so the same records and constant.
 template <int D>
 __device__ __forceinline__ float grad_prologue(const HJGradArgs& a, double* __restrict__ scr, float* __restrict__ rec) {
+  static_assert(D <= 64 && 256 % D == 0, "a pair's rows within one wave");
   const int n = a.n;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int p = wave; p < n; p += 4) {
+  const int tid = threadIdx.x;
+  constexpr int kIt = (kHJGradMaxPairs * D + 255) / 256;  // rows per thread (n * D <= 8 * 64)
+  double pv[kIt], pg[kIt], pd[kIt], px[kIt], pl[kIt];
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int i = tid + 256 * it;
+    const int p = i / D, d = i % D;
     double vv = 0.0, cl = 0.0;
-    for (int d = lane; d < D; d += 64) {
-      const double vd = a.v[p][d];
-      vv += vd * vd;
-      cl += log(fabs((double)a.d[p][d])) - log(fabs((double)a.lam[p][d]));
+    pv[it] = pg[it] = px[it] = 0.0;
+    pd[it] = pl[it] = 1.0;
+    if (p < n) {
+      pv[it] = a.v[p][d];
+      pg[it] = a.g[p][d];
+      pd[it] = a.d[p][d];
+      px[it] = a.xi[p][d];
+      pl[it] = a.lam[p][d];
+      vv = pv[it] * pv[it];
+      cl = log(fabs(pd[it])) - log(fabs(pl[it]));
     }
-    for (int m = 32; m >= 1; m >>= 1) {
+#pragma unroll
+    for (int m = D / 2; m >= 1; m >>= 1) {  // the D lanes of pair p (all lanes of the wave take part)
       vv += __shfl_xor(vv, m);
       cl += __shfl_xor(cl, m);
     }
-    if (lane == 0) {
+    if (p < n && d == 0) {
       scr[2 * p] = sqrt(2.0 / vv);
       scr[2 * p + 1] = cl;
     }
   }
-  __syncthreads();
-  for (int i = tid; i < n * D; i += blockDim.x) {
+  gh_lds_barrier();
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int i = tid + 256 * it;
     const int p = i / D, d = i % D;
+    if (p >= n) continue;
     float* r = rec + (size_t)p * kNP * D + (d / 4) * kNP * 4 + (d % 4);
-    const double lam = a.lam[p][d], xi = a.xi[p][d], del = a.d[p][d];
-    r[0] = (float)((double)a.v[p][d] * scr[2 * p]);
-    r[4] = a.g[p][d];
+    const double lam = pl[it], xi = px[it], del = pd[it];
+    r[0] = (float)(pv[it] * scr[2 * p]);
+    r[4] = (float)pg[it];
     r[8] = (float)(del * kLn2);
     r[12] = (float)(1.0 / lam);
     r[16] = (float)(-xi / lam);
@@ -227,7 +252,7 @@ __device__ __forceinline__ float grad_prologue(const HJGradArgs& a, double* __re
     r[24] = (float)xi;
     r[28] = (float)del;
   }
-  __syncthreads();
+  gh_lds_barrier();
   double c = 0.0;
   for (int p = 0; p < n; ++p) c += scr[2 * p + 1];
   return (float)c;
@@ -237,8 +262,8 @@ __device__ __forceinline__ float grad_prologue(const HJGradArgs& a, double* __re
 // enf_flow_param_count layout) of the block from the 4 waves' accumulators acc0 + w * wstride
 // ([pair][param 5][D] floats each), summed in a fixed order (deterministic).
 template <int D>
-__device__ __forceinline__ void grad_epilogue(const HJGradArgs& a, double* __restrict__ scr, const float* __restrict__ acc0,
-                                              size_t wstride, double lossp, int nvalid) {
+__device__ __forceinline__ void grad_epilogue(const HJGradArgs& a, double* __restrict__ scr, const float* __restrict__ rec,
+                                              const float* __restrict__ acc0, size_t wstride, double lossp, int nvalid) {
   const int n = a.n;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int m = 32; m >= 1; m >>= 1) {
@@ -258,7 +283,9 @@ __device__ __forceinline__ void grad_epilogue(const HJGradArgs& a, double* __res
     const int p = i / (5 * D), k = (i / D) % 5, d = i % D;
     const double s = (((double)acc0[i] + (double)acc0[wstride + i]) + (double)acc0[2 * wstride + i]) +
                      (double)acc0[3 * wstride + i];
-    const double del = a.d[p][d], lam = a.lam[p][d];
+    // delta and lambda from the records (the fp32 parameters, exactly), not a second round of global loads
+    const float* r = rec + (size_t)p * kNP * D + (d / 4) * kNP * 4 + (d % 4);
+    const double del = r[28], lam = r[20];
     double gval;
     int64_t o;
     switch (k) {
@@ -302,7 +329,7 @@ __global__ __launch_bounds__(256) void hj_grad_kernel(HJGradArgs a) {
     if (t < full) grad_tile<D, KU, false>(a, t * L::TC, lane, rec, zst, dst, acc, lossp, nvalid, ctot);
     else grad_tile<D, KU, true>(a, t * L::TC, lane, rec, zst, dst, acc, lossp, nvalid, ctot);
   }
-  grad_epilogue<D>(a, scr, reinterpret_cast<const float*>(smem + 256 + recb), (accb + zb + db) / 4, lossp, nvalid);
+  grad_epilogue<D>(a, scr, rec, reinterpret_cast<const float*>(smem + 256 + recb), (accb + zb + db) / 4, lossp, nvalid);
 }
 
 // ---- register variant (NP <= 4 pairs, compile time): z and the reflection dots of a tile stay in
@@ -444,6 +471,12 @@ __global__ __launch_bounds__(256) void hj_grad_reg_kernel(HJGradArgs a) {
   float* rec = reinterpret_cast<float*>(smem + 256);
   const size_t recb = (size_t)NP * kNP * D * 4;
   float* accs = reinterpret_cast<float*>(smem + 256 + recb);  // per wave [pair][param 5][D]
+  const int64_t ntiles = (a.N + L::TC - 1) / L::TC;
+  const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wave);
+  // the wave's first tile is loaded before the prologue: its HBM latency overlaps the parameter round trip
+  // (round 4; at the 8-rank share of config 5 a wave has about one tile)
+  float xc[KU][4], xn[KU][4];
+  if (wave_id < ntiles) grad_load_reg<D, KU>(a, wave_id * L::TC, lane, xc);
   const float ctot = grad_prologue<D>(a, scr, rec);
   float acc[NP][5][4];
 #pragma unroll
@@ -454,13 +487,9 @@ __global__ __launch_bounds__(256) void hj_grad_reg_kernel(HJGradArgs a) {
       for (int e = 0; e < 4; ++e) acc[p][k][e] = 0.f;
   double lossp = 0.0;
   int nvalid = 0;
-  const int64_t ntiles = (a.N + L::TC - 1) / L::TC;
   const int64_t full = a.N / L::TC;
-  const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wave);
   // the next tile's columns are loaded while the current one is processed
   const int64_t stride = (int64_t)gridDim.x * 4;
-  float xc[KU][4], xn[KU][4];
-  if (wave_id < ntiles) grad_load_reg<D, KU>(a, wave_id * L::TC, lane, xc);
   for (int64_t t = wave_id; t < ntiles; t += stride) {
     if (t + stride < ntiles) grad_load_reg<D, KU>(a, (t + stride) * L::TC, lane, xn);
     if (t < full) grad_tile_reg<D, KU, NP, false>(a, t * L::TC, lane, rec, xc, acc, lossp, nvalid, ctot);
@@ -482,7 +511,7 @@ __global__ __launch_bounds__(256) void hj_grad_reg_kernel(HJGradArgs a) {
         if (lane < G) wacc[(p * 5 + k) * D + 4 * lane + e] = sv;
       }
   __syncthreads();
-  grad_epilogue<D>(a, scr, accs, (size_t)NP * 5 * D, lossp, nvalid);
+  grad_epilogue<D>(a, scr, rec, accs, (size_t)NP * 5 * D, lossp, nvalid);
 }
 
 template <int D, int KU, int NP>

@@ -41,6 +41,16 @@ enf_status whitening_step(bool f64, int64_t D, int64_t N, const void* X, int64_t
                           const int64_t* hb, int32_t nhb, double eta, double epsilon, double* loss_out,
                           void* workspace, size_t workspace_bytes, hipStream_t st);
 
+// In-place cross-rank sum of `count` values (f64: double, else float) on stream st (enf_whitening_step_dp: RCCL
+// through the caller's communicator)
+typedef enf_status (*AllreduceFn)(void* ctx, void* buf, int64_t count, bool f64, hipStream_t st);
+// One rank's data-parallel optimize_whitening step (enf_whitening_step_dp): the gradient of its N columns, the
+// cross-rank sum ar of the slice totals (double; none on one rank), then the tail normalised by the global batch
+// B (loss, ADAGrad, re-normalisation) -- whitening_step is the case B = N, ar = none
+enf_status whitening_step_dp(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
+                             int32_t nlayers, void* theta, void* acc, const int64_t* runs, int32_t nruns,
+                             const int64_t* hb, int32_t nhb, double eta, double epsilon, int64_t B, double* loss_out,
+                             AllreduceFn ar, void* ar_ctx, void* workspace, size_t workspace_bytes, hipStream_t st);
 // Update half of a data-parallel step after the all-reduce (enf_whitening_apply): g = 1 + nparams
 // summed values of T, B = global batch size.
 enf_status whitening_apply(bool f64, int64_t D, int64_t nparams, const void* g, int64_t B, void* theta, void* acc,

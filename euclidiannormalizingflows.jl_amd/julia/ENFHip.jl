@@ -404,7 +404,8 @@ end
 #
 # comm: an EnfComm for data-parallel training; every rank holds the same smpls and processes its
 # contiguous share [B*rank/world, B*(rank+1)/world) of each minibatch; the unnormalised sums are
-# all-reduced and every rank applies the same update (enf_whitening_apply).
+# all-reduced and every rank applies the same update: enf_whitening_step_dp (gradient, RCCL sum of the
+# kernels' double slice totals, one tail launch), or with tied fields the separate sums + enf_whitening_apply.
 function _flatten(fs, D, ::Type{T}) where {T}
     host, offs, runs, hb, tied = T[], Int[], Int64[], Int64[], Tuple{Int,Int}[]
     for f in fs
@@ -479,6 +480,14 @@ function optimize_whitening(smpls::HipMatrix{T}, initial_trafo::Function, optimi
                             _dt(R), D, B, X.buf.ptr + b0 * D * sizeof(R), D, layers, length(layers), theta.buf.ptr,
                             acc.buf.ptr, runs, length(runs) ÷ 2, hb, length(hb) ÷ 3, rule.eta, rule.epsilon,
                             loss_ptr, ws.ptr, ws.bytes, C_NULL))
+            elseif isempty(tied)  # data-parallel: gradient, RCCL sum of the slice totals, tail (enf_whitening_step_dp)
+                check(ccall((:enf_whitening_step_dp, libenf), Cint,
+                            (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Ptr{EnfLayer}, Int32, Ptr{Cvoid}, Ptr{Cvoid},
+                             Ptr{Int64}, Int32, Ptr{Int64}, Int32, Cdouble, Cdouble, Int64, Ptr{Cdouble}, Ptr{Cvoid},
+                             Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
+                            _dt(R), D, hi - lo, X.buf.ptr + lo * D * sizeof(R), D, layers, length(layers), theta.buf.ptr,
+                            acc.buf.ptr, runs, length(runs) ÷ 2, hb, length(hb) ÷ 3, rule.eta, rule.epsilon, B,
+                            loss_ptr, comm === nothing ? C_NULL : comm.h, ws.ptr, ws.bytes, C_NULL))
             else      # local sums, cross-rank sum, tied-field sums, then the update on every rank
                 _memcpy(out.buf.ptr, Ptr{Cvoid}(pointer(zero_out)), sizeof(zero_out), MEMCPY_H2D)
                 hi > lo && _negll_grad_sums!(out, X, lo, hi - lo, layers, ws)

@@ -437,6 +437,15 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
                 for t in q:
                     hbuf[j:j + 1] += t
                 continue
+            if comm is not None and not tied and apply_fused and not similar_fill_quirk:
+                # data-parallel in one call: gradient of the share, RCCL sum of the kernels' double slice totals,
+                # one tail launch (enf_whitening_step_dp; round 4)
+                _lib.check(L.enf_whitening_step_dp(
+                    dt, D, hi - lo, M[:, lo:hi].data_ptr() if hi > lo else None, _ld(M), state.layers(),
+                    len(state.trafos), state.theta.data_ptr(), state.acc.data_ptr(), runs.ctypes.data, len(segs),
+                    hbs.ctypes.data, len(hbatches), optimizer.eta, optimizer.epsilon, B, hbuf[j:].data_ptr(),
+                    comm.handle, ws.data_ptr(), ws.numel() * 8, stream))
+                continue
             # data-parallel: local sums, cross-rank sum, then the update on every rank
             q = []
             if similar_fill_quirk:  # with the parameters of this step's forward

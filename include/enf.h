@@ -256,6 +256,21 @@ enf_status enf_comm_destroy(enf_comm comm);
 enf_status enf_allreduce_sum(enf_comm comm, void* buf, int64_t count, enf_dtype dtype,
                              void* hip_stream);
 
+/* One rank's DATA-PARALLEL optimize_whitening minibatch step in one call (round 4; src/optimize_whitening.jl:36-42):
+ * the loss / gradient sums of this rank's N columns X (its share of a minibatch of B columns in all; N may be 0),
+ * the cross-rank sum over `comm` (RCCL on hip_stream, of the kernels' double slice totals -- before any rounding
+ * to the dtype; NULL comm: one rank, no all-reduce), then *loss_out = negll (sum / B), ADAGrad on the runs with
+ * gradient / B and the Householder re-normalisation, as enf_whitening_step. Replaces enf_flow_negll_grad +
+ * enf_allreduce_sum + enf_whitening_apply (and the zeroing of their buffer) with gradient + all-reduce + one tail
+ * launch; on one rank (comm NULL or a 1-rank communicator, B = N) identical to enf_whitening_step. workspace:
+ * enf_flow_negll_grad_workspace(N) bytes. Every rank must call it with the same B, runs and batches. */
+enf_status enf_whitening_step_dp(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
+                                 const enf_layer* layers, int32_t nlayers, void* theta, void* acc, const int64_t* runs,
+                                 int32_t nruns, const int64_t* hbatches, int32_t nhb, double eta, double epsilon,
+                                 int64_t B, double* loss_out, enf_comm comm, void* workspace, size_t workspace_bytes,
+                                 void* hip_stream);
+
+
 #ifdef __cplusplus
 }
 #endif

@@ -265,3 +265,65 @@ def test_optimize_whitening_beyond_one_launch(enf, gpu, oracle, case):
     assert abs(res.negll_history[0] - ref0) <= 1e-4 * (abs(ref0) + 1)
     assert np.all(np.isfinite(res.negll_history))
     assert np.mean(res.negll_history[-5:]) < res.negll_history[0]
+
+
+# ------------------------------------------------- data-parallel step in one call (round 4) ----
+@pytest.mark.parametrize("case", ["hj", "20_layers"])
+def test_whitening_step_dp_single_rank_equals_fused(enf, gpu, case):
+    """enf_whitening_step_dp on a one-rank RCCL communicator (gradient, all-reduce of the double slice totals,
+    one tail launch) is bit-identical to the single-rank fused step (enf_whitening_step) and to the three-call
+    data-parallel step (gradient, all-reduce, update as separate launches), for the config-5 flow shape (fused
+    (J o H)^4 kernel) and a chunked 20-layer flow."""
+    rng = np.random.default_rng(4545)
+    if case == "hj":
+        D = 32
+        layers = []
+        for _ in range(4):
+            layers += [(5, rand_params(rng, 5, D, np.float32)), (3, rand_params(rng, 3, D, np.float32))]
+    else:
+        D = 8
+        layers = _long_flow(rng, D, np.float32)
+        layers = [(op, ps) for op, ps in layers if op != 0]  # (no length-D ScaleShift: keep every field a vector)
+    X = colmajor_cuda((rng.standard_normal((D, 20_000)) * 0.7).astype(np.float32))
+    comm = enf.EnfComm.single()
+    try:
+        runs = []
+        for kw in ({}, {"comm": comm}, {"comm": comm, "_separate_update": True}):
+            r = enf.optimize_whitening(X, make_flow(enf, layers), enf.ADAGrad(), nbatches=5, nepochs=2, **kw)
+            runs.append((to_np(r.optimizer_state.theta), to_np(r.optimizer_state.acc), r.negll_history))
+        for th, acc, h in runs[1:]:
+            assert np.array_equal(th, runs[0][0]) and np.array_equal(acc, runs[0][1]) and h == runs[0][2]
+    finally:
+        comm.close()
+
+
+def test_whitening_step_dp_empty_share(enf, gpu):
+    """A rank without columns in a minibatch (N = 0 < B): zero sums, so the loss is 0, ADAGrad leaves theta and
+    acc as they are, and only the Householder re-normalisation acts."""
+    import ctypes
+
+    import torch
+    from euclidiannormalizingflows_jl_amd.train import FlowState, _workspace, householder_batches, trainable_runs
+
+    rng = np.random.default_rng(4546)
+    D = 32
+    layers = [(5, rand_params(rng, 5, D, np.float32)), (3, rand_params(rng, 3, D, np.float32))]
+    st = FlowState(make_flow(enf, layers), D, torch.float32, torch.device("cuda"), enf.ADAGrad())
+    th0, acc0 = to_np(st.theta).copy(), to_np(st.acc).copy()
+    runs = np.ascontiguousarray(np.array(trainable_runs(st), dtype=np.int64).reshape(-1))
+    hbs = np.ascontiguousarray(np.array(householder_batches(st), dtype=np.int64).reshape(-1))
+    ws = _workspace(st, 1000)
+    loss = torch.full((1,), 7.0, dtype=torch.float64, device="cuda")
+    lib = enf._lib
+    lib.check(lib.lib().enf_whitening_step_dp(lib.ENF_F32, D, 0, None, D, st.layers(), len(st.trafos),
+                                              st.theta.data_ptr(), st.acc.data_ptr(), runs.ctypes.data,
+                                              len(runs) // 2, hbs.ctypes.data, len(hbs) // 3, 0.1, 1e-7, 1000,
+                                              loss.data_ptr(), None, ws.data_ptr(), ws.numel() * 8,
+                                              torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert float(loss.cpu()) == 0.0
+    th, acc = to_np(st.theta), to_np(st.acc)
+    assert np.array_equal(acc, acc0)
+    v0 = th0[:D].astype(np.float64)
+    assert np.allclose(th[:D], v0 / np.linalg.norm(v0), rtol=1e-6)
+    assert np.array_equal(th[D:], th0[D:])
