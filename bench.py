@@ -161,11 +161,19 @@ def pmc_evidence(D, N, args):
 PMC_PASSES = ("FETCH_SIZE SQ_WAVES", "WRITE_SIZE",
               "SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE",
               "SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_LDS")
-KERNEL_PAT = "flow_hj_kernel"  # the headline kernel; --inverse: flow_hji_kernel (kernel_pat())
+KERNEL_PAT = "flow_hj_kernel"  # the headline kernel; --inverse: flow_hji_kernel, fp64: flow_hj64_kernel
+# fp64 program (--dtype f64): one more pass with its instruction classes (wave64 VALU instructions)
+PMC_PASS_F64 = ("SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 "
+                "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64")
+# fp64 issue costs on gfx950 at 2 waves per SIMD (profiles/r02_microbench15_fp64_costs.txt: fma/add/mul_f64
+# 2.10 ns vs fma_f32 1.01 ns per wave-instruction, rcp/rsq_f64 6.84 ns), in cycles
+ISSUE_CYC_F64, ISSUE_CYC_F64_TRANS = 4.2, 13.6
 
 
 def kernel_pat(args):
-    return "flow_hji_kernel" if getattr(args, "inverse", False) else KERNEL_PAT
+    if getattr(args, "inverse", False):
+        return "flow_hji_kernel"
+    return "flow_hj64_kernel" if getattr(args, "dtype", "f32") == "f64" else KERNEL_PAT
 PMC_BUDGET_S = 180.0  # all in-run profiler passes together (bench.py's default run stays within minutes)
 
 
@@ -225,7 +233,8 @@ def _pmc_passes(prof, base, work, N, D, args):
         return max(1.0, min(90.0, deadline - time.monotonic()))
 
     per, dur = {}, []
-    for i, grp in enumerate(PMC_PASSES):
+    passes = PMC_PASSES + ((PMC_PASS_F64,) if args.dtype == "f64" else ())
+    for i, grp in enumerate(passes):
         if time.monotonic() >= deadline:
             return None
         d = os.path.join(work, f"p{i}")
@@ -273,6 +282,23 @@ def _pmc_passes(prof, base, work, N, D, args):
             "issue_floor_frac": cyc / (clk * dmed), "mix_cost_frac": mix / (clk * dmed),
             "wait_inst_any_frac": c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"],
             "lds_insts_per_launch": c.get("SQ_INSTS_LDS"), "source": src}
+    if args.dtype == "f64" and all(k in c for k in PMC_PASS_F64.split()):
+        # the fp64 program: classes per element-pair and the issue floor priced with the fp64 costs (fp64
+        # non-transcendental 4.2 cycles, rsq/rcp_f64 13.6, the rest as above)
+        epu = N * D * args.pairs / 64.0
+        f64 = c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"]
+        t64 = c["SQ_INSTS_VALU_TRANS_F64"]
+        rest = max(0.0, c["SQ_INSTS_VALU"] - f64 - t64 - trans)
+        cyc64 = (ISSUE_CYC_F64 * f64 + ISSUE_CYC_F64_TRANS * t64 + ISSUE_CYC_FAST * rest
+                 + ISSUE_CYC_TRANS * trans) / 1024.0
+        valu["f64_per_element_pair"] = {
+            "fma": c["SQ_INSTS_VALU_FMA_F64"] / epu, "add": c["SQ_INSTS_VALU_ADD_F64"] / epu,
+            "mul": c["SQ_INSTS_VALU_MUL_F64"] / epu, "trans": t64 / epu,
+            "int32": c["SQ_INSTS_VALU_INT32"] / epu, "int64": c["SQ_INSTS_VALU_INT64"] / epu,
+            "other": rest / epu}
+        valu["issue_cycle_floor_per_simd"] = cyc64
+        valu["issue_floor_frac"] = cyc64 / (clk * dmed)
+        valu.pop("mix_cost_frac", None)
     return traffic, valu, stats
 
 
@@ -442,7 +468,8 @@ def main():
     traffic, valu, rocprof = None, None, None
     if not args.selftest_cpu:
         live = None
-        if world == 1 and not args.no_pmc and args.pattern is None and args.dtype == "f32" and D in (32, 64, 128):
+        if (world == 1 and not args.no_pmc and args.pattern is None and D in (32, 64, 128)
+                and (args.dtype == "f32" or not args.inverse)):
             try:
                 live = pmc_live(D, N, args)
             except Exception:  # noqa: BLE001 -- the committed summary below, labelled "not this run"
