@@ -214,6 +214,44 @@ __device__ __forceinline__ double logprod64_tab(const double (&q)[NQ], const dou
   return qs < __builtin_huge_val() ? l : qs;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Round 4: the fp64 CenterStretch / CenterContract steps (center_stretch.jl:4-22, enf_steps.h) run on
+// exp64_in, sqrt64_ge1, div64 and the table log instead of ocml's exp / log (42 / 98 VALU instructions each
+// in the gfx950 ISA, log alone 76 of them fp64; an element of the literal CenterContract took 4 exp + 3 log
+// + 3 divisions, ~510 instructions), and JohnsonTrafoInv's ladj on log1p64_tab.
+
+// e^w for |w| <= 1000: n = rint(w log2e), r = w - n ln2 (hi + lo, |r| <= ln2/2), e^r by its Taylor series to
+// r^13 (truncation < 2^-57, as sinh64), then one ldexp (the fp64 Center steps' in-range path, |w| <= 200)
+__device__ __forceinline__ double exp64_in(double w) {
+  constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double kd = __builtin_rint(w * 1.44269504088896340736);
+  const double r = fma(-kd, ln2_lo, fma(-kd, ln2_hi, w));
+  double p = 1.6059043836821614599e-10;
+  p = fma(p, r, 2.0876756987868098979e-09);
+  p = fma(p, r, 2.5052108385441718775e-08);
+  p = fma(p, r, 2.7557319223985890653e-07);
+  p = fma(p, r, 2.7557319223985890653e-06);
+  p = fma(p, r, 2.4801587301587301587e-05);
+  p = fma(p, r, 1.9841269841269841270e-04);
+  p = fma(p, r, 1.3888888888888888889e-03);
+  p = fma(p, r, 8.3333333333333333333e-03);
+  p = fma(p, r, 4.1666666666666666667e-02);
+  p = fma(p, r, 1.6666666666666666667e-01);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return __builtin_amdgcn_ldexp(p, (int)kd);
+}
+
+// log(1 + t) for t >= 0 (t = +Inf gives +Inf) with the table log: log1p64_ge0's TwoSum correction
+__device__ __forceinline__ double log1p64_tab(double t, const double* __restrict__ tab) {
+  const double u = 1.0 + t;
+  const double bv = u - 1.0;
+  const double c = (1.0 - (u - bv)) + (t - bv);
+  const double r = log64_tab(u, 0, tab) + c * __builtin_amdgcn_rcp(u);
+  return u < __builtin_huge_val() ? r : u;
+}
+
 // sinh(w) over the whole double range (johnson_trafo.jl:36), odd, +-Inf -> +-Inf, NaN -> NaN:
 //   |w| < 1: the odd Taylor series to w^17 (truncation < 1e-17 relative);
 //   else e^|w|/2 - e^-|w|/2 with e^|w| = 2^k e^r (msun e_exp.c reduction, |r| <= ln2/2, e^r by its

@@ -29,7 +29,7 @@ static __shared__ double g_logtab[3 * kLogTabN];
 //  SCALESHIFT   W=2 {a, b}                           same
 //  JOHNSON      W=4 {gamma, delta*ln2, xi, 1/lambda} {gamma, delta, xi, 1/lambda}
 //  JOHNSON_INV  W=4 {gamma, 1/delta, xi, lambda}     {gamma, 1/delta, xi, lambda}
-//  CENTER_*     W=8 {b*log2e, c, ln2/b, exp(b*a),    {a, b, c, exp(b*a), exp(2*b*a), 0, ...}
+//  CENTER_*     W=8 {b*log2e, c, ln2/b, exp(b*a),    {a, b, c, exp(b*a), exp(2*b*a), exp(-b*a), 0, 0}
 //                    exp(2*b*a), b*a*log2e, a, b}
 // Layout: [group g][param q][element e] with RV elements per group; element (g, e) is row
 // g*RV + e (D >= RV) or e % D (D < RV). The fragment kernel uses RV = V = 16/sizeof(T), so a
@@ -80,7 +80,8 @@ __device__ __forceinline__ void param_values(int op, const LayerDesc& L, int col
       // double operations as the per-element expressions they replace, so the same values
       out[3] = exp(bv * av);
       out[4] = exp(2.0 * bv * av);
-      for (int q = 5; q < 8; ++q) out[q] = 0.0;
+      out[5] = exp(-bv * av);  // CenterContract: exp(-b(xu + a)) = exp(-b a) / exp(b xu) (round 4)
+      for (int q = 6; q < 8; ++q) out[q] = 0.0;
     }
   }
 }
@@ -114,10 +115,11 @@ __device__ __forceinline__ void neutral_values(int op, T (&out)[8]) {
       out[3] = 1.0f;
       out[4] = 1.0f;
       out[7] = 1.0f;
-    } else {  // {a, b, c, exp(ba), exp(2ba)}
+    } else {  // {a, b, c, exp(ba), exp(2ba), exp(-ba)}
       out[1] = 1.0;
       out[3] = 1.0;
       out[4] = 1.0;
+      out[5] = 1.0;
     }
   }
 }
@@ -316,7 +318,7 @@ __device__ __forceinline__ void step_johnson_inv(Tile<T, D, U>& x, Acc<T, D, U>&
             const double w = (x[u][e] - pg[e]) * pd[e];
             const double sh = sinh64(w);
             x[u][e] = fma(pl[e], sh, px[e]);
-            if (LADJ) acc[u][e / SEG] += 0.5 * log1p64_ge0(sh * sh);
+            if (LADJ) acc[u][e / SEG] += 0.5 * log1p64_tab(sh * sh, g_logtab);
           }
         }
       }
@@ -335,6 +337,24 @@ __device__ __forceinline__ void step_scaleshift(Tile<T, D, U>& x, const T* __res
         for (int e = 0; e < V; ++e) x[u][e] = fma(x[u][e], pa[e], pb[e]);
 }
 
+// fp64 Center steps (round 4): the wave votes on its tile. When every |b x| (stretch) / |b (x - c)|
+// (contract) is <= 200 and every row's b and exp(b a) are moderate (|b| in [1e-100, 1e100], exp(b a) in
+// [1e-50, 1e50]), no exp, sqrt, reciprocal or log below can overflow, underflow or meet Inf, and the wave
+// takes the in-range path: exp64_in / sqrt64_ge1 / div64 / the table log (enf_math64.h), no range selects,
+// and the stretch's ladj without its two exps (b (y - c) = sign(x) log(inner), so exp(-b (yu - a)) and
+// exp(b (yu + a)) are E1 / inner and E1 inner, the two swapping with the sign of x), the contract's four
+// exps from one, P = exp(b xu): P / E1, Ei / P, E1 / P, P E1 (E1 = exp(b a), Ei = exp(-b a), row records).
+// Any other wave runs the reference's formulas literally (ocml), the pre-round-4 code. Instruction counts
+// per element (gfx950 ISA): stretch ~395 -> ~110, contract ~510 -> ~120.
+template <int V>
+__device__ __forceinline__ bool center_rows_moderate(const double (&bv)[V], const double (&E1)[V]) {
+  bool ok = true;
+#pragma unroll
+  for (int e = 0; e < V; ++e)
+    ok = ok && fabs(bv[e]) >= 1e-100 && fabs(bv[e]) <= 1e100 && E1[e] >= 1e-50 && E1[e] <= 1e50;
+  return ok;
+}
+
 template <typename T, int D, int U, bool LADJ>
 __device__ __forceinline__ void step_center_stretch(Tile<T, D, U>& x, Acc<T, D, U>& acc,
                                                     const T* __restrict__ r) {
@@ -342,6 +362,34 @@ __device__ __forceinline__ void step_center_stretch(Tile<T, D, U>& x, Acc<T, D, 
       T rr[8][V];
 #pragma unroll
       for (int q = 0; q < 8; ++q) lds_vec<T, V>(r + q * V, rr[q]);
+  if constexpr (!std::is_same_v<T, float>) {
+    bool in = center_rows_moderate<V>(rr[1], rr[3]);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < V; ++e) in = in && fabs(rr[1][e] * x[u][e]) <= 200.0;
+    if (__all(in)) {
+#pragma unroll
+      for (int e = 0; e < V; ++e)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          // center_stretch.jl:4-8; ladj -contract_ladj(y) (:17-22, :41-42) as dy = 1/(1 + E1/inner) + 1/(1 + E1 inner)
+          const double bv = rr[1][e], c = rr[2][e], E1 = rr[3][e], E2 = rr[4][e];
+          const double xv = x[u][e];
+          const double ex = exp64_in(fabs(bv * xv));
+          const double ome = 1.0 - ex;
+          const double inner = (sqrt64_ge1(ome * ome * E2 + 4.0 * ex) - ome * E1) / 2.0;
+          // sign(x) log(inner): inner = 1 exactly at x = +-0 (log 0, so the sign of zero only reaches -0 + c)
+          x[u][e] = div64(__builtin_copysign(log64_tab(inner, 0, g_logtab), xv), bv) + c;
+          if (LADJ) {
+            const double ri = div64(1.0, inner);
+            const double dy = div64(1.0, fma(E1, ri, 1.0)) + div64(1.0, fma(E1, inner, 1.0));
+            acc[u][e / SEG] -= log64_tab(dy, 0, g_logtab);
+          }
+        }
+      return;
+    }
+  }
 #pragma unroll
       for (int e = 0; e < V; ++e) {
 #pragma unroll
@@ -366,6 +414,7 @@ __device__ __forceinline__ void step_center_stretch(Tile<T, D, U>& x, Acc<T, D, 
               acc[u][e / SEG] -= hw_log2(fabsf(dy));
             }
           } else {
+            // out of range somewhere in the wave: center_stretch.jl:4-8, :17-22 literally (ocml)
             const double av = rr[0][e], bv = rr[1][e], c = rr[2][e], E1 = rr[3][e], E2 = rr[4][e];
             const double xv = x[u][e];
             const double ex = exp(fabs(bv * xv));
@@ -391,6 +440,31 @@ __device__ __forceinline__ void step_center_contract(Tile<T, D, U>& x, Acc<T, D,
       T rr[8][V];
 #pragma unroll
       for (int q = 0; q < 8; ++q) lds_vec<T, V>(r + q * V, rr[q]);
+  if constexpr (!std::is_same_v<T, float>) {
+    bool in = center_rows_moderate<V>(rr[1], rr[3]);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < V; ++e) in = in && fabs(rr[1][e] * (x[u][e] - rr[2][e])) <= 200.0;
+    if (__all(in)) {
+#pragma unroll
+      for (int e = 0; e < V; ++e)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          // center_stretch.jl:11-15 / :17-22 from P = exp(b xu)
+          const double bv = rr[1][e], c = rr[2][e], E1 = rr[3][e], Ei = rr[5][e];
+          const double xu = x[u][e] - c;
+          const double P = exp64_in(bv * xu);
+          const double iP = div64(1.0, P);
+          x[u][e] = div64(log64_tab(1.0 + P * Ei, 0, g_logtab) - log64_tab(1.0 + Ei * iP, 0, g_logtab), bv);
+          if (LADJ) {
+            const double dy = div64(1.0, fma(E1, iP, 1.0)) + div64(1.0, fma(P, E1, 1.0));
+            acc[u][e / SEG] += log64_tab(dy, 0, g_logtab);
+          }
+        }
+      return;
+    }
+  }
 #pragma unroll
       for (int e = 0; e < V; ++e) {
 #pragma unroll
@@ -409,6 +483,7 @@ __device__ __forceinline__ void step_center_contract(Tile<T, D, U>& x, Acc<T, D,
               acc[u][e / SEG] += hw_log2(fabsf(dy));
             }
           } else {
+            // out of range somewhere in the wave: the literal formulas (ocml)
             const double av = rr[0][e], bv = rr[1][e], c = rr[2][e];
             const double xu = x[u][e] - c;
             x[u][e] = (log(1.0 + exp(bv * (xu - av))) - log(1.0 + exp(-bv * (xu + av)))) / bv;

@@ -362,3 +362,85 @@ def test_full_size_round_trip_config4_shard(enf, gpu, oracle):
     inv_layers = _inverse_layers(layers)
     check_vs_oracle(oracle, inv_layers, Ys, X2[:, idx].cpu().numpy(), L2[idx].cpu().numpy(), np.float32,
                     what="config4 shard inverse sample")
+
+
+# ----------------------------------------------------------- fp64 Center steps (round 4) ----
+# The fp64 CenterStretch / CenterContract fragment steps now vote per wave: in range (|b x| <= 200, moderate
+# rows) they run on exp64_in / sqrt64_ge1 / div64 / the table log, with the stretch's ladj exps and three of
+# the contract's four exps replaced by products with the row records; any other wave runs the literal
+# formulas (enf_steps.h). JohnsonTrafoInv's ladj log1p is on the table log. These check both paths over the
+# whole double range against the x87-extended evaluation of the reference's formulas, element by element:
+# set 0 / 1 mix extreme columns into the tile (those waves take the literal path), set 2 keeps every wave
+# in range with |b x| up to ~198.
+def _center_wide_inputs(D, rng, scale):
+    vals = np.array([0.0, -0.0, 1e-300, -1e-300, 5e-324, 1e-20, -1e-12, 1e-5, -0.1, 0.37, -1.0, 2.5, -10.0,
+                     30.0, -100.0, 170.0, -177.0, 178.0, 250.0, -349.0, 351.0, 360.0, -700.0, 705.0, 1e4, -1e10,
+                     1e300, np.inf, -np.inf, np.nan], dtype=np.float64)
+    N = 4096
+    X = rng.standard_normal((D, N)) * scale
+    X[:, : len(vals)] = vals[None, :] / np.linspace(1.0, 2.0, D)[:, None]
+    X[:, len(vals): 2 * len(vals)] = rng.permuted(np.tile(vals, (D, 1)), axis=1)
+    return np.asfortranarray(X)
+
+
+def _per_element_as_accurate(Y, Yt, Yhi, what):
+    """Per element: |y - y_hi| <= max(1e-13 (|y_hi| + 1), 4 |y_ref - y_hi|) where the reference (the oracle in
+    fp64) is finite, the same Inf / NaN where it is not; over the elements with |y_hi| > 1e-6, the RMS relative
+    error at most 2x the reference's own (as accurate as the reference, not just within tolerance)."""
+    Y, Yt, Yhi = (np.asarray(a, dtype=np.float64) for a in (Y, Yt, Yhi))
+    nonfin = ~np.isfinite(Yt)
+    assert np.array_equal(np.isnan(Y[nonfin]), np.isnan(Yt[nonfin])), what
+    inf = nonfin & ~np.isnan(Yt)
+    assert np.array_equal(Y[inf], Yt[inf]), what
+    fin = ~nonfin
+    e = np.abs(Y[fin] - Yhi[fin])
+    bound = np.maximum(1e-13 * (np.abs(Yhi[fin]) + 1.0), 4.0 * np.abs(Yt[fin] - Yhi[fin]))
+    bad = e > bound
+    assert not bad.any(), (what, int(bad.sum()), Y[fin][bad][:4], Yhi[fin][bad][:4], Yt[fin][bad][:4])
+    big = np.abs(Yhi[fin]) > 1e-6
+    rel = e[big] / np.abs(Yhi[fin][big])
+    rel_ref = np.abs(Yt[fin][big] - Yhi[fin][big]) / np.abs(Yhi[fin][big])
+    rms, rms_ref = np.sqrt(np.mean(rel ** 2)), np.sqrt(np.mean(rel_ref ** 2))
+    assert rms <= 2.0 * rms_ref + 1e-17, (what, rms, rms_ref)
+
+
+@pytest.mark.parametrize("op", [1, 2])
+@pytest.mark.parametrize("D", [2, 32])
+def test_fp64_center_wide_range(enf, gpu, oracle, op, D):
+    rng = np.random.default_rng(900 + 10 * op + D)
+    for k, (lo_a, hi_a) in enumerate([(0.0, 2.0), (-1.5, 1.5), (-2.0, 2.0)]):
+        ps = [rng.uniform(lo_a, hi_a, D), rng.uniform(0.5, 2.0, D), rng.uniform(-0.5, 0.5, D)]
+        layers = [(op, ps)]
+        X = _center_wide_inputs(D, rng, 3.0) if k < 2 else np.asfortranarray(rng.uniform(-98.0, 98.0, (D, 8192)))
+        Y, L = enf.with_logabsdet_jacobian(make_flow(enf, layers), colmajor_cuda(X))
+        what = f"op {op} D {D} set {k}"
+        check_vs_oracle(oracle, layers, X, to_np(Y), to_np(L), np.float64, what=what)
+        Yt, Lt = oracle.flow_apply(layers, X, nthreads=8)
+        Yhi, Lhi = oracle.flow_apply_hi(layers, X)
+        _per_element_as_accurate(to_np(Y), Yt, Yhi, what + " y")
+        _per_element_as_accurate(to_np(L).reshape(-1), np.asarray(Lt).reshape(-1), np.asarray(Lhi).reshape(-1),
+                                 what + " ladj")
+
+
+@pytest.mark.parametrize("D", [2, 32])
+def test_fp64_center_flows_and_round_trip(enf, gpu, oracle, D):
+    """The examples' flow shapes in fp64 (nf_example_2d.jl:12-25: ScaleShift o Householder o CenterStretch;
+    nf_example_1d.jl:8-23: CenterStretch o Johnson, and the initial JohnsonTrafo o CenterContract pairs) against
+    the oracle, and stretch o contract round trips."""
+    rng = np.random.default_rng(950 + D)
+    flows = [[(1, rand_params(rng, 1, D, np.float64)), (5, rand_params(rng, 5, D, np.float64)),
+              (0, rand_params(rng, 0, D, np.float64))],
+             [(3, rand_params(rng, 3, D, np.float64)), (1, rand_params(rng, 1, D, np.float64))],
+             [(2, rand_params(rng, 2, D, np.float64)), (3, rand_params(rng, 3, D, np.float64)),
+              (2, rand_params(rng, 2, D, np.float64)), (3, rand_params(rng, 3, D, np.float64))],
+             [(4, rand_params(rng, 4, D, np.float64)), (2, rand_params(rng, 2, D, np.float64))]]
+    X = np.asfortranarray(rng.standard_normal((D, 100_003)) * 2.0)
+    for i, layers in enumerate(flows):
+        Y, L = enf.with_logabsdet_jacobian(make_flow(enf, layers), colmajor_cuda(X))
+        check_vs_oracle(oracle, layers, X, to_np(Y), to_np(L), np.float64, what=f"flow {i} D {D}")
+    ps = rand_params(rng, 1, D, np.float64)
+    Yc, Lc = enf.with_logabsdet_jacobian(make_flow(enf, [(2, ps)]), colmajor_cuda(X))
+    Xr, Lr = enf.with_logabsdet_jacobian(make_flow(enf, [(1, ps)]), Yc)
+    from parity import col_err, ladj_err
+    assert col_err(to_np(Xr), X) < 1e-12
+    assert ladj_err(to_np(Lr), -to_np(Lc)) < 1e-12
