@@ -20,6 +20,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -171,9 +172,20 @@ ISSUE_CYC_F64, ISSUE_CYC_F64_TRANS = 4.2, 13.6
 
 
 def kernel_pat(args):
+    f64 = getattr(args, "dtype", "f32") == "f64"
     if getattr(args, "inverse", False):
-        return "flow_hji_kernel"
-    return "flow_hj64_kernel" if getattr(args, "dtype", "f32") == "f64" else KERNEL_PAT
+        return "flow_hj64_kernel" if f64 else "flow_hji_kernel"
+    return "flow_hj64_kernel" if f64 else KERNEL_PAT
+
+
+def kernel_match(args, name):
+    """True for the measured kernel's rocprofv3 name. The fp64 forward and inverse programs are one template,
+    flow_hj64_kernel<D, U, LM, PAD, OCC, INV> (round 4): its last argument tells them apart (the inverse leg's
+    untimed forward pass runs the forward one)."""
+    if kernel_pat(args) not in name:
+        return False
+    m = re.search(r"flow_hj64_kernel<[^>]*, (true|false)>", name)
+    return m is None or (m.group(1) == "true") == bool(getattr(args, "inverse", False))
 PMC_BUDGET_S = 180.0  # all in-run profiler passes together (bench.py's default run stays within minutes)
 
 
@@ -245,14 +257,14 @@ def _pmc_passes(prof, base, work, N, D, args):
         agg = {}
         with open(os.path.join(d, "run_counter_collection.csv")) as f:
             for r in csv.DictReader(f):
-                if kernel_pat(args) in r["Kernel_Name"]:
+                if kernel_match(args, r["Kernel_Name"]):
                     key = (r["Dispatch_Id"], r["Counter_Name"])
                     agg[key] = agg.get(key, 0.0) + float(r["Counter_Value"])
         for (_, c), v in agg.items():
             per.setdefault(c, []).append(v)
         with open(os.path.join(d, "run_kernel_trace.csv")) as f:
             dur += [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(f)
-                    if kernel_pat(args) in r["Kernel_Name"]]
+                    if kernel_match(args, r["Kernel_Name"])]
     c = {k: sorted(v)[len(v) // 2] for k, v in per.items()}
     if not dur or not all(k in c for k in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "SQ_INSTS_VALU_TRANS_F32",
                                            "GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY")):
@@ -266,7 +278,7 @@ def _pmc_passes(prof, base, work, N, D, args):
     stats = None
     with open(os.path.join(d, "run_kernel_stats.csv")) as f:
         for r in csv.DictReader(f):
-            if kernel_pat(args) in r["Name"]:
+            if kernel_match(args, r["Name"]):
                 stats = {"kernel": r["Name"], "calls": int(r["Calls"]), "average_ms": float(r["AverageNs"]) / 1e6,
                          "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6}
     src = "this run: rocprofv3 --kernel-trace --pmc passes over child runs of this bench (same flow and sizes)"
@@ -468,8 +480,7 @@ def main():
     traffic, valu, rocprof = None, None, None
     if not args.selftest_cpu:
         live = None
-        if (world == 1 and not args.no_pmc and args.pattern is None and D in (32, 64, 128)
-                and (args.dtype == "f32" or not args.inverse)):
+        if world == 1 and not args.no_pmc and args.pattern is None and D in (32, 64, 128):
             try:
                 live = pmc_live(D, N, args)
             except Exception:  # noqa: BLE001 -- the committed summary below, labelled "not this run"

@@ -381,11 +381,10 @@ static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, cons
                                               : launch_hj64_program(a, LADJ, st, dev);
       if (e != hipErrorNotSupported) return e;
     }
-    if constexpr (std::is_same_v<T, float>) {
-      if (!nospec && hji_program_pairs(a) > 0) {
-        hipError_t e = launch_hji_program(a, LADJ, st, dev);
-        if (e != hipErrorNotSupported) return e;
-      }
+    if (!nospec && hji_program_pairs(a) > 0) {
+      hipError_t e = std::is_same_v<T, float> ? launch_hji_program(a, LADJ, st, dev)
+                                              : launch_hji64_program(a, LADJ, st, dev);
+      if (e != hipErrorNotSupported) return e;
     }
     return dispatch_pad<T, LADJ>(a, lds, st, dev);
   }
@@ -420,6 +419,11 @@ static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, cons
     static const int nospec = ENF_KNOB("ENF_NO_SPECIALIZE", 0);
     if (!nospec && hj_program_pairs(a) > 0) {
       hipError_t e = launch_hj64_program(a, LADJ, st, dev);
+      if (e != hipErrorNotSupported) return e;
+    }
+    // the compiled fp64 inverse program (J^-1, H)^n (round 4)
+    if (!nospec && hji_program_pairs(a) > 0) {
+      hipError_t e = launch_hji64_program(a, LADJ, st, dev);
       if (e != hipErrorNotSupported) return e;
     }
   }

@@ -55,11 +55,13 @@ __device__ __forceinline__ float dpp_f(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL,
                                                                0xF, 0xF, false));
 }
+// (mov_dpp with bound_ctrl: every lane of these patterns reads a lane of its own row, so no `old` value is
+// needed and none is materialised -- update_dpp(0, ...) cost two v_mov of zero per stage; round 4)
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double x) {
   const uint64_t u = __builtin_bit_cast(uint64_t, x);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, true);
   return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 template <int CTRL, typename T>

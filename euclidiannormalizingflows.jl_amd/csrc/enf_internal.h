@@ -182,6 +182,7 @@ int hji_program_pairs(const FlowArgs& a);  // (J^-1, H)^n -- the inverse of (J o
 hipError_t launch_hji_program(const FlowArgs& a, int lm, hipStream_t st, const DeviceInfo& dev);
 // the same program in fp64 (enf_flow_hj64.hip); hipErrorNotSupported: not a program
 hipError_t launch_hj64_program(const FlowArgs& a, int lm, hipStream_t st, const DeviceInfo& dev);
+hipError_t launch_hji64_program(const FlowArgs& a, int lm, hipStream_t st, const DeviceInfo& dev);  // fp64 (J^-1, H)^n
 // config 2 (J o H, D = 2, fp64): enf_flow_d2.hip
 bool d2_program(const FlowArgs& a);
 hipError_t launch_d2_program(const FlowArgs& a, int lm, hipStream_t st, const DeviceInfo& dev);

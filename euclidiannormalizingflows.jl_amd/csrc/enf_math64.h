@@ -41,10 +41,12 @@ __device__ __forceinline__ double div64(double n, double d) {
 // one residual correction of g (within 1 ulp)
 __device__ __forceinline__ double sqrt64_ge1(double q) {
   const double y = __builtin_amdgcn_rsq(q);
-  double g = q * y, h = 0.5 * y;
+  double g = q * y;
+  const double h = 0.5 * y;
   const double r = fma(-g, h, 0.5);
   g = fma(g, r, g);
-  h = fma(h, r, h);
+  // the residual q - g^2 is ~2^-44 g, so the seed's h (relative error ~2^-22) suffices for its correction
+  // (2^-66 g); the Goldschmidt update of h is not needed (round 4)
   return fma(fma(-g, g, q), h, g);
 }
 
@@ -132,11 +134,24 @@ __device__ __forceinline__ double log64_tab_b(double u, int kadd, const double* 
   const double kd = (double)k;
   const double lhi = fma(kd, ln2_hi, t[1]);
   const double llo = fma(kd, ln2_lo, t[2]);
-  // log1p(r) = r + r^2 P(r), P to r^(NP-2): |r| <= 2^-(B+1), truncation r^NP/NP < 2^-53 r
-  constexpr int NP = B >= 8 ? 7 : B >= 7 ? 8 : B >= 5 ? 10 : 12;
-  double p = ((NP - 1) & 1 ? 1.0 : -1.0) / (NP - 1);
+  double p;
+  if constexpr (B == 5) {
+    // log1p(r) = r + r^2 P(r) with P the degree-6 Chebyshev economisation of (log1p(r) - r)/r^2 on
+    // the reduced range [-0.01515, 2^-6] widened by 2 % (tools/gen_logtab.py --poly; round 4): relative error
+    // 2^-57.1 of log1p, as the Taylor form to r^9 it replaces (2^-57.4), with one FMA fewer
+    p = fma(-0.12485538735806584, r, 0.14290490248495968);
+    p = fma(p, r, -0.16666671910057598);
+    p = fma(p, r, 0.19999999413011174);
+    p = fma(p, r, -0.24999999999589934);
+    p = fma(p, r, 0.33333333333351384);
+    p = fma(p, r, -0.5);
+  } else {
+    // log1p(r) = r + r^2 P(r), P to r^(NP-2): |r| <= 2^-(B+1), truncation r^NP/NP < 2^-53 r
+    constexpr int NP = B >= 8 ? 7 : B >= 7 ? 8 : 12;
+    p = ((NP - 1) & 1 ? 1.0 : -1.0) / (NP - 1);
 #pragma unroll
-  for (int n = NP - 2; n >= 2; --n) p = fma(p, r, (n & 1 ? 1.0 : -1.0) / n);
+    for (int n = NP - 2; n >= 2; --n) p = fma(p, r, (n & 1 ? 1.0 : -1.0) / n);
+  }
   return lhi + (r + fma(r * r, p, llo));
 }
 
@@ -145,7 +160,7 @@ __device__ __forceinline__ double log64_tab(double u, int kadd, const double* __
 }
 
 // asinh(x) over the whole double range, odd, +-Inf -> +-Inf, NaN -> NaN, with the table log:
-//   a = |x| < 2^26: s = sqrt(1 + a^2) as s1 + corr (rsq seed, one Goldschmidt step; corr carries
+//   a = |x| < 2^26: s = sqrt(1 + a^2) as s1 + corr (rsq seed, one Goldschmidt step on s1 only; corr carries
 //     the residual q - s1^2 AND the rounding of q = fl(1 + a^2), e_q = fma(a, a, 1 - q) exactly);
 //     u = fl(a + s1) and c its exact error (Fast2Sum) plus corr: a + sqrt(1 + a^2) = u + c, so
 //     asinh a = log(u) + c/u, and 1/u = s - a exactly (math), computed as (s1 - a) + corr (s1 - a
@@ -158,10 +173,10 @@ __device__ __forceinline__ double asinh64_tab(double x, const double* __restrict
   const bool big = a >= 67108864.0;
   const double q = fma(a, a, 1.0);
   const double y = __builtin_amdgcn_rsq(q);
-  double g = q * y, h = 0.5 * y;
+  double g = q * y;
+  const double h = 0.5 * y;  // the seed's 1/(2 s): enough for corr (~2^-44 s, so its error is ~2^-66 s)
   const double rr = fma(-g, h, 0.5);
   g = fma(g, rr, g);
-  h = fma(h, rr, h);
   const double eq = fma(a, a, 1.0 - q);
   const double corr = (fma(-g, g, q) + eq) * h;
   const double u0 = a + g;
@@ -181,10 +196,10 @@ __device__ __forceinline__ double asinh64_tab_fin(double x, const double* __rest
   const double a = __builtin_fabs(x);
   const double q = fma(a, a, 1.0);
   const double y = __builtin_amdgcn_rsq(q);
-  double g = q * y, h = 0.5 * y;
+  double g = q * y;
+  const double h = 0.5 * y;  // the seed's 1/(2 s): enough for corr (~2^-44 s, so its error is ~2^-66 s)
   const double rr = fma(-g, h, 0.5);
   g = fma(g, rr, g);
-  h = fma(h, rr, h);
   const double eq = fma(a, a, 1.0 - q);
   const double corr = (fma(-g, g, q) + eq) * h;
   const double u0 = a + g;
@@ -297,6 +312,35 @@ __device__ __forceinline__ double sinh64(double w) {
   double res = a < 1.0 ? small : big;
   res = a < __builtin_huge_val() ? res : a;  // Inf stays Inf, NaN stays NaN
   return __builtin_copysign(res, w);
+}
+
+// sinh(w) for |w| < ~709 (the compiled fp64 inverse program's in-range path, round 4; its range check admits
+// |w| < ~347), branch-free, with msun's expm1 form (s_sinh.c): t = expm1(|w|), sinh = (t + t/(t + 1))/2 (an
+// identity for every w; both terms >= 0, so no cancellation). expm1(a) = 2^k (1 + em) - 1 = fma(2^k, em,
+// 2^k - 1) with k = rint(a/ln2), r = a - k ln2 (hi + lo), em = expm1(r) = r + r^2 P(r), P the degree-10
+// Chebyshev economisation on |r| <= ln2/2 (tools/gen_logtab.py --poly-expm1: relative error 2^-60.7); 2^k - 1 is
+// exact (k <= 53; beyond it the 1 no longer matters). t/(t + 1) as div64. One v_rcp_f64, ~28 fp64 instructions,
+// against sinh64's two exp-form evaluations plus the Taylor series.
+__device__ __forceinline__ double sinh64_in(double w) {
+  constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double a = __builtin_fabs(w);
+  const double kd = __builtin_rint(a * 1.44269504088896340736);
+  const double r = fma(-kd, ln2_lo, fma(-kd, ln2_hi, a));
+  double p = fma(2.0914686968086876e-09, r, 2.5105217004720745e-08);
+  p = fma(p, r, 2.75572736431103e-07);
+  p = fma(p, r, 2.7557255400206422e-06);
+  p = fma(p, r, 2.4801587325547743e-05);
+  p = fma(p, r, 0.00019841269874820627);
+  p = fma(p, r, 0.0013888888888883748);
+  p = fma(p, r, 0.008333333333326136);
+  p = fma(p, r, 0.04166666666666667);
+  p = fma(p, r, 0.1666666666666667);
+  p = fma(p, r, 0.5);
+  const double em = fma(r * r, p, r);
+  const double S = __builtin_amdgcn_ldexp(1.0, (int)kd);
+  const double t = fma(S, em, S - 1.0);
+  const double d = div64(t, t + 1.0);
+  return __builtin_copysign(0.5 * (t + d), w);
 }
 
 }  // namespace enf

@@ -120,6 +120,35 @@ def test_inverse_program_vs_oracle(enf, gpu, oracle, D):
     assert ladj_err(to_np(Lr).reshape(-1)[ok], -to_np(L).reshape(-1)[ok]) < 1e-4
 
 
+@pytest.mark.parametrize("D,pairs", [(24, 4), (32, 1), (32, 4), (32, 8), (64, 4), (100, 4), (128, 2)])
+def test_inverse_program_fp64_vs_oracle(enf, gpu, oracle, D, pairs):
+    """The compiled fp64 inverse program (enf_flow_hj64.hip flow_hj64_kernel<..., INV = true>: sinh64_in, the
+    q products carried across the pairs) against the oracle at fp64 rtol 1e-12: forward outputs, raw normal
+    columns, columns large enough to leave the in-range path (the wave's tile is redone on sinh64 /
+    log1p64_tab), Inf and NaN; then the round trip through the compiled fp64 forward program."""
+    rng = np.random.default_rng(7100 + 10 * D + pairs)
+    fwd = _hj_layers(rng, D, pairs, np.float64)
+    layers = _inverse_layers(fwd)
+    N = 40_009
+    X0 = np.asfortranarray(rng.standard_normal((D, N)))
+    X, _ = oracle.flow_apply(fwd, X0, nthreads=8)
+    X = np.asfortranarray(X)
+    X[:, 1000:1400] = 0.5 * X0[:, 1000:1400]
+    X[:, 7:11] *= 40.0
+    X[:, 12:14] *= 1e3  # sinh overflows the q product: the redo path
+    X[:, 20] = np.inf
+    X[3, 21] = np.nan
+    Y, L = enf.with_logabsdet_jacobian(make_flow(enf, layers), colmajor_cuda(X))
+    check_vs_oracle(oracle, layers, X, to_np(Y), to_np(L), np.float64, what=f"fp64 inverse program D={D} n={pairs}")
+    Xr, Lr = enf.with_logabsdet_jacobian(make_flow(enf, fwd), Y)
+    ok = np.r_[22:1000, 1400:N]
+    from parity import col_err, ladj_err
+    assert col_err(to_np(Xr)[:, ok], X[:, ok]) < 1e-9
+    assert ladj_err(to_np(Lr).reshape(-1)[ok], -to_np(L).reshape(-1)[ok]) < 1e-9
+    # f(X) without the ladj gives the same outputs
+    assert np.array_equal(to_np(make_flow(enf, layers)(colmajor_cuda(X))), to_np(Y), equal_nan=True)
+
+
 # ------------------------------------------------------------------ chunked training (round 4) ----
 # VERDICT r03 missing item 1: the reference differentiates ANY composed flow (src/optimize_whitening.jl:18-22,
 # 25-45); the gradient / VJP / whitening step now run flows beyond one launch's bounds (more than 16 layers or
