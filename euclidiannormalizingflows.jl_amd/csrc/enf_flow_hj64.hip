@@ -9,7 +9,7 @@
 //   y   = fma(delta, asinh64_tab(z), gamma),       ladj += log|delta/lambda| - log(q_1 ... q_R)/2
 // with q = fma(z, z, 1) and one table logarithm per column and lane of the product of the lane's R = 8 q of
 // every pair (round 4; before, one per pair), carried as a mantissa and an exponent sum so that it never
-// overflows. A tile in which some |z| of the wave is huge (a q product of 2^1000), Inf or NaN is redone from X on the whole-range
+// overflows. A tile in which some |z| of the wave reaches 2^26, Inf or NaN is redone from X on the whole-range
 // path (asinh64_tab over the whole double range, logprod64_tab per pair: Inf / NaN propagate as the
 // reference's log(1/sqrt(Inf)) / NaN do).
 //
@@ -245,8 +245,8 @@ __device__ __forceinline__ double h64_mant(double v, int& ke) {
 
 // One pair. FULL = false (the tile's first pass): the range-free asinh64_tab_fin, and the ladj's q products
 // carried across the pairs as a mantissa pm in [1, 2) and an exponent sum pk (one table log per tile and lane
-// instead of one per pair; round 4), with far set when a q product of this lane reaches 2^1000, Inf or NaN
-// (some |z| >= 2^500, Inf or NaN) -- no branch,
+// instead of one per pair; round 4), with far set when some |z| of this lane reaches 2^26, Inf or NaN -- no
+// branch,
 // so the pair loop has no per-pair vote and no register copies at a join. FULL = true: asinh64_tab over the
 // whole double range and logprod64_tab per pair into acc (the tile's redo when some lane of the wave was far).
 template <int D, int U, bool LADJ, bool FULL>
@@ -289,17 +289,21 @@ __device__ __forceinline__ void h64_pair(double (&x)[U][8], double (&acc)[U], do
   h64_param(r + H64_DL * 8, pd);
   h64_param(r + H64_GM * 8, pg);
   if constexpr (!FULL) {
-    // The product of the lane's 8 q is the range check too: below 2^1000 every q is (so |z| < 2^500 and
-    // finite), where the range-free asinh64_tab_fin holds (q = fl(1 + z^2) and s = sqrt(q) stay finite; above
-    // 2^26 it is within an ulp of asinh64_tab's log(2a) form); Inf / NaN z make it Inf / NaN. The product
-    // times the tile's running mantissa (< 2^1001) is renormalised. One compare per 8 elements instead of one
-    // per element.
+    // Range check: every q of the lane below 2^52 (|z| < 2^26, where asinh64_tab_fin equals asinh64_tab; past
+    // ~2^40 its 1/u = (s1 - a) + corr loses to rounding, tools/asinh64_tab_check.hip), as the largest high
+    // word of the 8 q (q >= 1, so the unsigned order of the high words is the order of the values; +Inf and
+    // NaN compare above): three v_max3_u32 and one compare per 8 elements instead of a compare per element.
+    // The product of the 8 q (< 2^416) times the tile's running mantissa is renormalised.
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+      uint32_t mx = 0;
       double p = q[u][0];
 #pragma unroll
-      for (int e = 1; e < 8; ++e) p *= q[u][e];
-      far = far || !(p < 0x1p1000);
+      for (int e = 0; e < 8; ++e) {
+        mx = max(mx, (uint32_t)(__builtin_bit_cast(uint64_t, q[u][e]) >> 32));
+        if (e) p *= q[u][e];
+      }
+      far = far || !(mx < 0x43300000u);  // 2^52
       if (LADJ) pm[u] = h64_mant(pm[u] * p, pk[u]);
     }
 #pragma unroll
@@ -379,7 +383,7 @@ __device__ __forceinline__ void h64i_pair(double (&x)[U][8], double (&acc)[U], d
     for (int e = 0; e < 8; ++e) x[u][e] = fma(-dot[u], vh[e], x[u][e]);
 }
 
-// A tile: every pair on the in-range path; if any lane of the wave met a huge, Inf or NaN z (a wave-uniform
+// A tile: every pair on the in-range path; if any lane of the wave left it (a wave-uniform
 // vote after the last pair), the wave reloads the tile's X (not yet overwritten: Y is stored after this) and
 // redoes every pair on the whole-range path.
 template <int D, int U, int LM, bool TAIL, bool PAD, bool INV>

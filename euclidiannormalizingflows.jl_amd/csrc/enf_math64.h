@@ -121,7 +121,9 @@ __device__ __forceinline__ double log1p64_ge0(double t) {
 // and lost that in LDS bank conflicts (profiles/r03_c2_table_bits_nt.txt);
 // j = 0 has 1/c = 1 exactly, so log(1 + tiny) keeps full relative accuracy. tab: the table in LDS
 // (3 doubles per entry), filled by the kernel prologue.
-template <int B>
+// FOLD (round 4, measured variant): k ln2 as one fma with the double nearest ln2 into the table's hi part, the
+// table's lo part added directly (one fma fewer; error k (ln2 - RN(ln2)) ~ k 2.3e-17 more)
+template <int B, bool FOLD = false>
 __device__ __forceinline__ double log64_tab_b(double u, int kadd, const double* __restrict__ tab) {
   constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
   const uint64_t b = __builtin_bit_cast(uint64_t, u);
@@ -132,8 +134,8 @@ __device__ __forceinline__ double log64_tab_b(double u, int kadd, const double* 
   const double* t = tab + 3 * j;
   const double r = fma(m, t[0], -1.0);
   const double kd = (double)k;
-  const double lhi = fma(kd, ln2_hi, t[1]);
-  const double llo = fma(kd, ln2_lo, t[2]);
+  const double lhi = FOLD ? fma(kd, 6.93147180559945286227e-01, t[1]) : fma(kd, ln2_hi, t[1]);
+  const double llo = FOLD ? t[2] : fma(kd, ln2_lo, t[2]);
   double p;
   if constexpr (B == 5) {
     // log1p(r) = r + r^2 P(r) with P the degree-6 Chebyshev economisation of (log1p(r) - r)/r^2 on
@@ -191,7 +193,7 @@ __device__ __forceinline__ double asinh64_tab(double x, const double* __restrict
 // asinh64_tab for |x| < 2^26 and finite only (no range selects): the fused kernels take it for a wave whose
 // arguments are all in that range (a wave-uniform vote), asinh64_tab otherwise. Same operations and
 // roundings as asinh64_tab's a < 2^26 branch, so the same results there.
-template <int B = kLogTabBits>
+template <int B = kLogTabBits, bool FOLD = false>
 __device__ __forceinline__ double asinh64_tab_fin(double x, const double* __restrict__ tab) {
   const double a = __builtin_fabs(x);
   const double q = fma(a, a, 1.0);
@@ -205,7 +207,7 @@ __device__ __forceinline__ double asinh64_tab_fin(double x, const double* __rest
   const double u0 = a + g;
   const double c0 = (a - (u0 - g)) + corr;
   const double cu = c0 * ((g - a) + corr);
-  return __builtin_copysign(log64_tab_b<B>(u0, 0, tab) + cu, x);
+  return __builtin_copysign(log64_tab_b<B, FOLD>(u0, 0, tab) + cu, x);
 }
 // true when asinh64_tab_fin applies to x (|x| < 2^26; false for Inf and NaN)
 __device__ __forceinline__ bool asinh64_fin_ok(double x) { return __builtin_fabs(x) < 67108864.0; }
@@ -340,6 +342,9 @@ __device__ __forceinline__ double sinh64_in(double w) {
   const double S = __builtin_amdgcn_ldexp(1.0, (int)kd);
   const double t = fma(S, em, S - 1.0);
   const double d = div64(t, t + 1.0);
+  // (t + d for every |w|: max 2.3 ulp, mean 0.31 (sinh64: 1.6 / 0.26), tools/asinh64_tab_check.hip. msun's
+  // 2t - t d below |w| = 1 would take ~1 ulp off the small-|w| side for a select per element: +5 VALU per
+  // element of the inverse program, not taken.)
   return __builtin_copysign(0.5 * (t + d), w);
 }
 

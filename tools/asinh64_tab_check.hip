@@ -1,7 +1,8 @@
 // Accuracy probe of the fp64 table functions of enf_math64.h that the compiled fp64 program uses (design probe,
-// not product; round 4): asinh64_tab_fin over |x| < 2^500 (the range flow_hj64_kernel's product check admits),
+// not product; round 4): asinh64_tab_fin over |x| < 2^26 (the range flow_hj64_kernel's check admits) and,
+// to show why the check is needed, over 2^26 .. 2^500 (1/u = (s1 - a) + corr loses to rounding past ~2^40),
 // asinh64_tab over the whole double range, log64_tab over u >= 1 (the degree-6 log1p polynomial), each in ulps
-// against x86 long-double asinhl / logl; sinh64_in (the fp64 inverse program's sinh) and sinh64 over |w| < 709
+// against x86 long-double asinhl / logl (also their FOLD variants); sinh64_in (the fp64 inverse program's sinh) and sinh64 over |w| < 709
 // against sinhl.
 // Build: hipcc --offload-arch=gfx950 -O3 -I euclidiannormalizingflows.jl_amd/csrc \
 //          -o tools/asinh64_tab_check tools/asinh64_tab_check.hip
@@ -28,6 +29,8 @@ __global__ __launch_bounds__(256) void eval(const double* x, double* y, long n) 
   if (F == 2) y[i] = enf::log64_tab(v, 0, enf::kLogTab);
   if (F == 3) y[i] = enf::sinh64_in(v);
   if (F == 4) y[i] = enf::sinh64(v);
+  if (F == 5) y[i] = enf::asinh64_tab_fin<enf::kLogTabBits, true>(v, enf::kLogTab);
+  if (F == 6) y[i] = enf::log64_tab_b<enf::kLogTabBits, true>(v, 0, enf::kLogTab);
 }
 
 static double ulps(double got, long double ref) {
@@ -63,15 +66,19 @@ int main() {
   CK(hipMalloc(&dy, n * 8));
   CK(hipMemcpy(dx, xs.data(), n * 8, hipMemcpyHostToDevice));
   std::vector<double> y(n);
-  const char* nm[5] = {"asinh64_tab_fin (|x| < 2^500)", "asinh64_tab", "log64_tab (u >= 1)",
-                       "sinh64_in (|w| < 709)", "sinh64 (|w| < 709)"};
-  for (int f = 0; f < 5; ++f) {
+  const char* nm[8] = {"asinh64_tab_fin (|x| < 2^26)", "asinh64_tab", "log64_tab (u >= 1)",
+                       "sinh64_in (|w| < 709)", "sinh64 (|w| < 709)", "asinh64_tab_fin FOLD", "log64_tab FOLD",
+                       "asinh64_tab_fin 2^26..2^500"};
+  for (int f = 0; f < 8; ++f) {
     const int blocks = (n + 255) / 256;
     if (f == 0) eval<0><<<blocks, 256>>>(dx, dy, n);
     if (f == 1) eval<1><<<blocks, 256>>>(dx, dy, n);
     if (f == 2) eval<2><<<blocks, 256>>>(dx, dy, n);
     if (f == 3) eval<3><<<blocks, 256>>>(dx, dy, n);
     if (f == 4) eval<4><<<blocks, 256>>>(dx, dy, n);
+    if (f == 5) eval<5><<<blocks, 256>>>(dx, dy, n);
+    if (f == 6) eval<6><<<blocks, 256>>>(dx, dy, n);
+    if (f == 7) eval<0><<<blocks, 256>>>(dx, dy, n);
     CK(hipDeviceSynchronize());
     CK(hipMemcpy(y.data(), dy, n * 8, hipMemcpyDeviceToHost));
     double worst = 0, sum = 0;
@@ -79,12 +86,15 @@ int main() {
     for (long i = 0; i < n; ++i) {
       const double v = xs[i];
       long double ref;
-      if (f == 0) {
-        if (!(std::fabs(v) < 0x1p500)) continue;
+      if (f == 0 || f == 5) {
+        if (!(std::fabs(v) < 0x1p26)) continue;
+        ref = asinhl((long double)v);
+      } else if (f == 7) {
+        if (!(std::fabs(v) >= 0x1p26 && std::fabs(v) < 0x1p500)) continue;
         ref = asinhl((long double)v);
       } else if (f == 1) {
         ref = asinhl((long double)v);
-      } else if (f == 2) {
+      } else if (f == 2 || f == 6) {
         if (!(v >= 1.0) || std::isinf(v)) continue;
         ref = logl((long double)v);
       } else {
