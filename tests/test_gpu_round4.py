@@ -149,6 +149,27 @@ def test_inverse_program_fp64_vs_oracle(enf, gpu, oracle, D, pairs):
     assert np.array_equal(to_np(make_flow(enf, layers)(colmajor_cuda(X))), to_np(Y), equal_nan=True)
 
 
+@pytest.mark.parametrize("inverse", [False, True])
+def test_fp64_programs_wide_range_columns(enf, gpu, oracle, inverse):
+    """The compiled fp64 programs' range checks (round 4): columns scaled by 1e4 .. 1e300 -- |z| past 2^26 where
+    the forward's range-free asinh64_tab_fin stops being exact (tools/asinh64_tab_check.hip: it is garbage past
+    ~2^48), |w| past sinh's overflow for the inverse -- sit in the same waves as ordinary columns; their tiles
+    must be redone on the whole-range path. Against the oracle at fp64 rtol 1e-12, every column."""
+    rng = np.random.default_rng(7300 + inverse)
+    D, N = 32, 20_011
+    fwd = _hj_layers(rng, D, 4, np.float64)
+    layers = _inverse_layers(fwd) if inverse else fwd
+    X = np.asfortranarray(rng.standard_normal((D, N)))
+    scales = [1e4, 1e8, 1e12, 1e30, 1e100, 1e200, 1e300]
+    for i, s in enumerate(scales):
+        X[:, 100 * i + 3] *= s  # one column per wave tile region, the rest of the wave ordinary
+        X[5, 100 * i + 50] = s  # a single large element
+        X[6, 100 * i + 51] = -s
+    Y, L = enf.with_logabsdet_jacobian(make_flow(enf, layers), colmajor_cuda(X))
+    check_vs_oracle(oracle, layers, X, to_np(Y), to_np(L), np.float64,
+                    what=f"fp64 {'inverse' if inverse else 'forward'} program, wide-range columns")
+
+
 # ------------------------------------------------------------------ chunked training (round 4) ----
 # VERDICT r03 missing item 1: the reference differentiates ANY composed flow (src/optimize_whitening.jl:18-22,
 # 25-45); the gradient / VJP / whitening step now run flows beyond one launch's bounds (more than 16 layers or
