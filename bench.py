@@ -467,8 +467,10 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / args.steps if stream is not None else wall / args.steps * 1e3
     per_launch = None
     if stream is not None:
-        pl = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
-        per_launch = {"min": pl[0], "median": pl[len(pl) // 2], "max": pl[-1], "launches": len(pl)}
+        seq = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+        pl = sorted(seq)
+        per_launch = {"min": pl[0], "median": pl[len(pl) // 2], "max": pl[-1], "launches": len(pl),
+                      "in_order": [round(v, 4) for v in seq]}
     t_local, kern_ms_max = max_over_ranks([wall, kern_ms], dev, world)
     per_rank_kernel_ms = gather_ranks(kern_ms, dev, world, rank)
     ms_per_step = t_local / args.steps * 1e3

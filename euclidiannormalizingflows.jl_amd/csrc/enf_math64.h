@@ -147,6 +147,13 @@ __device__ __forceinline__ double log64_tab_b(double u, int kadd, const double* 
     p = fma(p, r, -0.24999999999589934);
     p = fma(p, r, 0.33333333333351384);
     p = fma(p, r, -0.5);
+  } else if constexpr (B == 6) {
+    // the B = 6 table (diagnostics A/B of the fp64 program, round 4): degree 5 on |r| <= 2^-7 (--poly 6 5: 2^-56.9)
+    p = fma(0.14282159536610894, r, -0.16667838296658544);
+    p = fma(p, r, 0.20000000262923848);
+    p = fma(p, r, -0.2499999997254017);
+    p = fma(p, r, 0.3333333333333005);
+    p = fma(p, r, -0.500000000000001);
   } else {
     // log1p(r) = r + r^2 P(r), P to r^(NP-2): |r| <= 2^-(B+1), truncation r^NP/NP < 2^-53 r
     constexpr int NP = B >= 8 ? 7 : B >= 7 ? 8 : 12;

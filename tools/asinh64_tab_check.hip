@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "enf_math64.h"
+#include "enf_logtab_b78.h"
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
@@ -31,6 +32,8 @@ __global__ __launch_bounds__(256) void eval(const double* x, double* y, long n) 
   if (F == 4) y[i] = enf::sinh64(v);
   if (F == 5) y[i] = enf::asinh64_tab_fin<enf::kLogTabBits, true>(v, enf::kLogTab);
   if (F == 6) y[i] = enf::log64_tab_b<enf::kLogTabBits, true>(v, 0, enf::kLogTab);
+  if (F == 8) y[i] = enf::asinh64_tab_fin<6>(v, enf::kLogTabB6);
+  if (F == 9) y[i] = enf::log64_tab_b<6>(v, 0, enf::kLogTabB6);
 }
 
 static double ulps(double got, long double ref) {
@@ -66,10 +69,10 @@ int main() {
   CK(hipMalloc(&dy, n * 8));
   CK(hipMemcpy(dx, xs.data(), n * 8, hipMemcpyHostToDevice));
   std::vector<double> y(n);
-  const char* nm[8] = {"asinh64_tab_fin (|x| < 2^26)", "asinh64_tab", "log64_tab (u >= 1)",
+  const char* nm[10] = {"asinh64_tab_fin (|x| < 2^26)", "asinh64_tab", "log64_tab (u >= 1)",
                        "sinh64_in (|w| < 709)", "sinh64 (|w| < 709)", "asinh64_tab_fin FOLD", "log64_tab FOLD",
-                       "asinh64_tab_fin 2^26..2^500"};
-  for (int f = 0; f < 8; ++f) {
+                       "asinh64_tab_fin 2^26..2^500", "asinh64_tab_fin B=6", "log64_tab B=6"};
+  for (int f = 0; f < 10; ++f) {
     const int blocks = (n + 255) / 256;
     if (f == 0) eval<0><<<blocks, 256>>>(dx, dy, n);
     if (f == 1) eval<1><<<blocks, 256>>>(dx, dy, n);
@@ -79,6 +82,8 @@ int main() {
     if (f == 5) eval<5><<<blocks, 256>>>(dx, dy, n);
     if (f == 6) eval<6><<<blocks, 256>>>(dx, dy, n);
     if (f == 7) eval<0><<<blocks, 256>>>(dx, dy, n);
+    if (f == 8) eval<8><<<blocks, 256>>>(dx, dy, n);
+    if (f == 9) eval<9><<<blocks, 256>>>(dx, dy, n);
     CK(hipDeviceSynchronize());
     CK(hipMemcpy(y.data(), dy, n * 8, hipMemcpyDeviceToHost));
     double worst = 0, sum = 0;
@@ -86,7 +91,7 @@ int main() {
     for (long i = 0; i < n; ++i) {
       const double v = xs[i];
       long double ref;
-      if (f == 0 || f == 5) {
+      if (f == 0 || f == 5 || f == 8) {
         if (!(std::fabs(v) < 0x1p26)) continue;
         ref = asinhl((long double)v);
       } else if (f == 7) {
@@ -94,7 +99,7 @@ int main() {
         ref = asinhl((long double)v);
       } else if (f == 1) {
         ref = asinhl((long double)v);
-      } else if (f == 2 || f == 6) {
+      } else if (f == 2 || f == 6 || f == 9) {
         if (!(v >= 1.0) || std::isinf(v)) continue;
         ref = logl((long double)v);
       } else {
