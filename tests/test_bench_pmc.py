@@ -141,3 +141,26 @@ def test_pmc_live_time_budget(monkeypatch, rocprof_present, tmp_path):
     monkeypatch.setattr(bench, "_run_group", lambda cmd, t, log: (seen.append(t), run(cmd, t, log))[1])
     assert bench.pmc_live(32, 10_000_000, _args()) is not None
     assert seen and all(0 < t <= 90.0 for t in seen)
+
+
+def test_kernel_match_tells_the_fp64_programs_apart():
+    """The fp64 forward and inverse programs are one template, flow_hj64_kernel<D, U, LM, PAD, OCC, INV> (round 4):
+    the in-run profiler passes of an --inverse --dtype f64 line must follow the INV = true launches only (the
+    line's untimed forward pass runs the forward one), and the forward line the INV = false ones."""
+    import types
+
+    import bench
+
+    fwd = "void enf::flow_hj64_kernel<32, 1, 1, false, 1, false>(enf::HJ64Args)"
+    inv = "void enf::flow_hj64_kernel<32, 1, 1, false, 1, true>(enf::HJ64Args)"
+    pad_inv = "void enf::flow_hj64_kernel<128, 1, 2, true, 1, true>(enf::HJ64Args)"
+    a = types.SimpleNamespace(dtype="f64", inverse=True)
+    assert bench.kernel_match(a, inv) and bench.kernel_match(a, pad_inv) and not bench.kernel_match(a, fwd)
+    a = types.SimpleNamespace(dtype="f64", inverse=False)
+    assert bench.kernel_match(a, fwd) and not bench.kernel_match(a, inv)
+    a = types.SimpleNamespace(dtype="f32", inverse=False)
+    assert bench.kernel_match(a, "void enf::flow_hj_kernel<32, 8, 2, 1, 4, 0, 1, false>(enf::HJArgs)")
+    assert not bench.kernel_match(a, fwd)
+    a = types.SimpleNamespace(dtype="f32", inverse=True)
+    assert bench.kernel_match(a, "void enf::flow_hji_kernel<32, 8, 2, 1, false>(enf::HJArgs)")
+    assert not bench.kernel_match(a, "void enf::flow_hj_kernel<32, 8, 2, 1, 4, 0, 1, false>(enf::HJArgs)")
