@@ -34,9 +34,6 @@
 #include "enf_internal.h"
 #include "enf_logtab.h"
 #include "enf_math64.h"
-#if ENF_DIAG
-#include "enf_logtab_b78.h"  // kLogTabB6: the B = 6 table of the diagnostics A/B (ENF_HJ64_TB=6)
-#endif
 
 namespace enf {
 
@@ -61,14 +58,10 @@ struct HJ64Args {
 };
 
 // LDS: [scratch: per pair {hs, cl} + ctot][log table][ladj staging: 4 waves x kStagePerWave][records]
-// (TB: the table's bits, 5 in the product; 6 only in the diagnostics build's A/B)
 constexpr size_t kHj64Scratch = ((2 * kHj64MaxPairs + 2) * sizeof(double) + 15) / 16 * 16;
-template <int TB>
-constexpr size_t hj64_tab_bytes() { return ((3 * ((1 << TB) + 1)) * sizeof(double) + 15) / 16 * 16; }
-template <int TB>
-constexpr size_t hj64_header() { return kHj64Scratch + hj64_tab_bytes<TB>() + 4 * kStagePerWave * sizeof(double); }
-template <int TB>
-static size_t hj64_lds_bytes(int D, int n) { return hj64_header<TB>() + (size_t)n * kHj64W * D * sizeof(double); }
+constexpr size_t kHj64Tab = ((3 * kLogTabN) * sizeof(double) + 15) / 16 * 16;
+constexpr size_t kHj64Header = kHj64Scratch + kHj64Tab + 4 * kStagePerWave * sizeof(double);
+static size_t hj64_lds_bytes(int D, int n) { return kHj64Header + (size_t)n * kHj64W * D * sizeof(double); }
 
 template <int D, int U>
 struct H64Lay {
@@ -173,18 +166,12 @@ __device__ __forceinline__ void h64_store(const HJ64Args& a, double ctot, int64_
 
 // Block prologue: the log table, then per pair (one wave each) v'v and sum_d log|delta/lambda| in double,
 // then the records. ctot = the sum of the per-pair constants (INV: their negation, -johnsontrafo_ladj).
-template <int D, bool INV, int TB>
+template <int D, bool INV>
 __device__ void build_hj64_program(const HJ64Args& a, double* __restrict__ rec, double* __restrict__ scr,
                                    double* __restrict__ tab, double* ctot) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int n = a.n;
-#if ENF_DIAG
-  const double* src = TB == 6 ? kLogTabB6 : kLogTab;
-#else
-  static_assert(TB == kLogTabBits, "the product's table");
-  const double* src = kLogTab;
-#endif
-  for (int i = threadIdx.x; i < 3 * ((1 << TB) + 1); i += blockDim.x) tab[i] = src[i];
+  for (int i = threadIdx.x; i < 3 * kLogTabN; i += blockDim.x) tab[i] = kLogTab[i];
   for (int p = wave; p < n; p += nw) {
     double vv = 0.0, cl = 0.0;
     for (int d = lane; d < a.dreal; d += 64) {  // the batch's rows (padded rows: neutral records below)
@@ -262,7 +249,7 @@ __device__ __forceinline__ double h64_mant(double v, int& ke) {
 // branch,
 // so the pair loop has no per-pair vote and no register copies at a join. FULL = true: asinh64_tab over the
 // whole double range and logprod64_tab per pair into acc (the tile's redo when some lane of the wave was far).
-template <int D, int U, bool LADJ, bool FULL, int TB = kLogTabBits>
+template <int D, int U, bool LADJ, bool FULL>
 __device__ __forceinline__ void h64_pair(double (&x)[U][8], double (&acc)[U], double (&pm)[U], int (&pk)[U],
                                          bool& far, const double* __restrict__ r, const double* __restrict__ tab) {
   constexpr int G = H64Lay<D, U>::G;
@@ -322,15 +309,15 @@ __device__ __forceinline__ void h64_pair(double (&x)[U][8], double (&acc)[U], do
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) x[u][e] = fma3_f64(pd[e], asinh64_tab_fin<TB>(x[u][e], tab), pg[e]);
+      for (int e = 0; e < 8; ++e) x[u][e] = fma3_f64(pd[e], asinh64_tab_fin(x[u][e], tab), pg[e]);
   } else {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) x[u][e] = fma(pd[e], asinh64_tab<TB>(x[u][e], tab), pg[e]);
+      for (int e = 0; e < 8; ++e) x[u][e] = fma(pd[e], asinh64_tab(x[u][e], tab), pg[e]);
     if (LADJ)
 #pragma unroll
-      for (int u = 0; u < U; ++u) acc[u] -= 0.5 * logprod64_tab<8, TB>(q[u], tab);
+      for (int u = 0; u < U; ++u) acc[u] -= 0.5 * logprod64_tab<8>(q[u], tab);
   }
 }
 
@@ -399,7 +386,7 @@ __device__ __forceinline__ void h64i_pair(double (&x)[U][8], double (&acc)[U], d
 // A tile: every pair on the in-range path; if any lane of the wave left it (a wave-uniform
 // vote after the last pair), the wave reloads the tile's X (not yet overwritten: Y is stored after this) and
 // redoes every pair on the whole-range path.
-template <int D, int U, int LM, bool TAIL, bool PAD, bool INV, int TB>
+template <int D, int U, int LM, bool TAIL, bool PAD, bool INV>
 __device__ __forceinline__ void h64_tile(const HJ64Args& a, const double* __restrict__ rec, const double* tab,
                                          double ctot, double* stage, int64_t col0, double (&x)[U][8],
                                          const double (&old)[H64Lay<D, U>::NLS]) {
@@ -414,35 +401,34 @@ __device__ __forceinline__ void h64_tile(const HJ64Args& a, const double* __rest
   bool far = false;
   for (int p = 0; p < a.n; ++p) {
     if constexpr (INV) h64i_pair<D, U, (LM > 0), false>(x, acc, pm, pk, far, rec + (size_t)p * kHj64W * D, tab);
-    else h64_pair<D, U, (LM > 0), false, TB>(x, acc, pm, pk, far, rec + (size_t)p * kHj64W * D, tab);
+    else h64_pair<D, U, (LM > 0), false>(x, acc, pm, pk, far, rec + (size_t)p * kHj64W * D, tab);
   }
   if (__builtin_expect(__any(far), 0)) {
     h64_load<D, U, TAIL, PAD>(a, col0, x);
     for (int p = 0; p < a.n; ++p) {
       if constexpr (INV) h64i_pair<D, U, (LM > 0), true>(x, acc, pm, pk, far, rec + (size_t)p * kHj64W * D, tab);
-      else h64_pair<D, U, (LM > 0), true, TB>(x, acc, pm, pk, far, rec + (size_t)p * kHj64W * D, tab);
+      else h64_pair<D, U, (LM > 0), true>(x, acc, pm, pk, far, rec + (size_t)p * kHj64W * D, tab);
     }
   } else if constexpr (LM > 0) {
     // -+log(prod q)/2 over the pairs: log(pm 2^pk), pm in [1, 2)
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc[u] += (INV ? 0.5 : -0.5) * log64_tab_b<TB>(pm[u], pk[u], tab);
+    for (int u = 0; u < U; ++u) acc[u] += (INV ? 0.5 : -0.5) * log64_tab(pm[u], pk[u], tab);
   }
   h64_store<D, U, LM, TAIL, PAD>(a, ctot, col0, x, acc, old, stage);
 }
 
 // OCC: minimum waves per SIMD the register allocation must allow (1: no constraint; the D = 32 / 64 program
 // takes 164 VGPRs, 3 waves per SIMD; OCC = 4 caps it at 128). INV: the inverse program (J^-1, H)^n (round 4).
-template <int D, int U, int LM, bool PAD = false, int OCC = 1, bool INV = false, int TB = kLogTabBits>
+template <int D, int U, int LM, bool PAD = false, int OCC = 1, bool INV = false>
 __global__ __launch_bounds__(256, OCC) void flow_hj64_kernel(HJ64Args a) {
-  static_assert(!INV || TB == kLogTabBits, "the inverse's log1p64_tab reads the B = 5 table");
   using L = H64Lay<D, U>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* scr = reinterpret_cast<double*>(smem);
   double* ctotp = scr + 2 * kHj64MaxPairs;
   double* tab = reinterpret_cast<double*>(smem + kHj64Scratch);
-  double* stage = reinterpret_cast<double*>(smem + kHj64Scratch + hj64_tab_bytes<TB>()) + (threadIdx.x >> 6) * kStagePerWave;
-  double* rec = reinterpret_cast<double*>(smem + hj64_header<TB>());
-  build_hj64_program<D, INV, TB>(a, rec, scr, tab, ctotp);
+  double* stage = reinterpret_cast<double*>(smem + kHj64Scratch + kHj64Tab) + (threadIdx.x >> 6) * kStagePerWave;
+  double* rec = reinterpret_cast<double*>(smem + kHj64Header);
+  build_hj64_program<D, INV>(a, rec, scr, tab, ctotp);
   const double ctot = *ctotp;
   const double* myrec = rec + ((threadIdx.x & 63) % L::G) * kHj64W * 8;
   constexpr int64_t CT = L::TC;
@@ -459,7 +445,7 @@ __global__ __launch_bounds__(256, OCC) void flow_hj64_kernel(HJ64Args a) {
       const int64_t t1 = t + nwaves;
       const bool more = t1 < ntiles_full;
       h64_load<D, U, false, PAD>(a, (more ? t1 : t) * CT, xb);  // prefetch (the current tile again at the end)
-      h64_tile<D, U, LM, false, PAD, INV, TB>(a, myrec, tab, ctot, stage, t * CT, xa, old);
+      h64_tile<D, U, LM, false, PAD, INV>(a, myrec, tab, ctot, stage, t * CT, xa, old);
       if (!more) break;
       h64_load_old<D, U, LM>(a, t1 * CT, old, false);
 #pragma unroll
@@ -473,18 +459,18 @@ __global__ __launch_bounds__(256, OCC) void flow_hj64_kernel(HJ64Args a) {
     const int64_t c0 = ntiles_full * CT;
     h64_load<D, U, true, PAD>(a, c0, xa);
     h64_load_old<D, U, LM>(a, c0, old, true);
-    h64_tile<D, U, LM, true, PAD, INV, TB>(a, myrec, tab, ctot, stage, c0, xa, old);
+    h64_tile<D, U, LM, true, PAD, INV>(a, myrec, tab, ctot, stage, c0, xa, old);
   }
 }
 
-template <int D, int U, int LM, bool PAD = false, int OCC = 1, bool INV = false, int TB = kLogTabBits>
+template <int D, int U, int LM, bool PAD = false, int OCC = 1, bool INV = false>
 static hipError_t launch_hj64(const HJ64Args& h, hipStream_t st, const DeviceInfo& dev) {
-  const size_t lds = hj64_lds_bytes<TB>(D, h.n);
-  const void* k = reinterpret_cast<const void*>(&flow_hj64_kernel<D, U, LM, PAD, OCC, INV, TB>);
+  const size_t lds = hj64_lds_bytes(D, h.n);
+  const void* k = reinterpret_cast<const void*>(&flow_hj64_kernel<D, U, LM, PAD, OCC, INV>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)H64Lay<D, U>::TC * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_hj64_kernel<D, U, LM, PAD, OCC, INV, TB>), dim3((unsigned)blocks), dim3(256), lds, st, h);
+  hipLaunchKernelGGL((flow_hj64_kernel<D, U, LM, PAD, OCC, INV>), dim3((unsigned)blocks), dim3(256), lds, st, h);
   return hipGetLastError();
 }
 
@@ -494,11 +480,6 @@ static hipError_t launch_hj64_lm(const HJ64Args& h, int lm, hipStream_t st, cons
   // ENF_HJ64_OCC (diagnostics build): 4 = the register allocation capped for 4 waves per SIMD (A/B)
   static const int occ = ENF_KNOB("ENF_HJ64_OCC", 1);
   if (occ == 4 && lm == 1 && !PAD && D <= 64) return launch_hj64<D, 1, 1, false, 4, INV>(h, st, dev);
-  // ENF_HJ64_TB (diagnostics build, round 4): 6 = the forward program on the B = 6 log table (A/B)
-  static const int tb = ENF_KNOB("ENF_HJ64_TB", 5);
-  if constexpr (!INV) {
-    if (tb == 6 && lm == 1 && !PAD && D <= 64) return launch_hj64<D, 1, 1, false, 1, false, 6>(h, st, dev);
-  }
 #endif
   if (lm == 0) return launch_hj64<D, 1, 0, PAD, 1, INV>(h, st, dev);
   if (lm == 1) return launch_hj64<D, 1, 1, PAD, 1, INV>(h, st, dev);

@@ -148,7 +148,9 @@ __device__ __forceinline__ double log64_tab_b(double u, int kadd, const double* 
     p = fma(p, r, 0.33333333333351384);
     p = fma(p, r, -0.5);
   } else if constexpr (B == 6) {
-    // the B = 6 table (diagnostics A/B of the fp64 program, round 4): degree 5 on |r| <= 2^-7 (--poly 6 5: 2^-56.9)
+    // the B = 6 table (round 4, measured and not taken: in flow_hj64_kernel 2.374-2.385 vs 2.400-2.418 ms, -1.3 %,
+    // for asinh max 1.97 vs 1.50 ulp; profiles/r04_hj64_tb_ab.jsonl, tools/asinh64_tab_check.hip): degree 5 on
+    // |r| <= 2^-7 (--poly 6 5: 2^-56.9)
     p = fma(0.14282159536610894, r, -0.16667838296658544);
     p = fma(p, r, 0.20000000262923848);
     p = fma(p, r, -0.2499999997254017);
