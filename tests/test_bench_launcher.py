@@ -29,6 +29,8 @@ def run_bench(*args, env_extra=None):
 def test_bench_single_rank_line():
     out = run_bench()
     assert out["n_gpus"] == 1 and out["steps"] == 3 and out["warmup"] == 1
+    # the settle phase is reported in the line (the CPU stand-in step never settles a GPU clock)
+    assert out["settle"]["launches"] == 0 and "steady clock" in out["settle"]["why"]
     assert out["distributed"]["world_size"] == 1 and len(out["distributed"]["per_rank_kernel_ms"]) == 1
     assert out["value"] == pytest.approx(1000 * 3 / (out["ms_per_step"] * 3 / 1e3), rel=1e-6)
 
