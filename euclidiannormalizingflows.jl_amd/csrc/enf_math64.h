@@ -331,10 +331,10 @@ __device__ __forceinline__ double sinh64(double w) {
 // 2^k - 1) with k = rint(a/ln2), r = a - k ln2 (hi + lo), em = expm1(r) = r + r^2 P(r), P the degree-10
 // Chebyshev economisation on |r| <= ln2/2 (tools/gen_logtab.py --poly-expm1: relative error 2^-60.7); 2^k - 1 is
 // exact (k <= 53; beyond it the 1 no longer matters). t/(t + 1) as div64. One v_rcp_f64, ~28 fp64 instructions,
-// against sinh64's two exp-form evaluations plus the Taylor series.
-__device__ __forceinline__ double sinh64_in(double w) {
+// against sinh64's two exp-form evaluations plus the Taylor series. expm1_64_in (a >= 0) is shared with the fp64
+// CenterContract's in-range path (enf_steps.h).
+__device__ __forceinline__ double expm1_64_in(double a) {
   constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
-  const double a = __builtin_fabs(w);
   const double kd = __builtin_rint(a * 1.44269504088896340736);
   const double r = fma(-kd, ln2_lo, fma(-kd, ln2_hi, a));
   double p = fma(2.0914686968086876e-09, r, 2.5105217004720745e-08);
@@ -349,7 +349,11 @@ __device__ __forceinline__ double sinh64_in(double w) {
   p = fma(p, r, 0.5);
   const double em = fma(r * r, p, r);
   const double S = __builtin_amdgcn_ldexp(1.0, (int)kd);
-  const double t = fma(S, em, S - 1.0);
+  return fma(S, em, S - 1.0);
+}
+
+__device__ __forceinline__ double sinh64_in(double w) {
+  const double t = expm1_64_in(__builtin_fabs(w));
   const double d = div64(t, t + 1.0);
   // (t + d for every |w|: max 2.3 ulp, mean 0.31 (sinh64: 1.6 / 0.26), tools/asinh64_tab_check.hip. msun's
   // 2t - t d below |w| = 1 would take ~1 ulp off the small-|w| side for a select per element: +5 VALU per

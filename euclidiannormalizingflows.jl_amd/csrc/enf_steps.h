@@ -29,7 +29,7 @@ static __shared__ double g_logtab[3 * kLogTabN];
 //  SCALESHIFT   W=2 {a, b}                           same
 //  JOHNSON      W=4 {gamma, delta*ln2, xi, 1/lambda} {gamma, delta, xi, 1/lambda}
 //  JOHNSON_INV  W=4 {gamma, 1/delta, xi, lambda}     {gamma, 1/delta, xi, lambda}
-//  CENTER_*     W=8 {b*log2e, c, ln2/b, exp(b*a),    {a, b, c, exp(b*a), exp(2*b*a), exp(-b*a), 0, 0}
+//  CENTER_*     W=8 {b*log2e, c, ln2/b, exp(b*a),    {a, b, c, exp(b*a), exp(2*b*a), exp(-b*a), 1/b, 0}
 //                    exp(2*b*a), b*a*log2e, a, b}
 // Layout: [group g][param q][element e] with RV elements per group; element (g, e) is row
 // g*RV + e (D >= RV) or e % D (D < RV). The fragment kernel uses RV = V = 16/sizeof(T), so a
@@ -81,7 +81,8 @@ __device__ __forceinline__ void param_values(int op, const LayerDesc& L, int col
       out[3] = exp(bv * av);
       out[4] = exp(2.0 * bv * av);
       out[5] = exp(-bv * av);  // CenterContract: exp(-b(xu + a)) = exp(-b a) / exp(b xu) (round 4)
-      for (int q = 6; q < 8; ++q) out[q] = 0.0;
+      out[6] = 1.0 / bv;       // the in-range paths multiply by it instead of dividing (round 4, last session)
+      out[7] = 0.0;
     }
   }
 }
@@ -115,11 +116,12 @@ __device__ __forceinline__ void neutral_values(int op, T (&out)[8]) {
       out[3] = 1.0f;
       out[4] = 1.0f;
       out[7] = 1.0f;
-    } else {  // {a, b, c, exp(ba), exp(2ba), exp(-ba)}
+    } else {  // {a, b, c, exp(ba), exp(2ba), exp(-ba), 1/b}
       out[1] = 1.0;
       out[3] = 1.0;
       out[4] = 1.0;
       out[5] = 1.0;
+      out[6] = 1.0;
     }
   }
 }
@@ -374,16 +376,19 @@ __device__ __forceinline__ void step_center_stretch(Tile<T, D, U>& x, Acc<T, D, 
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           // center_stretch.jl:4-8; ladj -contract_ladj(y) (:17-22, :41-42) as dy = 1/(1 + E1/inner) + 1/(1 + E1 inner)
-          const double bv = rr[1][e], c = rr[2][e], E1 = rr[3][e], E2 = rr[4][e];
+          // = (inner (1 + E1 inner) + inner + E1) / ((inner + E1)(1 + E1 inner)): one division instead of three
+          // (every term positive: inner >= 1, E1 > 0), and log(inner) / b as a product with the record's 1/b
+          // (round 4, last session)
+          const double bv = rr[1][e], c = rr[2][e], E1 = rr[3][e], E2 = rr[4][e], ib = rr[6][e];
           const double xv = x[u][e];
           const double ex = exp64_in(fabs(bv * xv));
           const double ome = 1.0 - ex;
           const double inner = (sqrt64_ge1(ome * ome * E2 + 4.0 * ex) - ome * E1) / 2.0;
           // sign(x) log(inner): inner = 1 exactly at x = +-0 (log 0, so the sign of zero only reaches -0 + c)
-          x[u][e] = div64(__builtin_copysign(log64_tab(inner, 0, g_logtab), xv), bv) + c;
+          x[u][e] = fma(__builtin_copysign(log64_tab(inner, 0, g_logtab), xv), ib, c);
           if (LADJ) {
-            const double ri = div64(1.0, inner);
-            const double dy = div64(1.0, fma(E1, ri, 1.0)) + div64(1.0, fma(E1, inner, 1.0));
+            const double pe = fma(E1, inner, 1.0), ie = inner + E1;
+            const double dy = div64(fma(inner, pe, ie), ie * pe);
             acc[u][e / SEG] -= log64_tab(dy, 0, g_logtab);
           }
         }
@@ -451,14 +456,22 @@ __device__ __forceinline__ void step_center_contract(Tile<T, D, U>& x, Acc<T, D,
       for (int e = 0; e < V; ++e)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          // center_stretch.jl:11-15 / :17-22 from P = exp(b xu)
-          const double bv = rr[1][e], c = rr[2][e], E1 = rr[3][e], Ei = rr[5][e];
-          const double xu = x[u][e] - c;
-          const double P = exp64_in(bv * xu);
-          const double iP = div64(1.0, P);
-          x[u][e] = div64(log64_tab(1.0 + P * Ei, 0, g_logtab) - log64_tab(1.0 + Ei * iP, 0, g_logtab), bv);
+          // center_stretch.jl:11-15 / :17-22 in t = b xu (round 4, last session): with P = e^|t| and A = b a,
+          // b y = log(1 + e^(t-A)) - log(1 + e^(-t-A)) is odd in t, and for t >= 0 it is
+          // log1p(e^-A (P^2 - 1) / (P + e^-A)), P^2 - 1 = em (2 + em), em = expm1(|t|): one log1p of a
+          // positive argument instead of a difference of two logs (which cancels near t = 0 -- this form does
+          // not); dy = 1/(1 + e^(-(t-A))) + 1/(1 + e^(t+A)) is even in t, = P/(P + E1) + 1/(1 + P E1)
+          // = (P (1 + P E1) + P + E1) / ((P + E1)(1 + P E1)), one division. (E1 = e^A, Ei = e^-A, ib = 1/b.)
+          const double bv = rr[1][e], c = rr[2][e], E1 = rr[3][e], Ei = rr[5][e], ib = rr[6][e];
+          const double t = bv * (x[u][e] - c);
+          const double em = expm1_64_in(fabs(t));
+          const double P = 1.0 + em;
+          const double arg = div64(Ei * (em * (2.0 + em)), P + Ei);
+          // (+ 0.0: the reference's difference is +0 at t = +-0, so its y is +0 / b; the product keeps that sign)
+          x[u][e] = (__builtin_copysign(log1p64_tab(arg, g_logtab), t) + 0.0) * ib;
           if (LADJ) {
-            const double dy = div64(1.0, fma(E1, iP, 1.0)) + div64(1.0, fma(P, E1, 1.0));
+            const double pe = fma(P, E1, 1.0), pi = P + E1;
+            const double dy = div64(fma(P, pe, pi), pi * pe);
             acc[u][e / SEG] += log64_tab(dy, 0, g_logtab);
           }
         }
