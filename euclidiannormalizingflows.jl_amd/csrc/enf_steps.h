@@ -412,11 +412,12 @@ __device__ __forceinline__ void step_center_stretch(Tile<T, D, U>& x, Acc<T, D, 
             const float y = sg * L * lnb + c;
             x[u][e] = y;
             if (LADJ) {
-              const float yu = y - c;
-              const float e1 = hw_exp2(fmaf(-bl, yu, bal));
-              const float e2 = hw_exp2(fmaf(bl, yu, bal));
-              const float dy = hw_rcp(1.0f + e1) + hw_rcp(1.0f + e2);
-              acc[u][e / SEG] -= hw_log2(fabsf(dy));
+              // -contract_ladj(y): exp(-b(yu - a)) and exp(b(yu + a)) are E1/inner and E1 inner (b yu = sign(x)
+              // log(inner); the two swap with the sign of x), so dy = inner/(inner + E1) + 1/(1 + E1 inner) --
+              // two rcp instead of two exp2 and two rcp (round 4, last session, as the fp64 in-range path). inner =
+              // +Inf: Inf * rcp(Inf) is NaN and fminf takes the 1 (the reference's 1/(1 + 0)).
+              const float dy = fminf(inner * hw_rcp(inner + E1), 1.0f) + hw_rcp(fmaf(E1, inner, 1.0f));
+              acc[u][e / SEG] -= hw_log2(dy);
             }
           } else {
             // out of range somewhere in the wave: center_stretch.jl:4-8, :17-22 literally (ocml)
@@ -488,12 +489,16 @@ __device__ __forceinline__ void step_center_contract(Tile<T, D, U>& x, Acc<T, D,
             const float xu = x[u][e] - c;
             const float e1 = hw_exp2(fmaf(bl, xu, -bal));   // exp(b(xu - a))
             const float e2 = hw_exp2(fmaf(-bl, xu, -bal));  // exp(-b(xu + a))
-            x[u][e] = (hw_log2(1.0f + e1) - hw_log2(1.0f + e2)) * lnb;
+            // exp(-b(xu - a)) = 1/e1 and exp(b(xu + a)) = 1/e2, so dy = e1/(1 + e1) + e2/(1 + e2), and
+            // log(1 + e1) - log(1 + e2) = log((1 + e1)/(1 + e2)): two exp2, two rcp and two log2 instead of four
+            // exp2, two rcp and three log2 (round 4, last session; the output the same with or without the ladj).
+            // An overflowing e (Inf * rcp(Inf) = NaN) gives its term 1 through fminf, as the reference's
+            // 1/(1 + 0); (1 + e1) r2 is Inf / 0 exactly where the reference's difference of logs is +-Inf.
+            const float r2 = hw_rcp(1.0f + e2);
+            x[u][e] = hw_log2((1.0f + e1) * r2) * lnb;
             if (LADJ) {
-              const float e3 = hw_exp2(fmaf(-bl, xu, bal));  // exp(-b(xu - a))
-              const float e4 = hw_exp2(fmaf(bl, xu, bal));   // exp(b(xu + a))
-              const float dy = hw_rcp(1.0f + e3) + hw_rcp(1.0f + e4);
-              acc[u][e / SEG] += hw_log2(fabsf(dy));
+              const float dy = fminf(e1 * hw_rcp(1.0f + e1), 1.0f) + fminf(e2 * r2, 1.0f);
+              acc[u][e / SEG] += hw_log2(dy);
             }
           } else {
             // out of range somewhere in the wave: the literal formulas (ocml)
