@@ -266,7 +266,35 @@ __device__ __forceinline__ void step_johnson(Tile<T, D, U>& x, Acc<T, D, U>& acc
         // y = gamma + delta*asinh(z) (asinh64_tab: enf_math64.h, the table log, no reciprocal);
         // ladj: -log(prod of the fragment column segment's q = 1 + z^2)/2, one table log per segment
         // (exponents summed as integers, so no product overflows; q = +Inf gives -Inf as the
-        // reference's log(1/sqrt(Inf)) does)
+        // reference's log(1/sqrt(Inf)) does). Round 4, last session: a wave whose |z| are all below 2^26
+        // takes the range-free asinh64_tab_fin (the same values there) and the plain table log of the
+        // segment's q product (< 2^104), as the compiled fp64 programs do.
+        bool far = false;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int e = 0; e < V; ++e) far = far || !asinh64_fin_ok((x[u][e] - px[e]) * pl[e]);
+        if (!__any(far)) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            double q[V];
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+              const double z = (x[u][e] - px[e]) * pl[e];
+              x[u][e] = fma(pd[e], asinh64_tab_fin(z, g_logtab), pg[e]);
+              q[e] = fma(z, z, 1.0);
+            }
+            if (LADJ)
+#pragma unroll
+              for (int c = 0; c < CPF; ++c) {
+                double qp = q[c * SEG];
+#pragma unroll
+                for (int e = 1; e < SEG; ++e) qp *= q[c * SEG + e];
+                acc[u][c] -= 0.5 * log64_tab(qp, 0, g_logtab);
+              }
+          }
+          return;
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           double q[V];
