@@ -384,6 +384,11 @@ def main():
         sys.exit(rc)
     world, rank, local_rank = enf_launch.rank_env()
     enf_launch.check_world(args.gpus, world)
+    # stdout carries only the one JSON line: everything else written to file descriptor 1 from here on (RCCL's
+    # version banner when a communicator initialises, library prints) goes to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
 
     backend = "gloo" if args.selftest_cpu else "nccl"
@@ -574,7 +579,7 @@ def main():
             "cpu_baseline": cpu,
             "train": train,
         }
-        print(json.dumps(out))
+        print(json.dumps(out), file=json_out, flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 
