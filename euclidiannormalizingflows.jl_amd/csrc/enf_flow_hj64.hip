@@ -246,8 +246,7 @@ __device__ __forceinline__ double h64_mant(double v, int& ke) {
 // One pair. FULL = false (the tile's first pass): the range-free asinh64_tab_fin, and the ladj's q products
 // carried across the pairs as a mantissa pm in [1, 2) and an exponent sum pk (one table log per tile and lane
 // instead of one per pair; round 4), with far set when some |z| of this lane reaches 2^26, Inf or NaN -- no
-// branch,
-// so the pair loop has no per-pair vote and no register copies at a join. FULL = true: asinh64_tab over the
+// branch, so the pair loop has no per-pair vote and no register copies at a join. FULL = true: asinh64_tab over the
 // whole double range and logprod64_tab per pair into acc (the tile's redo when some lane of the wave was far).
 template <int D, int U, bool LADJ, bool FULL>
 __device__ __forceinline__ void h64_pair(double (&x)[U][8], double (&acc)[U], double (&pm)[U], int (&pk)[U],
@@ -292,7 +291,8 @@ __device__ __forceinline__ void h64_pair(double (&x)[U][8], double (&acc)[U], do
     // Range check: every q of the lane below 2^52 (|z| < 2^26, where asinh64_tab_fin equals asinh64_tab; past
     // ~2^40 its 1/u = (s1 - a) + corr loses to rounding, tools/asinh64_tab_check.hip), as the largest high
     // word of the 8 q (q >= 1, so the unsigned order of the high words is the order of the values; +Inf and
-    // NaN compare above): three v_max3_u32 and one compare per 8 elements instead of a compare per element.
+    // NaN of either sign compare above): three v_max3_u32 and one compare per 8 elements instead of a compare per
+    // element.
     // The product of the 8 q (< 2^416) times the tile's running mantissa is renormalised.
 #pragma unroll
     for (int u = 0; u < U; ++u) {
