@@ -359,10 +359,11 @@ def main():
     ap.add_argument("--N", type=int, default=10_000_000, help="samples per GPU")
     ap.add_argument("--pairs", type=int, default=4, help="number of (Householder, Johnson) pairs")
     ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
-    ap.add_argument("--settle-ms", type=float, default=100.0,
+    ap.add_argument("--settle-ms", type=float, default=200.0,
                     help="before the warmup steps, run the flow for this long (wall clock) so that the GPU reaches "
                          "its steady clock: the first ~25 launches of the 0.7 ms headline kernel run 0.86 -> 0.63 ms "
-                         "(profiles/r04_bench_order_*.json), longer than the driver's 5 warmup steps; 0 disables")
+                         "(profiles/r04_bench_order_*.json), longer than the driver's 5 warmup steps; 200 ms leaves a 10x margin "
+                         "for nodes whose power management settles more slowly; 0 disables")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-train", action="store_true", help="skip the config-5 training leg (`train` object)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of each CPU baseline leg")
