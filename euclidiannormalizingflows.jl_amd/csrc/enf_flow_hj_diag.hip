@@ -621,6 +621,11 @@ hipError_t diag_dispatch_hj(const HJArgs& a, int D, int lm, int dbg, hipStream_t
     if (lm == 1) return launch_hjm_d<1>(D, v, a, st, dev);
     return launch_hjm_d<2>(D, v, a, st, dev);
   }
+  // ENF_HJ_R16 (round 4, last session): the D = 64 program with 16 rows per lane and one column per lane tile
+  // (4 lanes per column: two DPP stages per dot instead of three, one ladj log2 per 16 rows) against the product's
+  // 8 rows x 2 columns
+  static const int r16 = ENF_KNOB("ENF_HJ_R16", 0);
+  if (r16 && dbg == 0 && D == 64 && lm == 1) return launch_hj<64, 16, 1, 1, 4>(a, st, dev);
   if (D != 32 || lm != 1) return hipErrorNotSupported;
   static const int as = ENF_KNOB("ENF_HJ_ASINH", 1);
   if (dbg == 0 && as == 1) return hipErrorNotSupported;
