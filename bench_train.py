@@ -114,6 +114,10 @@ def main():
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="one process: rank 0's data-parallel step at this world size (its share of each minibatch)")
     ap.add_argument("--breakdown", action="store_true", help="per-phase event times of eager steps after the timed ones")
+    ap.add_argument("--example", choices=["1d", "2d"], default=None,
+                    help="the reference examples' training loops (examples/nf_example_1d.jl, nf_example_2d.jl): their "
+                         "flows, N = 1e5, nbatches and nepochs, fp64; steps/s of graph-replayed epochs beside the "
+                         "oracle's optimize_whitening on the host (one thread)")
     args = ap.parse_args()
 
     # N > 1 started by hand: start the N ranks as child processes before anything touches a GPU
@@ -138,6 +142,9 @@ def main():
         from enf_pkg import load
 
         load()._lib.use_diagnostics_library()
+    if args.example:
+        print(json.dumps(example_leg(dev, args.example)))
+        return
     res = train_leg(dev, world, rank, D=args.D, N=args.N, nbatches=args.nbatches, pairs=args.pairs, steps=args.steps,
                     warmup=args.warmup, graph=bool(args.graph), comm_kind=args.comm, history=args.history,
                     emulate_world=args.emulate_world or None, breakdown=args.breakdown)
@@ -351,6 +358,110 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
     if comm is not None:
         comm.close()
     return res
+
+
+def example_flows(example):
+    """(D, true flow, initial flow, nbatches, nepochs) of a reference example, layers innermost first:
+    nf_example_1d.jl:8-10,20-29 (X = CenterStretch o JohnsonTrafo (randn), initial J o inverse(C) o J o inverse(C),
+    nbatches 100, nepochs 10) and nf_example_2d.jl:12-15,21-30 (X = ScaleShift o Householder o CenterStretch
+    (randn), initial inverse(C) o inverse(H(randn(2))) o ScaleShift, nbatches 1000, nepochs 10)."""
+    a = lambda *v: np.array(v, dtype=np.float64)
+    if example == "1d":
+        true = [(3, [a(10.0), a(3.5), a(10.0), a(1.0)]), (1, [a(4.0), a(1.0), a(0.0)])]
+        init = [(2, [a(0.0), a(1.0), a(0.0)]), (3, [a(0.0), a(5.0), a(0.0), a(5.0)]),
+                (2, [a(0.0), a(1.0), a(0.0)]), (3, [a(0.0), a(5.0), a(0.0), a(5.0)])]
+        return 1, true, init, 100, 10
+    rs = np.random.default_rng(2)
+    true = [(1, [a(4.0, 4.1), a(2.0, 2.1), a(3.0, 3.1)]), (5, [a(1.0, 0.3)]), (0, [a(1.3, 0.4), a(2.5, -1.2)])]
+    init = [(0, [a(1.0, 1.0), a(0.0, 0.0)]), (5, [rs.standard_normal(2)]), (2, [a(0.0, 0.0), a(1.0, 1.0), a(0.0, 0.0)])]
+    return 2, true, init, 1000, 10
+
+
+def example_leg(dev, example, N=100_000):
+    """The reference example's optimize_whitening on the device (fp64, ADAGrad, graph=True: one epoch captured as
+    a HIP graph and replayed per epoch) after one untimed warm-up run; steps/s over the replayed epochs (the
+    capture of the epoch's launches is timed separately), beside the oracle's optimize_whitening on the host."""
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # bench: the CPU baseline and the parity check of the history only
+
+    from enf_pkg import load
+
+    enf = load()
+    D, true, init, nbatches, nepochs = example_flows(example)
+    rng = np.random.default_rng(1)
+    XW = np.asfortranarray(rng.standard_normal((D, N)))
+    X, _ = oracle.flow_apply(true, XW)
+    X = np.asfortranarray(X)
+    mk = lambda layers: enf.compose(*[
+        {0: lambda ps: enf.ScaleShiftTrafo(*ps), 1: lambda ps: enf.CenterStretch(*ps),
+         2: lambda ps: enf.CenterContract(*ps), 3: lambda ps: enf.JohnsonTrafo(*ps),
+         5: lambda ps: enf.HouseholderTrafo(ps[0])}[op](ps) for op, ps in reversed(layers)])
+    Xd = torch.from_numpy(np.ascontiguousarray(X.T)).to(dev).t()
+    opt = enf.ADAGrad()
+    enf.optimize_whitening(Xd, mk(init), opt, nbatches=nbatches, nepochs=1, graph=True)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = enf.optimize_whitening(Xd, mk(init), opt, nbatches=nbatches, nepochs=nepochs, graph=True)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    # the replay rate alone: the same epoch graph replayed (capture excluded)
+    from euclidiannormalizingflows_jl_amd.train import FlowState, _workspace, householder_batches, trainable_runs
+
+    lib = enf._lib
+    L = lib.lib()
+    state = FlowState(mk(init), D, torch.float64, dev, opt)
+    plan = enf.minibatch_plan(N, nbatches, 0, 1)
+    ws = _workspace(state, max(B for B, _, _ in plan))
+    runs = np.ascontiguousarray(np.array(trainable_runs(state), dtype=np.int64).reshape(-1))
+    hbs = np.ascontiguousarray(np.array(householder_batches(state), dtype=np.int64).reshape(-1))
+    hep = torch.zeros(len(plan), dtype=torch.float64, device=dev)
+    cg = torch.cuda.CUDAGraph()
+    tc = time.perf_counter()
+    with torch.cuda.graph(cg):
+        st = torch.cuda.current_stream().cuda_stream
+        for j, (B, lo, hi) in enumerate(plan):
+            lib.check(L.enf_whitening_step(lib.ENF_F64, D, hi - lo, Xd[:, lo:hi].data_ptr(), D, state.layers(),
+                                           len(state.trafos), state.theta.data_ptr(), state.acc.data_ptr(),
+                                           runs.ctypes.data, len(runs) // 2, hbs.ctypes.data, len(hbs) // 3, opt.eta,
+                                           opt.epsilon, hep[j:].data_ptr(), ws.data_ptr(), ws.numel() * 8, st))
+    capture_s = time.perf_counter() - tc
+    cg.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    stream = torch.cuda.current_stream()
+    e0.record(stream)
+    for _ in range(nepochs):
+        cg.replay()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    replay_ms = e0.elapsed_time(e1)
+    del cg
+    steps = nepochs * len(plan)
+    # the oracle on the host, one thread: the same loop (gradient on the CPU, ADAGrad, normalize!)
+    tcpu = time.perf_counter()
+    _, _, hist_ref = oracle.optimize_whitening(init, X, nbatches=nbatches, nepochs=nepochs, eta=opt.eta,
+                                               epsilon=opt.epsilon)
+    cpu_s = time.perf_counter() - tcpu
+    hist = np.asarray(r.negll_history)
+    B = plan[0][0]
+    return {"metric": f"optimize_whitening training steps/s (reference example {example})", "unit": "steps/s",
+            "value": steps / (replay_ms * 1e-3), "us_per_step": replay_ms * 1e3 / steps,
+            "launch": "one epoch captured as a HIP graph, replayed nepochs times (capture excluded)",
+            "end_to_end": {"steps_per_s": steps / wall, "wall_s": wall,
+                           "what": "optimize_whitening(graph=True) call: capture + replays + history copy"},
+            "capture_s": capture_s, "steps": steps, "dtype": "f64",
+            "config": {"workload": f"examples/nf_example_{example}.jl: D={D}, N={N}, nbatches={nbatches} (B={B}), "
+                                   f"nepochs={nepochs}, {'JKJK' if example == '1d' else 'KHS'} initial flow, ADAGrad",
+                       "flow_letters_application_order": "KJKJ" if example == "1d" else "SHK"},
+            "cpu_baseline": {"value": steps / cpu_s, "unit": "steps/s", "cores": 1, "kind": "port",
+                             "sample": f"the whole loop ({steps} steps) in the oracle (oracle/enf_oracle_grad.c "
+                                       f"or_optimize_whitening_f64: the reference-structured reverse pass), one thread",
+                             "seconds": cpu_s},
+            "parity": {"history_max_rel_diff_vs_oracle": float(np.max(np.abs(hist - hist_ref) / np.abs(hist_ref))),
+                       "negll_first": float(hist[0]), "negll_last": float(hist[-1])},
+            "data": "synthetic: X = the example's true flow of randn (numpy seed 1), as the example script"}
 
 
 if __name__ == "__main__":

@@ -29,6 +29,7 @@ EXPORTED = (
     "enf_adagrad_step", "enf_householder_normalize", "enf_householder_normalize_strided", "enf_comm_unique_id", "enf_comm_init",
     "enf_comm_destroy", "enf_allreduce_sum", "enf_johnsonsu_eval", "enf_johnsonsu_sample",
     "enf_whitening_step", "enf_whitening_apply", "enf_flow_vjp", "enf_flow_apply_cpu", "enf_whitening_step_dp",
+    "enf_stream_copy",
 )
 
 
@@ -78,6 +79,7 @@ _SIGS = {
     "enf_adagrad_step": (ctypes.c_int, [ctypes.c_int, _i64, _vp, _vp, _vp, _dbl, _dbl, _dbl, _vp]),
     "enf_householder_normalize": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _vp, _vp]),
     "enf_householder_normalize_strided": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _vp, _i64, _vp]),
+    "enf_stream_copy": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp]),
     "enf_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "enf_comm_init": (ctypes.c_int, [ctypes.POINTER(_vp), _i32, ctypes.c_char_p, _i32]),
     "enf_comm_destroy": (ctypes.c_int, [_vp]),

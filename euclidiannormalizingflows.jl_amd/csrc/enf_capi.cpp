@@ -681,6 +681,14 @@ enf_status enf_householder_normalize_strided(enf_dtype dtype, int64_t D, int64_t
   ENF_CATCH
 }
 
+enf_status enf_stream_copy(const void* src, void* dst, int64_t bytes, int32_t variant, void* hip_stream) {
+  ENF_TRY
+  if (bytes < 0) return fail(ENF_ERR_INVALID, "bytes < 0");
+  if (bytes > 0 && (!src || !dst)) return fail(ENF_ERR_INVALID, "src or dst is NULL");
+  return enf::stream_copy(src, dst, bytes, variant, (hipStream_t)hip_stream);
+  ENF_CATCH
+}
+
 // ------------------------------------------------------------------------ JohnsonSU ----
 enf_status enf_johnsonsu_eval(enf_dtype dtype, int32_t fn, int64_t n, const void* x, void* out, double gamma,
                               double delta, double xi, double lambda, void* hip_stream) {

@@ -436,46 +436,6 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
   }
 }
 
-// Sum of the block partials in kSumSlices slices (blockIdx.y): slice s covers blocks
-// [s*bs, (s+1)*bs), summed in block order per wave (b = start + w, + 4, ...) with 8 independent
-// accumulators and then over the 4 waves, in double -> tot[s][i] for the loss (i = 0) and every
-// gradient entry. grad_finalize_kernel adds the slices in order: a fixed summation tree, so the
-// result is deterministic. 64 entries per block.
-__global__ __launch_bounds__(256) void grad_sum_kernel(ReduceArgs r) {
-  __shared__ double red[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
-  const int64_t n = 1 + (int64_t)r.nparams;
-  const int bs = (r.nblocks + kSumSlices - 1) / kSumSlices;
-  const int b0 = (int)blockIdx.y * bs;
-  const int b1 = b0 + bs < r.nblocks ? b0 + bs : r.nblocks;
-  double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (i < n) {
-    int b = b0 + w;
-    for (; b + 28 < b1; b += 32)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) s8[k] += r.partial[(int64_t)(b + 4 * k) * n + i];
-    for (; b < b1; b += 4) s8[0] += r.partial[(int64_t)b * n + i];
-  }
-  const double s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
-  red[w][lane] = s;
-  __syncthreads();
-  if (w == 0 && i < n) r.tot[(int64_t)blockIdx.y * n + i] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-}
-
-// Householder direction projection and accumulation into out (one block).
-template <typename T>
-__global__ __launch_bounds__(256) void grad_finalize_kernel(ReduceArgs r) {
-  finalize_into_out<T>(r);
-}
-
-// The rest of a single-rank optimize_whitening step in one block (enf_whitening_step), when it does not
-// run at the end of the gradient kernel (enf_grad_tail.h whitening_tail_body).
-template <typename T>
-__global__ __launch_bounds__(256) void whitening_tail_kernel(ReduceArgs r, StepArgs a) {
-  whitening_tail_body<T>(r, a);
-}
-
 // The update half of a data-parallel step (enf_whitening_apply): the same loss / ADAGrad /
 // re-normalisation as whitening_tail_kernel, reading the cross-rank sum g (1 + nparams values of T,
 // the all-reduced enf_flow_negll_grad output) instead of the totals. Same operations and roundings
@@ -503,7 +463,8 @@ struct Plan {
   GradArgs ga;
   ReduceArgs ra;
   size_t lds = 0;
-  int blocks = 0;
+  int blocks = 0;   // blocks (partial rows) of the generic kernel
+  int ws_rows = 0;  // partial rows the workspace reserves: the generic kernel's or the fused (J o H)^n kernel's
   int nw = 4;  // waves per block of the generic kernel
 };
 
@@ -581,11 +542,37 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   P.blocks = (int)blocks;
+  P.ws_rows = P.blocks;
+  if (!f64 && hj_grad_shape_ok(D, layers, nlayers)) P.ws_rows = std::max(P.ws_rows, hj_grad_blocks(D, N, nlayers / 2));
   P.ra.nblocks = P.blocks;
   P.ra.nparams = goff;
   P.ra.D = (int32_t)D;
+  P.ra.upb = reduce_units_per_block(D);
+  P.ra.nloc = N;
   return ENF_OK;
 }
+
+template <typename T, int MODE>
+hipError_t launch_reduce(const ReduceArgs& r, const StepArgs& s, hipStream_t st) {
+  hipLaunchKernelGGL((grad_reduce_kernel<T, MODE>), dim3(reduce_grid(r.D, r.nparams)), dim3(kRedThreads), 0, st, r, s);
+  return hipGetLastError();
+}
+template <int MODE>
+hipError_t launch_reduce(bool f64, const ReduceArgs& r, const StepArgs& s, hipStream_t st) {
+  return f64 ? launch_reduce<double, MODE>(r, s, st) : launch_reduce<float, MODE>(r, s, st);
+}
+
+// workspace: [partial rows: ws_rows x (1 + nparams)][tot: 1 + nparams][the constant ladj: 1][...] (doubles)
+size_t plan_workspace_bytes(const Plan& P) {
+  return ((size_t)P.ws_rows + kSumSlices) * (1 + (size_t)P.ga.nparams) * sizeof(double);
+}
+void plan_bind_workspace(Plan& P, void* workspace) {
+  const size_t n = 1 + (size_t)P.ga.nparams;
+  P.ga.partial = workspace;
+  P.ra.partial = (const double*)workspace;
+  P.ra.tot = (double*)workspace + (size_t)P.ws_rows * n;
+}
+double* plan_ctot_slot(const Plan& P) { return P.ra.tot + 1 + P.ga.nparams; }
 
 template <typename T, int DD, bool VJP>
 hipError_t launch_grad_D(const Plan& P, hipStream_t st) {
@@ -618,34 +605,34 @@ enf_status single_workspace(bool f64, int64_t D, int64_t N, const enf_layer* lay
   Plan P;
   enf_status s = make_plan(f64, D, N > 0 ? N : 1, layers, nlayers, P);
   if (s != ENF_OK) return s;
-  *bytes = ((size_t)P.blocks + kSumSlices) * (1 + (size_t)P.ga.nparams) * sizeof(double);
+  *bytes = plan_workspace_bytes(P);
   return ENF_OK;
 }
 
-// The per-block partials (fused (J o H)^n kernel or the generic one) and their slice sums: tot of P.ra.
+// The per-block partial rows (fused (J o H)^n kernel or the generic one) in the workspace; P.ra then describes
+// them for grad_reduce_kernel (rows, the constant ladj the fused kernel computes once).
 enf_status grad_parts(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
                       int32_t nlayers, void* workspace, size_t workspace_bytes, hipStream_t st, Plan& P) {
   enf_status s = make_plan(f64, D, N, layers, nlayers, P);
   if (s != ENF_OK) return s;
-  const size_t need = ((size_t)P.blocks + kSumSlices) * (1 + (size_t)P.ga.nparams) * sizeof(double);
-  if (!workspace || workspace_bytes < need) return set_error(ENF_ERR_INVALID, "enf_flow_negll_grad: workspace too small");
+  if (!workspace || workspace_bytes < plan_workspace_bytes(P))
+    return set_error(ENF_ERR_INVALID, "enf_flow_negll_grad: workspace too small");
   P.ga.X = X;
   P.ga.ldx = ldx;
-  P.ga.partial = workspace;
-  P.ra.partial = (const double*)workspace;
-  P.ra.tot = (double*)workspace + (size_t)P.blocks * (1 + (size_t)P.ga.nparams);
+  plan_bind_workspace(P, workspace);
   hipError_t e;
   static const int generic = ENF_KNOB("ENF_GRAD_GENERIC", 0);
   if (!f64 && !generic && hj_grad_eligible(D, ldx, X, layers, nlayers)) {
-    e = launch_hj_grad(D, N, X, layers, nlayers, P.ga.nparams, (double*)workspace, P.blocks, st);
+    // (make_plan reserved hj_grad_blocks(D, N, n) rows for this shape: the launch writes that many)
+    int rows = 0;
+    e = launch_hj_grad(D, N, X, layers, nlayers, P.ga.nparams, (double*)workspace, plan_ctot_slot(P), &rows, st);
+    P.ra.nblocks = rows;
+    P.ra.ctot = plan_ctot_slot(P);
   } else {
     if (P.lds > kGradLdsMax) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: flow too large for LDS");
     e = f64 ? launch_grad<double>(P, st) : launch_grad<float>(P, st);
-  }
-  if (e == hipSuccess) {
-    hipLaunchKernelGGL(grad_sum_kernel, dim3((unsigned)((1 + P.ra.nparams + 63) / 64), kSumSlices), dim3(256), 0, st,
-                       P.ra);
-    e = hipGetLastError();
+    P.ra.nblocks = P.blocks;
+    P.ra.ctot = nullptr;
   }
   if (e != hipSuccess) return set_error(ENF_ERR_HIP, hipGetErrorString(e));
   return ENF_OK;
@@ -659,9 +646,9 @@ enf_status negll_grad_single(bool f64, int64_t D, int64_t N, const void* X, int6
   enf_status s = grad_parts(f64, D, N, X, ldx, layers, nlayers, workspace, workspace_bytes, st, P);
   if (s != ENF_OK) return s;
   P.ra.out = out;
-  if (f64) hipLaunchKernelGGL((grad_finalize_kernel<double>), dim3(1), dim3(256), 0, st, P.ra);
-  else hipLaunchKernelGGL((grad_finalize_kernel<float>), dim3(1), dim3(256), 0, st, P.ra);
-  hipError_t e = hipGetLastError();
+  StepArgs none;
+  std::memset(&none, 0, sizeof none);
+  hipError_t e = launch_reduce<MODE_OUT>(f64, P.ra, none, st);
   return e == hipSuccess ? ENF_OK : set_error(ENF_ERR_HIP, hipGetErrorString(e));
 }
 
@@ -680,21 +667,19 @@ enf_status flow_vjp_single(bool f64, int64_t D, int64_t N, const void* X, int64_
   P.ga.dX = dX;
   P.ga.lddx = lddx;
   if (dparams) {
-    const size_t need = ((size_t)P.blocks + kSumSlices) * (1 + (size_t)P.ga.nparams) * sizeof(double);
-    if (!workspace || workspace_bytes < need) return set_error(ENF_ERR_INVALID, "enf_flow_vjp: workspace too small");
-    P.ga.partial = workspace;
-    P.ra.partial = (const double*)workspace;
-    P.ra.tot = (double*)workspace + (size_t)P.blocks * (1 + (size_t)P.ga.nparams);
+    if (!workspace || workspace_bytes < plan_workspace_bytes(P))
+      return set_error(ENF_ERR_INVALID, "enf_flow_vjp: workspace too small");
+    plan_bind_workspace(P, workspace);
   }
   hipError_t e = f64 ? launch_grad<double, true>(P, st) : launch_grad<float, true>(P, st);
   if (e == hipSuccess && dparams) {
-    hipLaunchKernelGGL(grad_sum_kernel, dim3((unsigned)((1 + P.ra.nparams + 63) / 64), kSumSlices), dim3(256), 0, st,
-                       P.ra);
+    P.ra.nblocks = P.blocks;
+    P.ra.ctot = nullptr;
     P.ra.out = dparams;
     P.ra.skip_loss = 1;
-    if (f64) hipLaunchKernelGGL((grad_finalize_kernel<double>), dim3(1), dim3(256), 0, st, P.ra);
-    else hipLaunchKernelGGL((grad_finalize_kernel<float>), dim3(1), dim3(256), 0, st, P.ra);
-    e = hipGetLastError();
+    StepArgs none;
+    std::memset(&none, 0, sizeof none);
+    e = launch_reduce<MODE_OUT>(f64, P.ra, none, st);
   }
   if (e != hipSuccess) return set_error(ENF_ERR_HIP, hipGetErrorString(e));
   return ENF_OK;
@@ -736,8 +721,8 @@ enf_status whitening_apply(bool f64, int64_t D, int64_t nparams, const void* g, 
 }
 
 namespace {
-// B: the global batch size the update normalises by (N on one rank); ar: the cross-rank sum of the 8 slice
-// totals (double) between the gradient and the tail (enf_whitening_step_dp), or none
+// B: the global batch size the update normalises by (N on one rank); ar: the cross-rank sum of this rank's
+// totals (1 + nparams doubles, MODE_SUM) between the gradient and the update (enf_whitening_step_dp), or none
 enf_status whitening_step_single(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
                                  int32_t nlayers, void* theta, void* acc, const int64_t* runs, int32_t nruns,
                                  const int64_t* hb, int32_t nhb, double eta, double epsilon, double* loss_out,
@@ -769,29 +754,39 @@ enf_status whitening_step_single(bool f64, int64_t D, int64_t N, const void* X, 
   for (int i = 0; i < nruns; ++i)
     if (a.runs[i][0] < 0 || a.runs[i][1] < a.runs[i][0] || a.runs[i][1] > P.ga.nparams)
       return set_error(ENF_ERR_INVALID, "enf_whitening_step: parameter run outside theta");
-  for (int i = 0; i < nhb; ++i)
+  for (int i = 0; i < nhb; ++i) {
     if (a.hb[i][0] < 0 || a.hb[i][1] < 0 || a.hb[i][2] < D ||
         (a.hb[i][1] > 0 && a.hb[i][0] + (a.hb[i][1] - 1) * a.hb[i][2] + D > P.ga.nparams))
       return set_error(ENF_ERR_INVALID, "enf_whitening_step: Householder batch outside theta");
-  const size_t ntot = (size_t)kSumSlices * (1 + (size_t)P.ga.nparams);
+    // (each column is one D-entry vector of the parameter layout: the reduction re-normalises it where it updates it)
+    if (a.hb[i][0] % D != 0 || a.hb[i][2] % D != 0)
+      return set_error(ENF_ERR_INVALID, "enf_whitening_step: Householder batch columns must start at multiples of D");
+  }
+  const size_t n1 = 1 + (size_t)P.ga.nparams;
   if (N > 0) {
     s = grad_parts(f64, D, N, X, ldx, layers, nlayers, workspace, workspace_bytes, st, P);
     if (s != ENF_OK) return s;
-  } else {  // an empty share (a rank without columns in this minibatch): zero slice totals
-    const size_t need = ((size_t)P.blocks + kSumSlices) * (1 + (size_t)P.ga.nparams) * sizeof(double);
-    if (!workspace || workspace_bytes < need) return set_error(ENF_ERR_INVALID, "enf_whitening_step: workspace too small");
-    P.ra.partial = (const double*)workspace;
-    P.ra.tot = (double*)workspace + (size_t)P.blocks * (1 + (size_t)P.ga.nparams);
-    if (hipMemsetAsync(P.ra.tot, 0, ntot * sizeof(double), st) != hipSuccess)
-      return set_error(ENF_ERR_HIP, "hipMemsetAsync");
+  } else {  // an empty share (a rank without columns in this minibatch): zero totals
+    if (!workspace || workspace_bytes < plan_workspace_bytes(P))
+      return set_error(ENF_ERR_INVALID, "enf_whitening_step: workspace too small");
+    plan_bind_workspace(P, workspace);
+    if (hipMemsetAsync(P.ra.tot, 0, n1 * sizeof(double), st) != hipSuccess) return set_error(ENF_ERR_HIP, "hipMemsetAsync");
   }
-  if (ar) {  // the cross-rank sum of the slice totals, in double, before the tail sums the slices
-    s = ar(ar_ctx, P.ra.tot, (int64_t)ntot, true, st);
-    if (s != ENF_OK) return s;
+  hipError_t e = hipSuccess;
+  if (ar || N <= 0) {
+    if (N > 0) {  // this rank's totals (MODE_SUM), the all-reduce, then the update reading the one summed row
+      e = launch_reduce<MODE_SUM>(f64, P.ra, a, st);
+      if (e != hipSuccess) return set_error(ENF_ERR_HIP, hipGetErrorString(e));
+    }
+    if (ar) {
+      s = ar(ar_ctx, P.ra.tot, (int64_t)n1, true, st);
+      if (s != ENF_OK) return s;
+    }
+    P.ra.partial = P.ra.tot;
+    P.ra.nblocks = 1;
+    P.ra.ctot = nullptr;
   }
-  if (f64) hipLaunchKernelGGL((whitening_tail_kernel<double>), dim3(1), dim3(256), 0, st, P.ra, a);
-  else hipLaunchKernelGGL((whitening_tail_kernel<float>), dim3(1), dim3(256), 0, st, P.ra, a);
-  hipError_t e = hipGetLastError();
+  e = launch_reduce<MODE_STEP>(f64, P.ra, a, st);
   return e == hipSuccess ? ENF_OK : set_error(ENF_ERR_HIP, hipGetErrorString(e));
 }
 

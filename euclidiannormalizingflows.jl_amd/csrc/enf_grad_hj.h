@@ -16,7 +16,8 @@ struct HJGradArgs {
   int64_t N;
   int32_t n;  // pairs
   int32_t D;
-  double* partial;  // [gridDim.x][1 + nparams]
+  double* partial;  // [nblocks][1 + nparams]: block 1 + b writes row b (block 0 computes the constant below)
+  double* ctot_out;  // the flow's constant ladj sum_p sum_d log|delta/lambda| (double), written by block 0
   int32_t nparams;
   int32_t pad_;
   const float* v[kHJGradMaxPairs];
@@ -30,7 +31,13 @@ struct HJGradArgs {
 
 // fp32, D in {32, 64}, contiguous 16-byte aligned columns, layers H, J, H, J, ... (k = 1), <= 8 pairs
 bool hj_grad_eligible(int64_t D, int64_t ldx, const void* X, const enf_layer* layers, int32_t nlayers);
+// the flow's shape alone (no pointer / stride test): what the workspace query can know
+bool hj_grad_shape_ok(int64_t D, const enf_layer* layers, int32_t nlayers);
+// partial rows the fused kernel writes for N columns (the workspace holds at least this many)
+int hj_grad_blocks(int64_t D, int64_t N, int32_t npairs);
+// Launches the fused kernel (grid: 1 + *nblocks blocks); the loss partials EXCLUDE the constant ladj, which
+// block 0 writes to *ctot_out (the reduction subtracts N * ctot from the loss once).
 hipError_t launch_hj_grad(int64_t D, int64_t N, const void* X, const enf_layer* layers, int32_t nlayers,
-                          int32_t nparams, double* partial, int blocks, hipStream_t st);
+                          int32_t nparams, double* partial, double* ctot_out, int* nblocks, hipStream_t st);
 
 }  // namespace enf

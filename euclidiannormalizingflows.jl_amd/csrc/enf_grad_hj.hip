@@ -2,22 +2,29 @@
 // J_n o H_n o ... o J_1 o H_1 (fp32, D in {32, 64}, n <= 8, one reflection per H, contiguous
 // 16-byte aligned columns): mvnormal_negll_trafo / mvnormal_negll_trafograd
 // (src/optimize_whitening.jl:7-22) for the N local samples, as per-block partial sums in the
-// layout of enf_grad.hip (reduced and Householder-projected there).
+// layout of enf_grad.hip (reduced and Householder-projected by enf_grad_tail.h's reduction).
 //
 // Forward (per pair, per element; hardware transcendentals as the forward kernel):
 //   dot = vh'u, h = u - dot vh, z = (h - xi)/lambda, y = gamma + delta asinh z,
 //   ladj += log|delta/lambda| - log(1 + z^2)/2    (householder_trafo.jl:8-11, johnson_trafo.jl:29-52)
-// storing z and dot per pair in LDS (the backward needs nothing else: h = lambda z + xi and
-// u = h + dot vh recover the layer inputs exactly as in the reference's pullback, which recomputes
-// them by re-reflection, householder_trafo.jl:91-101).
 // Backward with g = dS/dy (g = y at the output), s = sqrt(1 + z^2):
 //   dS/dgamma += g, dS/ddelta += g asinh z - 1/delta, dz = g delta/s + z/s^2,
 //   dS/dxi -= dz/lambda, dS/dlambda += -dz z/lambda + 1/lambda, g_h = dz/lambda,
-//   Householder: dS/dvh-direction += g_h (vh'u) + u (vh'g_h) (projected in grad_finalize_kernel),
+//   Householder: dS/dvh-direction += g_h (vh'u) + u (vh'g_h) (projected in the reduction),
 //   g_u = g_h - vh (vh'g_h).
-// Per-lane gradient partials of a tile are summed over the lanes holding the same rows (cross-
-// lane shuffles) and added by one lane per row into the wave's LDS accumulators; the block sums
-// its 4 waves in a fixed order (deterministic).
+// The layer inputs are recovered as h = lambda z + xi, u = h + dot vh, as the reference's pullback
+// recomputes them by re-reflection (householder_trafo.jl:91-101).
+//
+// Round 5 (the per-step fixed cost at small minibatch shares):
+// * the register kernel takes V rows per lane (V = 4: one 16-byte fragment, as before; V = 2 / 1: a column
+//   over 16 / 32 lanes): at a share of 12 500 columns a wave had about one 8-column tile and ran it alone on
+//   its SIMD at a quarter of the issue rate; with V = 2 the same columns make twice the waves at half the
+//   registers (more waves per SIMD) and the cross-lane sums of a D = 32 column stay within DPP rows;
+// * a block holds W waves (the records and the partial row are per block);
+// * the per-block prologue no longer evaluates the double log|delta| - log|lambda| of every row: the flow's
+//   constant ladj does not depend on the samples and enters the loss only (its gradients are the -1/delta,
+//   +1/lambda terms, added from the block's column count), so block 0 of the grid computes it once and the
+//   reduction subtracts N times it from the loss.
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -27,20 +34,57 @@
 
 #include "enf_frag.h"
 #include "enf_grad_hj.h"
+#include "enf_train.h"
 
 namespace enf {
 
 namespace {
 
 constexpr int kNP = 8;  // records per pair: vh, gamma, delta*ln2, 1/lambda, -xi/lambda, lambda, xi, delta
+constexpr int kScrBytes = 512;  // block scratch: [0, 8) per-pair scale, [16, 16 + 2W) per-wave loss / count
 
-template <int D, int KU>
+typedef unsigned int u32x2h __attribute__((ext_vector_type(2)));
+
+// V rows per lane: G = D / V lanes per column, S = 64 / G columns per wave instruction, TC per tile
+template <int D, int V, int KU>
 struct GL {
-  static constexpr int V = 4;
-  static constexpr int G = D / V;            // lanes per column
-  static constexpr int S = 64 / G;           // column slots per wave instruction
-  static constexpr int TC = S * KU;          // columns per wave tile
+  static constexpr int G = D / V;
+  static constexpr int S = 64 / G;
+  static constexpr int TC = S * KU;
+  static_assert(D % V == 0 && G <= 64 && 64 % G == 0, "a column within one wave");
 };
+
+template <int V>
+__device__ __forceinline__ void gload_rows(const float* __restrict__ src, float (&x)[V]) {
+  if constexpr (V == 4) {
+    const u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
+    __builtin_memcpy(&x[0], &w, 16);
+  } else if constexpr (V == 2) {
+    const u32x2h w = __builtin_nontemporal_load(reinterpret_cast<const u32x2h*>(src));
+    __builtin_memcpy(&x[0], &w, 8);
+  } else {
+    x[0] = __builtin_nontemporal_load(src);
+  }
+}
+
+template <int V>
+__device__ __forceinline__ void lds_rows(const float* __restrict__ p, float (&v)[V]) {
+  if constexpr (V == 4) {
+    lds_vec<float, 4>(p, v);
+  } else if constexpr (V == 2) {
+    const u32x2h w = *reinterpret_cast<const u32x2h*>(p);
+    __builtin_memcpy(&v[0], &w, 8);
+  } else {
+    v[0] = *p;
+  }
+}
+
+template <int V>
+__device__ __forceinline__ float prod_rows(const float (&q)[V]) {
+  if constexpr (V == 4) return (q[0] * q[1]) * (q[2] * q[3]);
+  else if constexpr (V == 2) return q[0] * q[1];
+  else return q[0];
+}
 
 // cross-slot sum: lanes with equal lane % G hold the same rows
 template <int G>
@@ -50,12 +94,20 @@ __device__ __forceinline__ float slot_sum(float v) {
   return v;
 }
 
+// the records of the lane's rows r0 = V grp .. r0 + V - 1 (layout [pair][4-row group][param][4]); parameter q at +4q
+template <int D, int V>
+__device__ __forceinline__ const float* rec_lane(const float* __restrict__ rec, int p, int grp) {
+  const int r0 = V * grp;
+  return rec + (size_t)p * kNP * D + (r0 / 4) * kNP * 4 + (r0 % 4);
+}
+
+// LDS variant (n > 4 pairs): z and the reflection dot of every pair stored in LDS between the passes
 template <int D, int KU, bool TAIL>
 __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int lane, const float* __restrict__ rec,
                                           float* __restrict__ zst, float* __restrict__ dst, float* __restrict__ acc,
-                                          double& lossp, int& nvalid, float ctot) {
+                                          double& lossp, int& nvalid) {
   const uint32_t csign = sign_mask_vgpr();  // asinh2_f32: the accurate fp32 asinh (enf_frag.h)
-  using L = GL<D, KU>;
+  using L = GL<D, 4, KU>;
   constexpr int V = 4, G = L::G, S = L::S;
   const int grp = lane % G;
   const int n = a.n;
@@ -67,8 +119,7 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
     const float* src = a.X + c * D + V * grp;
     vm[u] = (!TAIL || c < a.N) ? 1.f : 0.f;
     if (!TAIL) {
-      const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
-      __builtin_memcpy(&x[u][0], &v4, 16);
+      gload_rows<V>(src, x[u]);
     } else {
 #pragma unroll
       for (int e = 0; e < V; ++e) x[u][e] = c < a.N ? src[e] : 0.f;
@@ -77,13 +128,13 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
   // ---- forward
   float lad[KU] = {};
   for (int p = 0; p < n; ++p) {
-    const float* r = rec + (size_t)p * kNP * D + grp * kNP * V;
+    const float* r = rec_lane<D, V>(rec, p, grp);
     float vh[V], gam[V], dl2[V], il[V], nxil[V];
-    lds_vec<float, V>(r, vh);
-    lds_vec<float, V>(r + V, gam);
-    lds_vec<float, V>(r + 2 * V, dl2);
-    lds_vec<float, V>(r + 3 * V, il);
-    lds_vec<float, V>(r + 4 * V, nxil);
+    lds_rows<V>(r, vh);
+    lds_rows<V>(r + 4, gam);
+    lds_rows<V>(r + 8, dl2);
+    lds_rows<V>(r + 12, il);
+    lds_rows<V>(r + 16, nxil);
     float dot[KU];
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
@@ -110,10 +161,10 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
         const float Lz = asinh2_f32(z[u][e], q[u][e], hw_sqrt(q[u][e]), csign);
         x[u][e] = fmaf(dl2[e], Lz, gam[e]);
       }
-      lad[u] = fmaf(-0.5f, hw_log2((q[u][0] * q[u][1]) * (q[u][2] * q[u][3])), lad[u]);
+      lad[u] = fmaf(-0.5f, hw_log2(prod_rows<V>(q[u])), lad[u]);
     }
   }
-  // ---- loss: sum_d (y^2 + log 2 pi)/2 - ladj, ladj = ctot + ln2 * lad (valid columns)
+  // ---- loss without the constant ladj: sum_d (y^2 + log 2 pi)/2 - ln2 * lad (valid columns)
 #pragma unroll
   for (int u = 0; u < KU; ++u) {
     float t = 0.f;
@@ -122,7 +173,7 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
     const float ysq = group_sum<G>(t);
     const float ltot = group_sum<G>(lad[u]);
     if (grp == 0 && vm[u] != 0.f) {
-      lossp += 0.5 * (double)ysq + 0.5 * D * 1.8378770664093454836 - ((double)ctot + kLn2 * (double)ltot);
+      lossp += 0.5 * (double)ysq + 0.5 * D * 1.8378770664093454836 - kLn2 * (double)ltot;
       ++nvalid;
     }
   }
@@ -133,13 +184,13 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
 #pragma unroll
     for (int e = 0; e < V; ++e) g[u][e] = x[u][e] * vm[u];
   for (int p = n - 1; p >= 0; --p) {
-    const float* r = rec + (size_t)p * kNP * D + grp * kNP * V;
+    const float* r = rec_lane<D, V>(rec, p, grp);
     float vh[V], il[V], lam[V], xi[V], del[V];
-    lds_vec<float, V>(r, vh);
-    lds_vec<float, V>(r + 3 * V, il);
-    lds_vec<float, V>(r + 5 * V, lam);
-    lds_vec<float, V>(r + 6 * V, xi);
-    lds_vec<float, V>(r + 7 * V, del);
+    lds_rows<V>(r, vh);
+    lds_rows<V>(r + 12, il);
+    lds_rows<V>(r + 20, lam);
+    lds_rows<V>(r + 24, xi);
+    lds_rows<V>(r + 28, del);
     float aG[V] = {}, aD[V] = {}, aX[V] = {}, aL[V] = {}, aV[V] = {};
     float gh[KU][V], u_[KU][V], dot1[KU];
 #pragma unroll
@@ -191,77 +242,88 @@ __device__ __forceinline__ void grad_tile(const HJGradArgs& a, int64_t col0, int
   }
 }
 
-// Block prologue shared by both kernels: per pair v'v and the constant ladj part sum log|delta/lambda|
-// (double, scr), then the records [pair][group][param][4] in rec. Returns ctot = sum of the constants.
 // LDS-only block barrier: global loads issued before it (a wave's first tile) stay in flight
 __device__ __forceinline__ void gh_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Block prologue: the per-row records of every pair in ONE round of global loads (round 4; round 3 read the
-// parameters twice, once per pass): thread i of the first n*D handles row d = i % D of pair p = i / D, loads its
-// five parameters, and the per-pair sums v'v and sum_d log|delta/lambda| (johnson_trafo.jl:41) are reduced over
-// the D adjacent lanes that hold pair p (D <= 64: within one wave); after one LDS barrier each thread writes its
-// row's records with the pair's reflection scale sqrt(2/v'v) (householder_trafo.jl:9-10). Double arithmetic as
-// before, so the same records and constant.
-template <int D>
-__device__ __forceinline__ float grad_prologue(const HJGradArgs& a, double* __restrict__ scr, float* __restrict__ rec) {
-  static_assert(D <= 64 && 256 % D == 0, "a pair's rows within one wave");
+// Block prologue: the per-row records of every pair in one round of global loads. Thread i of the first n*D
+// handles row d = i % D of pair p = i / D; the pair's v'v is reduced over the D adjacent lanes that hold it
+// (D <= 64: within one wave); after one LDS barrier each thread writes its row's records with the pair's
+// reflection scale sqrt(2/v'v) (householder_trafo.jl:9-10). Double arithmetic for the derived values.
+template <int D, int NT>
+__device__ __forceinline__ void grad_prologue(const HJGradArgs& a, double* __restrict__ scr, float* __restrict__ rec) {
+  static_assert(D <= 64 && 64 % D == 0, "a pair's rows within one wave");
   const int n = a.n;
   const int tid = threadIdx.x;
-  constexpr int kIt = (kHJGradMaxPairs * D + 255) / 256;  // rows per thread (n * D <= 8 * 64)
-  double pv[kIt], pg[kIt], pd[kIt], px[kIt], pl[kIt];
+  constexpr int kIt = (kHJGradMaxPairs * D + NT - 1) / NT;
+  float pv[kIt], pg[kIt], pd[kIt], px[kIt], pl[kIt];
 #pragma unroll
   for (int it = 0; it < kIt; ++it) {
-    const int i = tid + 256 * it;
+    const int i = tid + NT * it;
     const int p = i / D, d = i % D;
-    double vv = 0.0, cl = 0.0;
-    pv[it] = pg[it] = px[it] = 0.0;
-    pd[it] = pl[it] = 1.0;
+    double vv = 0.0;
+    pv[it] = pg[it] = px[it] = 0.f;
+    pd[it] = pl[it] = 1.f;
     if (p < n) {
       pv[it] = a.v[p][d];
       pg[it] = a.g[p][d];
       pd[it] = a.d[p][d];
       px[it] = a.xi[p][d];
       pl[it] = a.lam[p][d];
-      vv = pv[it] * pv[it];
-      cl = log(fabs(pd[it])) - log(fabs(pl[it]));
+      vv = (double)pv[it] * (double)pv[it];
     }
 #pragma unroll
-    for (int m = D / 2; m >= 1; m >>= 1) {  // the D lanes of pair p (all lanes of the wave take part)
-      vv += __shfl_xor(vv, m);
-      cl += __shfl_xor(cl, m);
-    }
-    if (p < n && d == 0) {
-      scr[2 * p] = sqrt(2.0 / vv);
-      scr[2 * p + 1] = cl;
-    }
+    for (int m = D / 2; m >= 1; m >>= 1) vv += __shfl_xor(vv, m);  // the D lanes of pair p (whole wave active)
+    if (p < n && d == 0) scr[p] = sqrt(2.0 / vv);
   }
   gh_lds_barrier();
 #pragma unroll
   for (int it = 0; it < kIt; ++it) {
-    const int i = tid + 256 * it;
+    const int i = tid + NT * it;
     const int p = i / D, d = i % D;
     if (p >= n) continue;
     float* r = rec + (size_t)p * kNP * D + (d / 4) * kNP * 4 + (d % 4);
     const double lam = pl[it], xi = px[it], del = pd[it];
-    r[0] = (float)(pv[it] * scr[2 * p]);
-    r[4] = (float)pg[it];
+    r[0] = (float)((double)pv[it] * scr[p]);
+    r[4] = pg[it];
     r[8] = (float)(del * kLn2);
     r[12] = (float)(1.0 / lam);
     r[16] = (float)(-xi / lam);
-    r[20] = (float)lam;
-    r[24] = (float)xi;
-    r[28] = (float)del;
+    r[20] = pl[it];
+    r[24] = px[it];
+    r[28] = pd[it];
   }
   gh_lds_barrier();
-  double c = 0.0;
-  for (int p = 0; p < n; ++p) c += scr[2 * p + 1];
-  return (float)c;
 }
 
-// Block epilogue shared by both kernels: loss and the flow gradient (layer order, the
-// enf_flow_param_count layout) of the block from the 4 waves' accumulators acc0 + w * wstride
-// ([pair][param 5][D] floats each), summed in a fixed order (deterministic).
-template <int D>
+// Block 0 of the grid: the flow's constant ladj sum_p sum_d (log|delta_d| - log|lambda_d|) (johnson_trafo.jl:41)
+// in double -- per pair over its D lanes, then the pairs in order -- to *ctot_out.
+template <int D, int NT>
+__device__ __forceinline__ void ctot_block(const HJGradArgs& a, double* __restrict__ scr) {
+  const int n = a.n;
+  const int tid = threadIdx.x;
+  constexpr int kIt = (kHJGradMaxPairs * D + NT - 1) / NT;
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int i = tid + NT * it;
+    const int p = i / D, d = i % D;
+    double cl = 0.0;
+    if (p < n) cl = log(fabs((double)a.d[p][d])) - log(fabs((double)a.lam[p][d]));
+#pragma unroll
+    for (int m = D / 2; m >= 1; m >>= 1) cl += __shfl_xor(cl, m);
+    if (p < n && d == 0) scr[p] = cl;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double c = 0.0;
+    for (int p = 0; p < n; ++p) c += scr[p];
+    *a.ctot_out = c;
+  }
+}
+
+// Block epilogue: loss (without the constant ladj) and the flow gradient (layer order, the enf_flow_param_count
+// layout) of the block from its W waves' accumulators acc0 + w * wstride ([pair][param 5][D] floats each),
+// summed in wave order (deterministic), to partial row blockIdx.x - 1.
+template <int D, int W>
 __device__ __forceinline__ void grad_epilogue(const HJGradArgs& a, double* __restrict__ scr, const float* __restrict__ rec,
                                               const float* __restrict__ acc0, size_t wstride, double lossp, int nvalid) {
   const int n = a.n;
@@ -270,20 +332,26 @@ __device__ __forceinline__ void grad_epilogue(const HJGradArgs& a, double* __res
     lossp += __shfl_xor(lossp, m);
     nvalid += __shfl_xor(nvalid, m);
   }
-  double* wl = scr + 2 * kHJGradMaxPairs;
+  double* wl = scr + 16;
   if (lane == 0) {
     wl[2 * wave] = lossp;
     wl[2 * wave + 1] = (double)nvalid;
   }
   __syncthreads();
-  double* out = a.partial + (int64_t)blockIdx.x * (1 + a.nparams);
-  const double nb = wl[1] + wl[3] + wl[5] + wl[7];
-  if (tid == 0) out[0] = ((wl[0] + wl[2]) + wl[4]) + wl[6];
-  for (int i = tid; i < n * 5 * D; i += blockDim.x) {
+  double* out = a.partial + (int64_t)(blockIdx.x - 1) * (1 + a.nparams);
+  double nb = wl[1], lb = wl[0];
+#pragma unroll
+  for (int w = 1; w < W; ++w) {
+    nb += wl[2 * w + 1];
+    lb += wl[2 * w];
+  }
+  if (tid == 0) out[0] = lb;
+  for (int i = tid; i < n * 5 * D; i += 64 * W) {
     const int p = i / (5 * D), k = (i / D) % 5, d = i % D;
-    const double s = (((double)acc0[i] + (double)acc0[wstride + i]) + (double)acc0[2 * wstride + i]) +
-                     (double)acc0[3 * wstride + i];
-    // delta and lambda from the records (the fp32 parameters, exactly), not a second round of global loads
+    double s = (double)acc0[i];
+#pragma unroll
+    for (int w = 1; w < W; ++w) s += (double)acc0[w * wstride + i];
+    // delta and lambda from the records (the fp32 parameters, exactly)
     const float* r = rec + (size_t)p * kNP * D + (d / 4) * kNP * 4 + (d % 4);
     const double del = r[28], lam = r[20];
     double gval;
@@ -303,64 +371,68 @@ __device__ __forceinline__ void grad_epilogue(const HJGradArgs& a, double* __res
 // blocks per CU) but doubles the per-tile flush of the gradient partials; 2 measured faster.
 template <int D, int KU>
 __global__ __launch_bounds__(256) void hj_grad_kernel(HJGradArgs a) {
-  using L = GL<D, KU>;
+  using L = GL<D, 4, KU>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = a.n;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // LDS: [scratch: per pair {hs, cl}, per wave {loss, nvalid}][records][per wave: acc, z, dot]
-  double* scr = reinterpret_cast<double*>(smem);                       // 2*8 + 8 doubles
-  float* rec = reinterpret_cast<float*>(smem + 256);                  // n * kNP * D floats
+  // LDS: [scratch][records][per wave: acc, z, dot]
+  double* scr = reinterpret_cast<double*>(smem);
+  if (blockIdx.x == 0) {
+    ctot_block<D, 256>(a, scr);
+    return;
+  }
+  float* rec = reinterpret_cast<float*>(smem + kScrBytes);
   const size_t recb = (size_t)n * kNP * D * 4;
   const size_t accb = (size_t)n * 5 * D * 4;
   const size_t zb = (size_t)n * KU * 64 * 16;
   const size_t db = (size_t)n * KU * 64 * 4;
-  unsigned char* wbase = smem + 256 + recb + (size_t)wave * (accb + zb + db);
+  unsigned char* wbase = smem + kScrBytes + recb + (size_t)wave * (accb + zb + db);
   float* acc = reinterpret_cast<float*>(wbase);
   float* zst = reinterpret_cast<float*>(wbase + accb);
   float* dst = reinterpret_cast<float*>(wbase + accb + zb);
   for (int i = lane; i < n * 5 * D; i += 64) acc[i] = 0.f;
-  const float ctot = grad_prologue<D>(a, scr, rec);
+  grad_prologue<D, 256>(a, scr, rec);
   double lossp = 0.0;
   int nvalid = 0;
   const int64_t ntiles = (a.N + L::TC - 1) / L::TC;
   const int64_t full = a.N / L::TC;
-  const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wave);
-  for (int64_t t = wave_id; t < ntiles; t += (int64_t)gridDim.x * 4) {
-    if (t < full) grad_tile<D, KU, false>(a, t * L::TC, lane, rec, zst, dst, acc, lossp, nvalid, ctot);
-    else grad_tile<D, KU, true>(a, t * L::TC, lane, rec, zst, dst, acc, lossp, nvalid, ctot);
+  const int64_t wave_id = (int64_t)(blockIdx.x - 1) * 4 + __builtin_amdgcn_readfirstlane(wave);
+  for (int64_t t = wave_id; t < ntiles; t += (int64_t)(gridDim.x - 1) * 4) {
+    if (t < full) grad_tile<D, KU, false>(a, t * L::TC, lane, rec, zst, dst, acc, lossp, nvalid);
+    else grad_tile<D, KU, true>(a, t * L::TC, lane, rec, zst, dst, acc, lossp, nvalid);
   }
-  grad_epilogue<D>(a, scr, rec, reinterpret_cast<const float*>(smem + 256 + recb), (accb + zb + db) / 4, lossp, nvalid);
+  grad_epilogue<D, 4>(a, scr, rec, reinterpret_cast<const float*>(smem + kScrBytes + recb), (accb + zb + db) / 4, lossp,
+                      nvalid);
 }
 
 // ---- register variant (NP <= 4 pairs, compile time): z and the reflection dots of a tile stay in
 // registers between its forward and backward, and the per-lane gradient partials accumulate in
 // registers over all of the wave's tiles (acc[pair][param][row]); one cross-slot reduction per
 // wave at the end instead of one per tile and pair. Same arithmetic per element as grad_tile.
-// the lane's fragments of a tile (zeros past N)
-template <int D, int KU>
-__device__ __forceinline__ void grad_load_reg(const HJGradArgs& a, int64_t col0, int lane, float (&x)[KU][4]) {
-  using L = GL<D, KU>;
+// the lane's rows of a tile (zeros past N)
+template <int D, int V, int KU>
+__device__ __forceinline__ void grad_load_reg(const HJGradArgs& a, int64_t col0, int lane, float (&x)[KU][V]) {
+  using L = GL<D, V, KU>;
   constexpr int G = L::G, S = L::S;
 #pragma unroll
   for (int u = 0; u < KU; ++u) {
     const int64_t c = col0 + (int64_t)u * S + lane / G;
     if (c < a.N) {
-      const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.X + c * D + 4 * (lane % G)));
-      __builtin_memcpy(&x[u][0], &v4, 16);
+      gload_rows<V>(a.X + c * D + V * (lane % G), x[u]);
     } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) x[u][e] = 0.f;
+      for (int e = 0; e < V; ++e) x[u][e] = 0.f;
     }
   }
 }
 
-template <int D, int KU, int NP, bool TAIL>
+template <int D, int V, int KU, int NP, bool TAIL>
 __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0, int lane, const float* __restrict__ rec,
-                                              const float (&xin)[KU][4], float (&acc)[NP][5][4], double& lossp,
-                                              int& nvalid, float ctot) {
+                                              const float (&xin)[KU][V], float (&acc)[NP][5][V], double& lossp,
+                                              int& nvalid) {
   const uint32_t csign = sign_mask_vgpr();  // asinh2_f32: the accurate fp32 asinh (enf_frag.h)
-  using L = GL<D, KU>;
-  constexpr int V = 4, G = L::G, S = L::S;
+  using L = GL<D, V, KU>;
+  constexpr int G = L::G, S = L::S;
   const int grp = lane % G;
   float x[KU][V];
   float vm[KU];
@@ -375,13 +447,13 @@ __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0,
   float lad[KU] = {};
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
-    const float* r = rec + (size_t)p * kNP * D + grp * kNP * V;
+    const float* r = rec_lane<D, V>(rec, p, grp);
     float vh[V], gam[V], dl2[V], il[V], nxil[V];
-    lds_vec<float, V>(r, vh);
-    lds_vec<float, V>(r + V, gam);
-    lds_vec<float, V>(r + 2 * V, dl2);
-    lds_vec<float, V>(r + 3 * V, il);
-    lds_vec<float, V>(r + 4 * V, nxil);
+    lds_rows<V>(r, vh);
+    lds_rows<V>(r + 4, gam);
+    lds_rows<V>(r + 8, dl2);
+    lds_rows<V>(r + 12, il);
+    lds_rows<V>(r + 16, nxil);
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
       float t = vh[0] * x[u][0];
@@ -400,7 +472,7 @@ __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0,
         ls[p][u][e] = asinh2_f32(zs[p][u][e], q[e], ss[p][u][e], csign);
         x[u][e] = fmaf(dl2[e], ls[p][u][e], gam[e]);
       }
-      lad[u] = fmaf(-0.5f, hw_log2((q[0] * q[1]) * (q[2] * q[3])), lad[u]);
+      lad[u] = fmaf(-0.5f, hw_log2(prod_rows<V>(q)), lad[u]);
     }
   }
 #pragma unroll
@@ -411,7 +483,7 @@ __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0,
     const float ysq = group_sum<G>(t);
     const float ltot = group_sum<G>(lad[u]);
     if (grp == 0 && vm[u] != 0.f) {
-      lossp += 0.5 * (double)ysq + 0.5 * D * 1.8378770664093454836 - ((double)ctot + kLn2 * (double)ltot);
+      lossp += 0.5 * (double)ysq + 0.5 * D * 1.8378770664093454836 - kLn2 * (double)ltot;
       ++nvalid;
     }
   }
@@ -422,13 +494,13 @@ __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0,
     for (int e = 0; e < V; ++e) g[u][e] = x[u][e] * vm[u];
 #pragma unroll
   for (int p = NP - 1; p >= 0; --p) {
-    const float* r = rec + (size_t)p * kNP * D + grp * kNP * V;
+    const float* r = rec_lane<D, V>(rec, p, grp);
     float vh[V], il[V], lam[V], xi[V], del[V];
-    lds_vec<float, V>(r, vh);
-    lds_vec<float, V>(r + 3 * V, il);
-    lds_vec<float, V>(r + 5 * V, lam);
-    lds_vec<float, V>(r + 6 * V, xi);
-    lds_vec<float, V>(r + 7 * V, del);
+    lds_rows<V>(r, vh);
+    lds_rows<V>(r + 12, il);
+    lds_rows<V>(r + 20, lam);
+    lds_rows<V>(r + 24, xi);
+    lds_rows<V>(r + 28, del);
     float gh[KU][V], u_[KU][V];
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
@@ -461,90 +533,170 @@ __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0,
   }
 }
 
-template <int D, int KU, int NP>
-__global__ __launch_bounds__(256) void hj_grad_reg_kernel(HJGradArgs a) {
-  using L = GL<D, KU>;
+template <int D, int V, int KU, int NP, int W>
+__global__ __launch_bounds__(64 * W) void hj_grad_reg_kernel(HJGradArgs a) {
+  using L = GL<D, V, KU>;
   constexpr int G = L::G;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   double* scr = reinterpret_cast<double*>(smem);
-  float* rec = reinterpret_cast<float*>(smem + 256);
+  if (blockIdx.x == 0) {
+    ctot_block<D, 64 * W>(a, scr);
+    return;
+  }
+  float* rec = reinterpret_cast<float*>(smem + kScrBytes);
   const size_t recb = (size_t)NP * kNP * D * 4;
-  float* accs = reinterpret_cast<float*>(smem + 256 + recb);  // per wave [pair][param 5][D]
+  float* accs = reinterpret_cast<float*>(smem + kScrBytes + recb);  // per wave [pair][param 5][D]
   const int64_t ntiles = (a.N + L::TC - 1) / L::TC;
-  const int64_t wave_id = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(wave);
+  const int64_t wave_id = (int64_t)(blockIdx.x - 1) * W + __builtin_amdgcn_readfirstlane(wave);
   // the wave's first tile is loaded before the prologue: its HBM latency overlaps the parameter round trip
-  // (round 4; at the 8-rank share of config 5 a wave has about one tile)
-  float xc[KU][4], xn[KU][4];
-  if (wave_id < ntiles) grad_load_reg<D, KU>(a, wave_id * L::TC, lane, xc);
-  const float ctot = grad_prologue<D>(a, scr, rec);
-  float acc[NP][5][4];
+  float xc[KU][V], xn[KU][V];
+  if (wave_id < ntiles) grad_load_reg<D, V, KU>(a, wave_id * L::TC, lane, xc);
+  grad_prologue<D, 64 * W>(a, scr, rec);
+  float acc[NP][5][V];
 #pragma unroll
   for (int p = 0; p < NP; ++p)
 #pragma unroll
     for (int k = 0; k < 5; ++k)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc[p][k][e] = 0.f;
+      for (int e = 0; e < V; ++e) acc[p][k][e] = 0.f;
   double lossp = 0.0;
   int nvalid = 0;
   const int64_t full = a.N / L::TC;
   // the next tile's columns are loaded while the current one is processed
-  const int64_t stride = (int64_t)gridDim.x * 4;
+  const int64_t stride = (int64_t)(gridDim.x - 1) * W;
   for (int64_t t = wave_id; t < ntiles; t += stride) {
-    if (t + stride < ntiles) grad_load_reg<D, KU>(a, (t + stride) * L::TC, lane, xn);
-    if (t < full) grad_tile_reg<D, KU, NP, false>(a, t * L::TC, lane, rec, xc, acc, lossp, nvalid, ctot);
-    else grad_tile_reg<D, KU, NP, true>(a, t * L::TC, lane, rec, xc, acc, lossp, nvalid, ctot);
+    if (t + stride < ntiles) grad_load_reg<D, V, KU>(a, (t + stride) * L::TC, lane, xn);
+    if (t < full) grad_tile_reg<D, V, KU, NP, false>(a, t * L::TC, lane, rec, xc, acc, lossp, nvalid);
+    else grad_tile_reg<D, V, KU, NP, true>(a, t * L::TC, lane, rec, xc, acc, lossp, nvalid);
 #pragma unroll
     for (int u = 0; u < KU; ++u)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) xc[u][e] = xn[u][e];
+      for (int e = 0; e < V; ++e) xc[u][e] = xn[u][e];
   }
-  // one cross-slot reduction per wave; lanes 0..G-1 then hold the row sums of their 4 rows
+  // one cross-slot reduction per wave; lanes 0..G-1 then hold the row sums of their V rows
   float* wacc = accs + (size_t)wave * NP * 5 * D;
 #pragma unroll
   for (int p = 0; p < NP; ++p)
 #pragma unroll
     for (int k = 0; k < 5; ++k)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < V; ++e) {
         const float sv = slot_sum<G>(acc[p][k][e]);
-        if (lane < G) wacc[(p * 5 + k) * D + 4 * lane + e] = sv;
+        if (lane < G) wacc[(p * 5 + k) * D + V * lane + e] = sv;
       }
   __syncthreads();
-  grad_epilogue<D>(a, scr, rec, accs, (size_t)NP * 5 * D, lossp, nvalid);
+  grad_epilogue<D, W>(a, scr, rec, accs, (size_t)NP * 5 * D, lossp, nvalid);
 }
 
-template <int D, int KU, int NP>
-size_t hj_grad_reg_lds() {
-  return 256 + (size_t)NP * kNP * D * 4 + 4 * (size_t)NP * 5 * D * 4;
+template <int D, int NP, int W>
+constexpr size_t hj_grad_reg_lds() {
+  return kScrBytes + (size_t)NP * kNP * D * 4 + (size_t)W * NP * 5 * D * 4;
 }
 
 template <int D, int KU>
 size_t hj_grad_lds(int n) {
-  return 256 + (size_t)n * kNP * D * 4 + 4 * ((size_t)n * 5 * D * 4 + (size_t)n * KU * 64 * 16 + (size_t)n * KU * 64 * 4);
+  return kScrBytes + (size_t)n * kNP * D * 4 + 4 * ((size_t)n * 5 * D * 4 + (size_t)n * KU * 64 * 16 + (size_t)n * KU * 64 * 4);
 }
 
-template <int D, int KU, int NP>
-hipError_t launch_reg_np(const HJGradArgs& a, int blocks, hipStream_t st) {
-  const size_t lds = hj_grad_reg_lds<D, KU, NP>();
-  hipLaunchKernelGGL((hj_grad_reg_kernel<D, KU, NP>), dim3(blocks), dim3(256), lds, st, a);
-  return hipGetLastError();
+// ---- variant table: (V rows per lane, KU fragments per tile, W waves per block) of the register kernel.
+// The product uses kProd; the diagnostics build can select the others (ENF_HJG_VARIANT) for A/B runs.
+struct RegVariant {
+  int V, KU, W;
+};
+constexpr RegVariant kRegVariants[] = {
+    {2, 2, 8},   // 0: the product (round 5)
+    {4, 1, 4},   // 1: round 4's kernel shape (16-byte fragments, 4 waves per block)
+    {4, 1, 8},   // 2
+    {2, 2, 4},   // 3
+    {1, 2, 8},   // 4
+    {1, 2, 16},  // 5
+    {2, 1, 8},   // 6
+};
+constexpr int kNumRegVariants = ENF_DIAG ? (int)(sizeof(kRegVariants) / sizeof(kRegVariants[0])) : 1;
+
+int reg_variant() {
+  static const int v = ENF_KNOB("ENF_HJG_VARIANT", 0);
+  return (v >= 0 && v < kNumRegVariants) ? v : 0;
 }
 
-template <int D, int KU>
-hipError_t launch_reg(const HJGradArgs& a, int blocks, hipStream_t st) {
-  switch (a.n) {
-    case 1: return launch_reg_np<D, KU, 1>(a, blocks, st);
-    case 2: return launch_reg_np<D, KU, 2>(a, blocks, st);
-    case 3: return launch_reg_np<D, KU, 3>(a, blocks, st);
-    default: return launch_reg_np<D, KU, 4>(a, blocks, st);
+template <int D, int V, int KU, int NP, int W>
+const void* reg_kernel_ptr() {
+  return reinterpret_cast<const void*>(&hj_grad_reg_kernel<D, V, KU, NP, W>);
+}
+
+// (kernel, LDS bytes, columns per wave tile, waves per block) of the register kernel for (D, n pairs, variant)
+struct KSel {
+  const void* k = nullptr;
+  size_t lds = 0;
+  int tc = 0, w = 0;
+};
+
+template <int D, int V, int KU, int W>
+KSel sel_np(int n) {
+  KSel s;
+  s.tc = GL<D, V, KU>::TC;
+  s.w = W;
+  switch (n) {
+    case 1: s.k = reg_kernel_ptr<D, V, KU, 1, W>(); s.lds = hj_grad_reg_lds<D, 1, W>(); break;
+    case 2: s.k = reg_kernel_ptr<D, V, KU, 2, W>(); s.lds = hj_grad_reg_lds<D, 2, W>(); break;
+    case 3: s.k = reg_kernel_ptr<D, V, KU, 3, W>(); s.lds = hj_grad_reg_lds<D, 3, W>(); break;
+    default: s.k = reg_kernel_ptr<D, V, KU, 4, W>(); s.lds = hj_grad_reg_lds<D, 4, W>(); break;
   }
+  return s;
+}
+
+template <int D>
+KSel select_reg(int n, int variant) {
+  switch (variant) {
+#if ENF_DIAG
+    case 1: return sel_np<D, 4, 1, 4>(n);
+    case 2: return sel_np<D, 4, 1, 8>(n);
+    case 3: return sel_np<D, 2, 2, 4>(n);
+    case 4: return sel_np<D, 1, 2, 8>(n);
+    case 5: return sel_np<D, 1, 2, 16>(n);
+    case 6: return sel_np<D, 2, 1, 8>(n);
+#endif
+    default: return sel_np<D, 2, 2, 8>(n);
+  }
+}
+
+KSel select_kernel(int64_t D, int n) {
+  if (n <= 4) return D == 32 ? select_reg<32>(n, reg_variant()) : select_reg<64>(n, reg_variant());
+  static const int ku = ENF_KNOB("ENF_GRAD_U", 2) == 1 ? 1 : 2;  // 2: measured 72 vs 93 us at config 5
+  KSel s;
+  s.w = 4;
+  s.tc = (D == 32 ? GL<32, 4, 1>::S : GL<64, 4, 1>::S) * ku;
+  s.lds = D == 32 ? (ku == 1 ? hj_grad_lds<32, 1>(n) : hj_grad_lds<32, 2>(n))
+                  : (ku == 1 ? hj_grad_lds<64, 1>(n) : hj_grad_lds<64, 2>(n));
+  s.k = D == 32 ? (ku == 1 ? (const void*)&hj_grad_kernel<32, 1> : (const void*)&hj_grad_kernel<32, 2>)
+                : (ku == 1 ? (const void*)&hj_grad_kernel<64, 1> : (const void*)&hj_grad_kernel<64, 2>);
+  return s;
+}
+
+// tile blocks for N columns: one tile per wave where the chip has room for them, otherwise the blocks that are
+// resident at once (occupancy of the kernel at its LDS size), each wave striding over the tiles
+int blocks_for(const KSel& s, int64_t N) {
+  static int cached_cu = 0;
+  if (!cached_cu) {
+    DeviceInfo dev;
+    cached_cu = current_device_info(&dev) == ENF_OK && dev.num_cu > 0 ? dev.num_cu : 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, s.k, 64 * s.w, s.lds) != hipSuccess || per_cu < 1) per_cu = 1;
+  static const int cap_knob = ENF_KNOB("ENF_HJG_BPC", 0);  // diagnostics: blocks per CU cap (0: occupancy)
+  if (cap_knob > 0 && per_cu > cap_knob) per_cu = cap_knob;
+  const int64_t tiles = (N + s.tc - 1) / s.tc;
+  int64_t blocks = (tiles + s.w - 1) / s.w;
+  const int64_t cap = (int64_t)cached_cu * per_cu;
+  if (blocks > cap) blocks = cap;
+  return (int)(blocks < 1 ? 1 : blocks);
 }
 
 }  // namespace
 
-bool hj_grad_eligible(int64_t D, int64_t ldx, const void* X, const enf_layer* layers, int32_t nlayers) {
-  if ((D != 32 && D != 64) || ldx != D || (((uintptr_t)X) & 15) != 0) return false;
+bool hj_grad_shape_ok(int64_t D, const enf_layer* layers, int32_t nlayers) {
+  if (D != 32 && D != 64) return false;
   if (nlayers < 2 || (nlayers & 1) || nlayers / 2 > kHJGradMaxPairs) return false;
   for (int32_t l = 0; l < nlayers; ++l) {
     const int want = (l & 1) ? OP_JOHNSON : OP_HOUSEHOLDER;
@@ -553,8 +705,14 @@ bool hj_grad_eligible(int64_t D, int64_t ldx, const void* X, const enf_layer* la
   return true;
 }
 
+bool hj_grad_eligible(int64_t D, int64_t ldx, const void* X, const enf_layer* layers, int32_t nlayers) {
+  return ldx == D && (((uintptr_t)X) & 15) == 0 && hj_grad_shape_ok(D, layers, nlayers);
+}
+
+int hj_grad_blocks(int64_t D, int64_t N, int32_t npairs) { return blocks_for(select_kernel(D, npairs), N); }
+
 hipError_t launch_hj_grad(int64_t D, int64_t N, const void* X, const enf_layer* layers, int32_t nlayers,
-                          int32_t nparams, double* partial, int blocks, hipStream_t st) {
+                          int32_t nparams, double* partial, double* ctot_out, int* nblocks, hipStream_t st) {
   HJGradArgs a;
   std::memset(&a, 0, sizeof a);
   a.X = (const float*)X;
@@ -562,6 +720,7 @@ hipError_t launch_hj_grad(int64_t D, int64_t N, const void* X, const enf_layer* 
   a.n = nlayers / 2;
   a.D = (int32_t)D;
   a.partial = partial;
+  a.ctot_out = ctot_out;
   a.nparams = nparams;
   int32_t off = 0;
   for (int p = 0; p < a.n; ++p) {
@@ -578,30 +737,15 @@ hipError_t launch_hj_grad(int64_t D, int64_t N, const void* X, const enf_layer* 
     off += 4 * (int32_t)D;
   }
   if (off != nparams) return hipErrorInvalidValue;
-  // register variant for <= 4 pairs (ENF_GRAD_REG=0: the LDS variant; ENF_GRAD_RU: its KU)
-  static const int reg = ENF_KNOB("ENF_GRAD_REG", 1);
-  static const int ru = ENF_KNOB("ENF_GRAD_RU", 1) == 2 ? 2 : 1;  // 1: 215 VGPRs at 4 pairs (2 waves/SIMD)
-  if (reg && a.n <= 4) {
-    if (D == 32) return ru == 1 ? launch_reg<32, 1>(a, blocks, st) : launch_reg<32, 2>(a, blocks, st);
-    return ru == 1 ? launch_reg<64, 1>(a, blocks, st) : launch_reg<64, 2>(a, blocks, st);
-  }
-  static const int ku = ENF_KNOB("ENF_GRAD_U", 2) == 1 ? 1 : 2;  // 2: measured 72 vs 93 us at config 5
-  const size_t lds = D == 32 ? (ku == 1 ? hj_grad_lds<32, 1>(a.n) : hj_grad_lds<32, 2>(a.n))
-                             : (ku == 1 ? hj_grad_lds<64, 1>(a.n) : hj_grad_lds<64, 2>(a.n));
-  const void* k = D == 32 ? (ku == 1 ? (const void*)&hj_grad_kernel<32, 1> : (const void*)&hj_grad_kernel<32, 2>)
-                          : (ku == 1 ? (const void*)&hj_grad_kernel<64, 1> : (const void*)&hj_grad_kernel<64, 2>);
-  if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const KSel s = select_kernel(D, a.n);
+  const int blocks = blocks_for(s, N);
+  *nblocks = blocks;
+  if (s.lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(s.k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds);
     if (e != hipSuccess) return e;
   }
-  if (D == 32) {
-    if (ku == 1) hipLaunchKernelGGL((hj_grad_kernel<32, 1>), dim3(blocks), dim3(256), lds, st, a);
-    else hipLaunchKernelGGL((hj_grad_kernel<32, 2>), dim3(blocks), dim3(256), lds, st, a);
-  } else {
-    if (ku == 1) hipLaunchKernelGGL((hj_grad_kernel<64, 1>), dim3(blocks), dim3(256), lds, st, a);
-    else hipLaunchKernelGGL((hj_grad_kernel<64, 2>), dim3(blocks), dim3(256), lds, st, a);
-  }
-  return hipGetLastError();
+  void* args[] = {&a};
+  return hipLaunchKernel(s.k, dim3(blocks + 1), dim3(64 * s.w), args, s.lds, st);
 }
 
 }  // namespace enf

@@ -1,17 +1,31 @@
 // enf_grad_tail.h -- the reduction side of the whitening-loss gradient (config 5), shared by the generic
 // gradient kernel (enf_grad.hip) and the fused (J o H)^n kernels (enf_grad_hj.hip).
 //
-// Every gradient block writes one partial vector [loss, gradient...] (double). They are summed in
-// kSumSlices slices of consecutive blocks, each slice in block order (grad_sum_kernel's fixed tree), the
-// slices in order, then the Householder direction projection (householder_trafo.jl:22-40) and, for the
-// fused single-rank optimize_whitening step, the loss / ADAGrad / re-normalisation
-// (optimize_whitening.jl:36-42).
+// Every gradient block writes one partial row [loss, gradient...] (double). grad_reduce_kernel sums them and
+// finishes the step in ONE launch (round 5; rounds 1-4 ran a slice-sum launch and a one-block tail that walked
+// every parameter in turn: 4.7 + 7.8 us per config-5 step):
 //
-// Round 3 measured running the finalisation / whitening tail inside the slice-sum launch (a ticket taken
-// after a device-scope fence, the last block runs the rest): 50.7 vs 44.7 us per config-5 step, and in the
-// gradient kernel 98.7 vs 44.5 us -- on gfx950 each device-scope fence writes back and invalidates the XCD's
-// L2 (profiles/r03_train_sum_tail_ab.txt, r03_train_fused_tail_in_gradient_ab.txt). Rejected; round 4
-// removed that code path, so the product always launches the slice sums and the tail separately.
+//   block 0            the loss entry: the partial rows' sum, minus N times the flow's constant ladj when the
+//                      fused (J o H)^n kernel computed it once instead of per column (enf_grad_hj.hip);
+//   block 1 + b        the gradient entries of `upb` consecutive parameter vectors ("units": every vector of the
+//                      gradient layout is D entries -- a Householder column, a Johnson gamma, ...): their sums
+//                      over the partial rows, then per mode
+//     MODE_SUM         the raw sums to tot (a data-parallel rank's contribution, before the cross-rank sum);
+//     MODE_OUT         the Householder direction projection (householder_trafo.jl:22-40) and out += (T) sum
+//                      (enf_flow_negll_grad, enf_flow_vjp);
+//     MODE_STEP        the projection, ADAGrad (Optimisers.update, optimize_whitening.jl:36-42) on the entries in
+//                      the trainable runs and the re-normalisation of the Householder columns among the block's
+//                      units -- no unit depends on another, so the blocks need no synchronisation.
+//
+// The sum of an entry is a fixed tree (J lanes per entry, each over partial rows j, j + J, ... with 8
+// accumulators, then the J lanes in order): deterministic, and the same in every mode, so the fused
+// single-rank step, the one-call data-parallel step on one rank (MODE_SUM, the identity all-reduce, MODE_STEP
+// over that one row) and the three-call step (MODE_OUT, all-reduce, enf_whitening_apply) agree bit for bit.
+//
+// Round 3 measured running the finalisation inside the gradient kernel (a ticket taken after a device-scope
+// fence, the last block runs the rest): slower, each device-scope fence writes back and invalidates the XCD's L2
+// (profiles/r03_train_sum_tail_ab.txt, r03_train_fused_tail_in_gradient_ab.txt). The reduction stays a launch
+// of its own.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -24,25 +38,32 @@
 namespace enf {
 
 constexpr int kMaxGradSteps = 32;
+// rows of totals the workspace reserves after the partial rows (one is used: tot, then the constant ladj)
 constexpr int kSumSlices = 8;
+constexpr int kRedThreads = 512;
+constexpr int kRedMaxEntries = 1024;  // entries of one reduction block: max(D, 32) <= 1024
 
-// Sum the block partials (double, block order), project Householder direction gradients, add to out.
+enum ReduceMode { MODE_SUM = 0, MODE_OUT = 1, MODE_STEP = 2 };
+
 struct ReduceArgs {
-  const double* partial;
+  const double* partial;  // [nblocks][1 + nparams] (nblocks == 1: an already reduced row)
   int32_t nblocks;
   int32_t nparams;
   int32_t D;
-  int32_t nh;  // Householder columns
-  int32_t skip_loss;  // enf_flow_vjp: out has no loss slot (out[i - 1] += tot[i])
-  void* out;
-  double* tot;  // kSumSlices x (1 + nparams) slice totals (workspace tail); slice 0 = the total
+  int32_t nh;         // Householder columns
+  int32_t skip_loss;  // MODE_OUT for enf_flow_vjp: out has no loss slot (out[i] += tot[1 + i])
+  int32_t upb;        // units (vectors of D entries) per reduction block
+  const double* ctot;  // nullable: the flow's constant ladj per column; the loss gets -nloc * ctot
+  int64_t nloc;
+  void* out;    // MODE_OUT
+  double* tot;  // MODE_SUM: 1 + nparams
   // per Householder column: offset of its gradient vector and its device column pointer
   int32_t hoff[kMaxGradSteps];
   const void* hcol[kMaxGradSteps];
 };
 
-// The rest of a single-rank optimize_whitening step (enf_whitening_step) / the update half of a
-// data-parallel one (enf_whitening_apply).
+// MODE_STEP: the rest of a single-rank optimize_whitening step (enf_whitening_step) / the update half of a
+// data-parallel one (enf_whitening_step_dp after the cross-rank sum).
 struct StepArgs {
   void* theta;
   void* acc;
@@ -54,89 +75,213 @@ struct StepArgs {
   int64_t hb[kMaxStepHB][3];  // offset, k, ldv
 };
 
-// Slices -> total, then the Householder direction projection on tot (whole block of 4 waves; ends
-// with a barrier, tot[0 .. nparams] final).
-template <typename T>
-__device__ __forceinline__ void finalize_totals(const ReduceArgs& r) {
-  double* tot = r.tot;
+inline int reduce_units_per_block(int64_t D) { return D >= 32 ? 1 : (int)(32 / D); }
+inline int reduce_grid(int64_t D, int64_t nparams) {
+  const int64_t units = nparams / D;
+  const int upb = reduce_units_per_block(D);
+  return 1 + (int)((units + upb - 1) / upb);
+}
+
+// Sum of entry column c over the partial rows j, j + J, j + 2J, ... (rows of n doubles), with up to kBatch loads in
+// flight per batch (the rows were written by the previous launch: every batch is one round trip to the caches),
+// added into 8 accumulators in a fixed order.
+constexpr int kBatch = 32;
+__device__ __forceinline__ double rows_sum(const double* __restrict__ P, int nb, int64_t n, int64_t c, int j, int J) {
+  double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int b0 = j; b0 < nb; b0 += kBatch * J) {
+    double v[kBatch];
+#pragma unroll
+    for (int k = 0; k < kBatch; ++k) {
+      const int b = b0 + k * J;
+      v[k] = b < nb ? P[(int64_t)b * n + c] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < kBatch; ++k) s8[k & 7] += v[k];
+  }
+  return ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
+}
+
+// Sums entries [e0, e0 + E) of the rows (column offset c0 + i) into gl[0 .. E) (LDS), block-wide: J threads per
+// entry over interleaved rows, then the J partial sums in order. nblocks == 1: the row itself.
+__device__ __forceinline__ void block_sums(const ReduceArgs& r, int64_t c0, int E, double* __restrict__ gl,
+                                           double* __restrict__ red) {
+  const int tid = threadIdx.x;
   const int64_t n = 1 + (int64_t)r.nparams;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  // Householder columns h = w, w + 4, ... of this wave: their first 64 entries (one per lane; D > 64
-  // adds entries lane + 64, lane + 128, ... below) loaded while the slices are summed (they do not
-  // depend on the totals)
-  constexpr int kPerWave = (kMaxGradSteps + 3) / 4;
-  double vh[kPerWave], nrm[kPerWave];
-#pragma unroll
-  for (int j = 0; j < kPerWave; ++j) {
-    const int h = w + 4 * j;
-    vh[j] = (h < r.nh && lane < r.D) ? (double)((const T*)r.hcol[h])[lane] : 0.0;
+  const double* P = r.partial;
+  if (r.nblocks == 1) {
+    for (int i = tid; i < E; i += kRedThreads) gl[i] = P[c0 + i];
+    __syncthreads();
+    return;
   }
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {  // the slices in order, into slice 0
-    double t = tot[i];
-    for (int s = 1; s < kSumSlices; ++s) t += tot[s * n + i];
-    tot[i] = t;
-  }
-#pragma unroll
-  for (int j = 0; j < kPerWave; ++j) {
-    const int h = w + 4 * j;
-    double vv = vh[j] * vh[j];
-    if (h < r.nh)
-      for (int d = lane + 64; d < r.D; d += 64) {
-        const double v = (double)((const T*)r.hcol[h])[d];
-        vv += v * v;
-      }
-    for (int m = 32; m >= 1; m >>= 1) vv += __shfl_xor(vv, m);
-    nrm[j] = sqrt(vv);
-  }
-  __syncthreads();
-  // Householder: dS/dw = -sqrt2 * G;  dS/dv = (dS/dw - w (dS/dw . w)) / |v|  (householder_trafo.jl:32)
-#pragma unroll
-  for (int j = 0; j < kPerWave; ++j) {
-    const int h = w + 4 * j;
-    if (h >= r.nh) break;  // wave-uniform
-    double* gw = tot + 1 + r.hoff[h];
-    const T* vc = (const T*)r.hcol[h];
-    const double g = lane < r.D ? gw[lane] : 0.0;
-    const double wv = vh[j] / nrm[j];
-    double wd = -1.4142135623730951 * g * wv;
-    for (int d = lane + 64; d < r.D; d += 64) wd += -1.4142135623730951 * gw[d] * ((double)vc[d] / nrm[j]);
-    for (int m = 32; m >= 1; m >>= 1) wd += __shfl_xor(wd, m);
-    if (lane < r.D) gw[lane] = (-1.4142135623730951 * g - wv * wd) / nrm[j];
-    for (int d = lane + 64; d < r.D; d += 64)
-      gw[d] = (-1.4142135623730951 * gw[d] - ((double)vc[d] / nrm[j]) * wd) / nrm[j];
-  }
-  __syncthreads();
-}
-
-// grad_finalize_kernel's work: totals, projection, added into out
-template <typename T>
-__device__ __forceinline__ void finalize_into_out(const ReduceArgs& r) {
-  finalize_totals<T>(r);
-  T* out = (T*)r.out;
-  if (r.skip_loss) {
-    for (int i = threadIdx.x; i < r.nparams; i += blockDim.x) out[i] += (T)r.tot[1 + i];
+  if (2 * E <= kRedThreads) {
+    const int J = kRedThreads / E;
+    const int i = tid % E, j = tid / E;
+    if (j < J) red[j * E + i] = rows_sum(P, r.nblocks, n, c0 + i, j, J);
+    __syncthreads();
+    if (tid < E) {
+      double s = red[tid];
+      for (int q = 1; q < J; ++q) s += red[q * E + tid];
+      gl[tid] = s;
+    }
   } else {
-    for (int i = threadIdx.x; i < 1 + r.nparams; i += blockDim.x) out[i] += (T)r.tot[i];
+    for (int i = tid; i < E; i += kRedThreads) gl[i] = rows_sum(P, r.nblocks, n, c0 + i, 0, 1);
   }
+  __syncthreads();
 }
 
-// whitening_tail_kernel's work (S: StepArgs): loss/B (as the host computes out[0] / B in T),
-// ADAGrad over the trainable runs with g = (T)total (what enf_adagrad_step reads from a zeroed out), then
-// the Householder re-normalisation of every batch -- the operations and roundings of the unfused sequence.
-template <typename T, typename S>
-__device__ __forceinline__ void whitening_tail_body(const ReduceArgs& r, const S& a) {
-  finalize_totals<T>(r);
-  const double* tot = r.tot;
-  T* th = (T*)a.theta;
-  T* ac = (T*)a.acc;
-  if (threadIdx.x == 0) *a.loss_out = (double)((T)tot[0] / (T)a.nsamp);
-  for (int q = 0; q < a.nruns; ++q)
-    for (int64_t i = a.runs[q][0] + threadIdx.x; i < a.runs[q][1]; i += blockDim.x)
-      adagrad_update<T>(th[i], ac[i], (T)tot[1 + i], (T)a.scale, (T)a.eta, (T)a.eps);
+// Householder index of the unit starting at gradient offset off, or -1
+__device__ __forceinline__ int unit_householder(const ReduceArgs& r, int64_t off) {
+  for (int h = 0; h < r.nh; ++h)
+    if (r.hoff[h] == off) return h;
+  return -1;
+}
+
+// dS/dv from the direction sums G of one column (in gl, D entries) and the column v (vc, double):
+//   dS/dw = -sqrt2 G, dS/dv = (dS/dw - w (dS/dw . w)) / |v|, w = v / |v|  (householder_trafo.jl:22-40)
+// by one wave (sums over the lanes: d = lane, lane + 64, ..., then the xor tree).
+__device__ __forceinline__ void project_column(double* __restrict__ g, const double* __restrict__ vc, int D, int lane) {
+  double vv = 0.0;
+  for (int d = lane; d < D; d += 64) vv += vc[d] * vc[d];
+  for (int m = 32; m >= 1; m >>= 1) vv += __shfl_xor(vv, m);
+  const double nrm = sqrt(vv);
+  double wd = 0.0;
+  for (int d = lane; d < D; d += 64) wd += -1.4142135623730951 * g[d] * (vc[d] / nrm);
+  for (int m = 32; m >= 1; m >>= 1) wd += __shfl_xor(wd, m);
+  for (int d = lane; d < D; d += 64) g[d] = (-1.4142135623730951 * g[d] - (vc[d] / nrm) * wd) / nrm;
+}
+
+// LinearAlgebra.normalize! of one column held in LDS (src/householder_trafo.jl:135-139), by one wave: the sum of
+// squares in double over d = lane, lane + 64, ..., the xor tree, then v *= (T)(1/sqrt) -- normalize_column's
+// arithmetic (enf_train.h), so the separate enf_householder_normalize call rounds the same
+template <typename T>
+__device__ __forceinline__ void normalize_lds(T* __restrict__ v, int D, int lane) {
+  double ss = 0.0;
+  for (int d = lane; d < D; d += 64) ss += (double)v[d] * (double)v[d];
+  for (int m = 32; m >= 1; m >>= 1) ss += __shfl_xor(ss, m);
+  const T inv = (T)(1.0 / sqrt(ss));
+  for (int d = lane; d < D; d += 64) v[d] *= inv;
+}
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(kRedThreads) void grad_reduce_kernel(ReduceArgs r, StepArgs s) {
+  __shared__ double red[kRedThreads];
+  __shared__ double gl[kRedMaxEntries];
+  __shared__ double vcol[kRedMaxEntries];
+  __shared__ T thl[MODE == MODE_STEP ? kRedMaxEntries : 1];
+  __shared__ T acl[MODE == MODE_STEP ? kRedMaxEntries : 1];
+  __shared__ int flags[kRedMaxEntries];  // MODE_STEP: bit 0 trainable, bit 1 normalised column
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int kWaves = kRedThreads / 64;
+  const int64_t n = 1 + (int64_t)r.nparams;
+  if (blockIdx.x == 0) {  // the loss entry: one wave
+    if (tid < 64) {
+      double v;
+      if (r.nblocks == 1) {
+        v = r.partial[0];
+      } else {
+        v = rows_sum(r.partial, r.nblocks, n, 0, tid, 64);
+        for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+      }
+      if (tid == 0) {
+        if (r.ctot) v -= (double)r.nloc * *r.ctot;
+        if constexpr (MODE == MODE_SUM) r.tot[0] = v;
+        else if constexpr (MODE == MODE_OUT) {
+          if (!r.skip_loss) ((T*)r.out)[0] += (T)v;
+        } else {
+          *s.loss_out = (double)((T)v / (T)s.nsamp);
+        }
+      }
+    }
+    return;
+  }
+  const int D = r.D;
+  const int64_t units = r.nparams / D;
+  const int64_t u0 = (int64_t)(blockIdx.x - 1) * r.upb;
+  const int64_t u1 = u0 + r.upb < units ? u0 + r.upb : units;
+  const int64_t e0 = u0 * D;  // first gradient entry of the block
+  const int E = (int)((u1 - u0) * D);
+  // What does not depend on the sums is loaded first, into registers (one entry per thread when E <= the block's
+  // threads), so its round trip overlaps the sums' loads: the Householder columns, theta and the ADAGrad state.
+  auto prefetch = [&](int i, double& hv, T& thv, T& acv, int& f) {
+    hv = 0.0;
+    thv = acv = (T)0;
+    f = 0;
+    const int64_t e = e0 + i;
+    const int64_t uo = e0 + (i / D) * D;
+    const int h = unit_householder(r, uo);
+    if (h >= 0) hv = (double)((const T*)r.hcol[h])[i % D];
+    if constexpr (MODE == MODE_STEP) {
+      for (int q = 0; q < s.nruns; ++q) f |= (e >= s.runs[q][0] && e < s.runs[q][1]) ? 1 : 0;
+      for (int q = 0; q < s.nhb; ++q) {
+        const int64_t rel = uo - s.hb[q][0];
+        if (rel >= 0 && rel % s.hb[q][2] == 0 && rel / s.hb[q][2] < s.hb[q][1]) f |= 2;
+      }
+      if (f) thv = ((const T*)s.theta)[e];
+      if (f & 1) acv = ((const T*)s.acc)[e];
+    }
+  };
+  auto stage = [&](int i, double hv, T thv, T acv, int f) {
+    vcol[i] = hv;
+    if constexpr (MODE == MODE_STEP) {
+      flags[i] = f;
+      thl[i] = thv;
+      acl[i] = acv;
+    }
+  };
+  if constexpr (MODE == MODE_SUM) {
+    block_sums(r, 1 + e0, E, gl, red);
+  } else if (E <= kRedThreads) {  // (block-uniform) the prefetched values are staged after the sums' loads
+    double hv = 0.0;
+    T thv = (T)0, acv = (T)0;
+    int f = 0;
+    if (tid < E) prefetch(tid, hv, thv, acv, f);
+    block_sums(r, 1 + e0, E, gl, red);
+    if (tid < E) stage(tid, hv, thv, acv, f);
+  } else {
+    for (int i = tid; i < E; i += kRedThreads) {
+      double hv;
+      T thv, acv;
+      int f;
+      prefetch(i, hv, thv, acv, f);
+      stage(i, hv, thv, acv, f);
+    }
+    block_sums(r, 1 + e0, E, gl, red);
+  }
+  if constexpr (MODE == MODE_SUM) {
+    for (int i = tid; i < E; i += kRedThreads) r.tot[1 + e0 + i] = gl[i];
+    return;
+  }
+  __syncthreads();  // (the staged values)
+  // Householder direction projection, one wave per column unit
+  for (int64_t u = u0 + wave; u < u1; u += kWaves) {
+    if (unit_householder(r, u * D) < 0) continue;  // wave-uniform
+    const int o = (int)((u - u0) * D);
+    project_column(gl + o, vcol + o, D, lane);
+  }
   __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int q = 0; q < a.nhb; ++q)
-    for (int64_t c = w; c < a.hb[q][1]; c += 4) normalize_column<T>(th + a.hb[q][0] + c * a.hb[q][2], a.D, lane);
+  if constexpr (MODE == MODE_OUT) {
+    T* out = (T*)r.out;
+    const int64_t base = r.skip_loss ? 0 : 1;
+    for (int i = tid; i < E; i += kRedThreads) out[base + e0 + i] += (T)gl[i];
+    return;
+  }
+  if constexpr (MODE == MODE_STEP) {
+    for (int i = tid; i < E; i += kRedThreads)
+      if (flags[i] & 1) adagrad_update<T>(thl[i], acl[i], (T)gl[i], (T)s.scale, (T)s.eta, (T)s.eps);
+    __syncthreads();
+    for (int64_t u = u0 + wave; u < u1; u += kWaves) {
+      const int o = (int)((u - u0) * D);
+      if (flags[o] & 2) normalize_lds<T>(thl + o, D, lane);  // wave-uniform
+    }
+    __syncthreads();
+    T* th = (T*)s.theta;
+    T* ac = (T*)s.acc;
+    for (int i = tid; i < E; i += kRedThreads) {
+      const int f = flags[i];
+      if (f) th[e0 + i] = thl[i];
+      if (f & 1) ac[e0 + i] = acl[i];
+    }
+  }
 }
 
 }  // namespace enf

@@ -520,13 +520,15 @@ __device__ __forceinline__ void step_center_contract(Tile<T, D, U>& x, Acc<T, D,
             // exp(-b(xu - a)) = 1/e1 and exp(b(xu + a)) = 1/e2, so dy = e1/(1 + e1) + e2/(1 + e2), and
             // log(1 + e1) - log(1 + e2) = log((1 + e1)/(1 + e2)): two exp2, two rcp and two log2 instead of four
             // exp2, two rcp and three log2 (round 4, last session; the output the same with or without the ladj).
-            // An overflowing e (Inf * rcp(Inf) = NaN) gives its term 1 through fminf, as the reference's
-            // 1/(1 + 0); (1 + e1) r2 is Inf / 0 exactly where the reference's difference of logs is +-Inf.
+            // An overflowing e (Inf * rcp(Inf) = NaN) gives its term 1 by a select on e == +Inf, as the
+            // reference's 1/(1 + 0); a NaN input keeps its NaN (round 5: a min(., 1) clamp turned it into 1);
+            // (1 + e1) r2 is Inf / 0 exactly where the reference's difference of logs is +-Inf.
             const float r2 = hw_rcp(1.0f + e2);
             x[u][e] = hw_log2((1.0f + e1) * r2) * lnb;
             if (LADJ) {
-              const float dy = fminf(e1 * hw_rcp(1.0f + e1), 1.0f) + fminf(e2 * r2, 1.0f);
-              acc[u][e / SEG] += hw_log2(dy);
+              const float t1 = e1 == __builtin_inff() ? 1.0f : e1 * hw_rcp(1.0f + e1);
+              const float t2 = e2 == __builtin_inff() ? 1.0f : e2 * r2;
+              acc[u][e / SEG] += hw_log2(t1 + t2);
             }
           } else {
             // out of range somewhere in the wave: the literal formulas (ocml)

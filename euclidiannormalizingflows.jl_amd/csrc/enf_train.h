@@ -57,6 +57,9 @@ enf_status whitening_apply(bool f64, int64_t D, int64_t nparams, const void* g, 
                            const int64_t* runs, int32_t nruns, const int64_t* hb, int32_t nhb, double eta,
                            double epsilon, double* loss_out, hipStream_t st);
 
+// enf_copy.hip: the measurement copy (enf_stream_copy)
+enf_status stream_copy(const void* src, void* dst, int64_t bytes, int32_t variant, hipStream_t st);
+
 // Optimisers.jl 0.2 ADAGrad on one parameter (src/optimize_whitening.jl:40): the arithmetic shared
 // by enf_adagrad_step and the fused step, so both round identically.
 template <typename T>

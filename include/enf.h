@@ -213,6 +213,12 @@ enf_status enf_householder_normalize(enf_dtype dtype, int64_t D, int64_t k, void
 enf_status enf_householder_normalize_strided(enf_dtype dtype, int64_t D, int64_t k, void* V, int64_t ldv,
                                              void* hip_stream);
 
+/* Measurement helper, not a reference operation: a hand-written streaming copy of `bytes` from src to dst
+ * (16-byte aligned device buffers) -- the practical HBM ceiling bench.py reports the flow kernels against
+ * (SURVEY.md §8(d)). variant: 0 = 4 x 16-byte fragments per lane per iteration, nontemporal; 1 = the same,
+ * plain loads / stores; 2 = 8 fragments, nontemporal; 3 = one fragment per lane, one pass. */
+enf_status enf_stream_copy(const void* src, void* dst, int64_t bytes, int32_t variant, void* hip_stream);
+
 /* ------------------------------------------------------- JohnsonSU distribution -------- */
 /* JohnsonSU(gamma, delta, xi, lambda) (src/johnson_trafo.jl:1-26) evaluated elementwise over n
  * device values of the dtype, out[i] = fn(x[i]) (out may equal x), with the reference's formulas

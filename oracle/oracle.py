@@ -30,7 +30,8 @@ class _Layer(ctypes.Structure):
 
 def build() -> str:
     """Compile liboracle.so with gcc (oracle/Makefile) if it is missing or stale."""
-    src = [os.path.join(_HERE, f) for f in ("enf_oracle.c", "enf_oracle_jsu.c", "enf_oracle.h", "Makefile")]
+    src = [os.path.join(_HERE, f) for f in ("enf_oracle.c", "enf_oracle_jsu.c", "enf_oracle_grad.c", "enf_oracle.h",
+                                             "Makefile")]
     if not os.path.exists(_LIB) or os.path.getmtime(_LIB) < max(os.path.getmtime(s) for s in src):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB
@@ -64,6 +65,17 @@ def lib() -> ctypes.CDLL:
             f = getattr(_lib, f"or_mvnormal_negll_{S}")
             f.restype = T
             f.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
+        for S, T in (("f64", ctypes.c_double), ("f80", ctypes.c_longdouble)):
+            f = getattr(_lib, f"or_param_count_{S}")
+            f.restype, f.argtypes = ctypes.c_int64, [ctypes.c_int64, ctypes.POINTER(_Layer), ctypes.c_int32]
+            f = getattr(_lib, f"or_negll_grad_{S}")
+            f.restype = ctypes.c_int
+            f.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(_Layer),
+                          ctypes.c_int32, ctypes.c_void_p]
+            f = getattr(_lib, f"or_optimize_whitening_{S}")
+            f.restype = ctypes.c_int64
+            f.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.POINTER(_Layer), ctypes.c_int32,
+                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, T, T, ctypes.c_void_p]
         f = _lib.or_norminvcdf_f64
         f.restype, f.argtypes = ctypes.c_double, [ctypes.c_double]
         f = _lib.or_jsu_eval_vec_f64
@@ -180,6 +192,70 @@ def mvnormal_negll(Y: np.ndarray, ladj: np.ndarray) -> float:
     D, N = Y.shape
     ladj = np.ascontiguousarray(ladj, dtype=Y.dtype)
     return getattr(lib(), f"or_mvnormal_negll_{_sfx(Y.dtype)}")(D, N, Y.ctypes.data, ladj.ctypes.data)
+
+
+def _grad_dtype(dtype):
+    if np.dtype(dtype) not in (np.dtype(np.float64), np.dtype(np.longdouble)):
+        raise ValueError("oracle gradient: float64 or longdouble")
+    return "f64" if np.dtype(dtype) == np.dtype(np.float64) else "f80"
+
+
+def theta_of(layers, D, dtype=np.float64):
+    """The flat parameter vector of a flow in the enf_flow_param_count layout (per layer, per field, length-D
+    vectors; a Householder V as its D x k matrix, column-major)."""
+    out = []
+    for op, ps in layers:
+        for p in ps:
+            a = np.asarray(p, dtype=dtype)
+            out.append(a.reshape(D, -1, order="F").reshape(-1, order="F") if op == OP_HOUSEHOLDER
+                       else np.broadcast_to(a, (D,)).astype(dtype))
+    return np.concatenate(out)
+
+
+def _theta_layers(layers, theta, D):
+    """ctypes layers whose parameter pointers point into theta (the layout of theta_of)."""
+    arr = (_Layer * max(1, len(layers)))()
+    o = 0
+    esz = theta.dtype.itemsize
+    for i, (op, ps) in enumerate(layers):
+        arr[i].op = op
+        arr[i].k = np.asarray(ps[0]).reshape(D, -1, order="F").shape[1] if op == OP_HOUSEHOLDER else 0
+        for q in range(len(ps)):
+            arr[i].p[q] = theta.ctypes.data + o * esz
+            o += D * (arr[i].k if op == OP_HOUSEHOLDER else 1)
+    return arr
+
+
+def negll_grad(layers, X: np.ndarray):
+    """mvnormal_negll_trafograd (src/optimize_whitening.jl:18-22) on the CPU: (negll, gradient) with the gradient
+    flat in the enf_flow_param_count layout (theta_of). float64 or longdouble (x87) data."""
+    X = np.asfortranarray(X)
+    D, N = X.shape
+    S = _grad_dtype(X.dtype)
+    theta = theta_of(layers, D, X.dtype)
+    arr = _theta_layers(layers, theta, D)
+    out = np.zeros(1 + theta.size, dtype=X.dtype)
+    if getattr(lib(), f"or_negll_grad_{S}")(D, N, X.ctypes.data, D, arr, len(layers), out.ctypes.data) != 0:
+        raise ValueError("oracle: unknown op in flow")
+    return float(out[0]), out[1:]
+
+
+def optimize_whitening(layers, X: np.ndarray, nbatches: int, nepochs: int, eta: float = 0.1, epsilon: float = 1e-8):
+    """optimize_whitening (src/optimize_whitening.jl:25-45) with ADAGrad(eta, epsilon) on the CPU: returns
+    (theta, acc, negll_history), theta in the theta_of layout."""
+    X = np.asfortranarray(X)
+    D, N = X.shape
+    S = _grad_dtype(X.dtype)
+    theta = theta_of(layers, D, X.dtype)
+    acc = np.full_like(theta, epsilon)
+    arr = _theta_layers(layers, theta, D)
+    bs = max(int(round(N / nbatches)), 1)
+    hist = np.zeros(nepochs * (-(-N // bs)), dtype=X.dtype)
+    n = getattr(lib(), f"or_optimize_whitening_{S}")(D, N, X.ctypes.data, arr, len(layers), theta.ctypes.data,
+                                                     acc.ctypes.data, nbatches, nepochs, eta, epsilon, hist.ctypes.data)
+    if n < 0:
+        raise ValueError("oracle: unknown op in flow")
+    return theta, acc, hist[:n]
 
 
 def inverse_layers(layers, dtype=np.float64):

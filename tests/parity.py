@@ -57,6 +57,16 @@ def ladj_err(L, Lref):
     return float(np.nanmax(np.where(np.isnan(e), np.inf, e)))
 
 
+def loss_close(got, ref, rtol):
+    """A scalar loss against the reference's: equal infinities (an overflowing flow in both) pass, NaN never does,
+    finite values within rtol * (|ref| + 1). (Plain |got - ref| <= tol cannot tell a matching +-Inf from a real
+    mismatch: Inf - Inf is NaN and the comparison is False either way.)"""
+    got, ref = float(got), float(ref)
+    if np.isinf(ref) or np.isinf(got):
+        return got == ref
+    return bool(np.isfinite(got) and np.isfinite(ref) and abs(got - ref) <= rtol * (abs(ref) + 1.0))
+
+
 K_REF = 4.0
 
 

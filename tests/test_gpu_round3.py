@@ -13,7 +13,7 @@
 import numpy as np
 import pytest
 
-from parity import check_vs_oracle, colmajor_cuda, make_flow, rand_params, to_np
+from parity import check_vs_oracle, colmajor_cuda, loss_close, make_flow, rand_params, to_np
 
 pytestmark = pytest.mark.gpu
 
@@ -46,7 +46,7 @@ def test_negll_grad_large_D_finite_differences(enf, gpu, oracle, D):
     X = np.asfortranarray(0.8 * rng.standard_normal((D, 301)))
     negll, grads = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X))
     ref = oracle_negll(oracle, layers, X)
-    assert abs(negll - ref) <= 1e-12 * (abs(ref) + 1)
+    assert loss_close(negll, ref, 1e-12), (negll, ref)
     g = np.concatenate([np.asarray(a).reshape(-1, order="F") for per in grads for a in per])
     nvec = g.size // D  # parameter vectors of length D
     idx = [v * D + int(r) for v in range(nvec) for r in rng.choice(D, 240 // nvec + 1, replace=False)]
@@ -68,7 +68,7 @@ def test_negll_grad_D256_fp32(enf, gpu, oracle):
     l64 = [(op, [np.asarray(p, np.float64) for p in ps]) for op, ps in layers]
     X64 = np.asfortranarray(X.astype(np.float64))
     ref = oracle_negll(oracle, l64, X64)
-    assert abs(n32 - ref) <= 1e-4 * (abs(ref) + 1)
+    assert loss_close(n32, ref, 1e-4), (n32, ref)
     g = np.concatenate([np.asarray(x, np.float64).reshape(-1, order="F") for per in g32 for x in per])
     idx = [v * D + int(r) for v in range(g.size // D) for r in rng.choice(D, 6, replace=False)]
     _fd_check(oracle, l64, X64, g, D, idx, rel=1e-3, floor=0.1)

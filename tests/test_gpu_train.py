@@ -6,7 +6,7 @@ item 5): "parity unpinned" -- pinned here by finite differences of the oracle in
 import numpy as np
 import pytest
 
-from parity import colmajor_cuda, make_flow, rand_params, to_np
+from parity import colmajor_cuda, loss_close, make_flow, rand_params, to_np
 
 pytestmark = pytest.mark.gpu
 
@@ -53,7 +53,7 @@ def test_negll_grad_finite_differences(enf, gpu, oracle, D):
     X = np.asfortranarray(0.8 * rng.standard_normal((D, 257)))
     negll, grads = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X))
     ref = oracle_negll(oracle, layers, X)
-    assert abs(negll - ref) <= 1e-12 * (abs(ref) + 1)
+    assert loss_close(negll, ref, 1e-12), (negll, ref)
     g = np.concatenate([np.asarray(a).reshape(-1, order="F") for per in grads for a in per])
     th0 = flat(layers, D)
     assert g.shape == th0.shape

@@ -137,3 +137,80 @@ def test_negll(oracle):
     L = np.full(4, 0.5)
     expect = -((-np.log(2 * np.pi) / 2) * 2 * 4 + 0.5 * 4) / 4
     assert abs(oracle.mvnormal_negll(Y, L) - expect) < 1e-14
+
+
+def _unflat(layers, theta, D):
+    res, o = [], 0
+    for op, ps in layers:
+        new = []
+        for p in ps:
+            n = np.asarray(p).size if op == 5 else D
+            v = theta[o:o + n]
+            new.append(v.reshape(D, -1, order="F") if op == 5 else v.copy())
+            o += n
+        res.append((op, new))
+    return res
+
+
+@pytest.mark.parametrize("D", [1, 2, 5])
+def test_oracle_gradient_vs_central_differences(oracle, D):
+    """The oracle's reverse pass (enf_oracle_grad.c: mvnormal_negll_trafograd restated with the reference's
+    Householder rrules and the analytic derivatives of the elementwise formulas) against central differences of
+    the oracle's own loss, on a flow of every transform (chained and single reflections); its loss equals
+    mvnormal_negll of the forward flow exactly. (Zygote is third-party and absent: parity unpinned beyond this.)"""
+    from parity import rand_params
+
+    rng = np.random.default_rng(700 + D)
+    layers = [(op, rand_params(rng, op, D, np.float64, K=2 if op == 5 else 1)) for op in [0, 5, 2, 3, 1, 4, 5, 3]]
+    X = np.asfortranarray(0.8 * rng.standard_normal((D, 301)))
+    negll, g = oracle.negll_grad(layers, X)
+    Y, L = oracle.flow_apply(layers, X)
+    assert negll == oracle.mvnormal_negll(Y, L)
+    th = oracle.theta_of(layers, D)
+    assert g.shape == th.shape
+
+    def loss(theta):
+        Yt, Lt = oracle.flow_apply(_unflat(layers, theta, D), X)
+        return oracle.mvnormal_negll(Yt, Lt)
+
+    fd = np.empty_like(th)
+    for i in range(th.size):
+        h = 1e-6 * max(1.0, abs(th[i]))
+        tp, tm = th.copy(), th.copy()
+        tp[i] += h
+        tm[i] -= h
+        fd[i] = (loss(tp) - loss(tm)) / (2 * h)
+    err = np.abs(g - fd) / (np.abs(fd) + 1e-3 * np.abs(fd).max())
+    assert err.max() < 2e-6, (err.argmax(), g[err.argmax()], fd[err.argmax()])
+    # the x87 evaluation of the same reverse pass agrees to fp64 rounding
+    _, g80 = oracle.negll_grad([(op, [np.asarray(p, np.longdouble) for p in ps]) for op, ps in layers],
+                               X.astype(np.longdouble))
+    assert np.allclose(g, np.asarray(g80, np.float64), rtol=1e-10, atol=1e-12 * np.abs(g).max())
+
+
+def test_oracle_optimize_whitening_step(oracle):
+    """One optimize_whitening epoch of the oracle == manual steps: per minibatch the oracle gradient, ADAGrad
+    (acc from epsilon), then normalize! of every Householder column (src/optimize_whitening.jl:25-45,
+    householder_trafo.jl:134-146)."""
+    from parity import rand_params
+
+    rng = np.random.default_rng(77)
+    D = 2
+    layers = [(0, rand_params(rng, 0, D, np.float64)), (5, rand_params(rng, 5, D, np.float64)),
+              (2, rand_params(rng, 2, D, np.float64))]
+    X = np.asfortranarray(rng.standard_normal((D, 1003)))
+    th, acc, hist = oracle.optimize_whitening(layers, X, nbatches=4, nepochs=1, eta=0.1, epsilon=1e-8)
+    assert hist.shape == (4,)  # round(1003/4) = 251 -> 251, 251, 251, 250
+    t = oracle.theta_of(layers, D)
+    a = np.full_like(t, 1e-8)
+    for k, b0 in enumerate(range(0, 1003, 251)):
+        n, g = oracle.negll_grad(_unflat(layers, t, D), np.asfortranarray(X[:, b0:b0 + 251]))
+        assert n == hist[k]
+        a = a + g * g
+        t = t - 0.1 * g / (np.sqrt(a) + 1e-8)
+        v = t[2 * D:3 * D]
+        ss = 0.0
+        for x in v:  # (the oracle's sum of squares, in order)
+            ss += x * x
+        t[2 * D:3 * D] = v / np.sqrt(ss)
+    assert np.array_equal(th, t) and np.array_equal(acc, a)
