@@ -384,6 +384,10 @@ def main():
                          "enough sets that more than 1 GiB passes between two uses of a set (the 256 MiB Infinity "
                          "Cache then holds none of it); warm: one set (cache-resident when it is small); both: warm "
                          "then cold, value = cold; auto: both when one set is under 1 GiB, else warm (= cold by size)")
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="time the K steps as one HIP graph replay (on), or as eager launches with an event between "
+                         "launches (off); auto: the graph when one launch moves under 1 GiB (a kernel of tens of "
+                         "microseconds, shorter than the host's launch cost), eager otherwise (the headline)")
     ap.add_argument("--selftest-cpu", action="store_true",
                     help="CPU tests only: the launch / barrier / max-over-ranks harness on gloo with a CPU "
                          "stand-in step (measures nothing)")
@@ -481,8 +485,9 @@ def main():
         def step():
             Xs, Ys, Ls = sets[cur["i"] % cur["k"]]
             cur["i"] += 1
+            # (torch's current stream: the launch stream, or the capture stream inside a graph capture)
             lib.check(L.enf_flow_apply(dt_code, D, N, Xs.data_ptr(), D, Ys.data_ptr(), D, Ls.data_ptr(), 0,
-                                       arr, len(layers), sh))
+                                       arr, len(layers), torch.cuda.current_stream(dev).cuda_stream))
 
         sync = torch.cuda.synchronize
 
@@ -500,6 +505,8 @@ def main():
             if (time.perf_counter() - ts) * 1e3 >= args.settle_ms:
                 break
         settle["ms"] = round((time.perf_counter() - ts) * 1e3, 2)
+    use_graph = (not args.selftest_cpu) and (args.graph == "on" or (args.graph == "auto" and set_bytes < (1 << 30)))
+
     def timed(nsets):
         """The contract's W warmup steps and K timed steps (barrier + device sync on both sides) over nsets
         buffer sets in rotation; returns (wall s, mean kernel ms from HIP events, per-launch spread)."""
@@ -511,6 +518,32 @@ def main():
         if world > 1:
             torch.distributed.barrier()
         sync()
+        if use_graph:
+            # the K timed launches captured once as a HIP graph (on the same buffer-set rotation) and replayed once
+            # untimed, then once timed: the event pair measures the device's back-to-back launches without the
+            # host's per-call launch cost (~5-8 us per ctypes call here, more than a D = 2 kernel's own time)
+            cur["i"] = 0
+            cg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(cg):
+                for _ in range(args.steps):
+                    step()
+            cg.replay()
+            sync()
+            if world > 1:
+                torch.distributed.barrier()
+            sync()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            e0.record(stream)
+            cg.replay()
+            e1.record(stream)
+            sync()
+            if world > 1:
+                torch.distributed.barrier()
+            sync()
+            wall = time.perf_counter() - t0
+            del cg
+            return wall, e0.elapsed_time(e1) / args.steps, None
         if stream is not None:
             # HIP events on the launch stream (torch.cuda.Event on the stream the kernel is launched on), one
             # between consecutive launches: the per-launch spread besides the mean
@@ -610,6 +643,8 @@ def main():
             "ms_per_step": ms_per_step,
             "cache": cache,
             "warm": warm,
+            "timing": ("one HIP graph replay of the K launches (events around it; no host launch cost)" if use_graph
+                       else "eager launches, HIP events between consecutive launches"),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

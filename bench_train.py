@@ -219,7 +219,7 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
         B, lo, hi = plan[i % len(plan)]
         if ph is not None:
             ph[0].record(stream)
-        if fused:  # enf_whitening_step: gradient, loss, ADAGrad, re-normalisation (3 launches)
+        if fused:  # enf_whitening_step: gradient, loss, ADAGrad, re-normalisation (2 launches; 1 for one-block batches)
             if ev is not None:
                 ev[0].record(stream)
             lib.check(L.enf_whitening_step(lib.ENF_F32, D, hi - lo, X[:, lo:hi].data_ptr(), ldx, state.layers(),
@@ -318,14 +318,16 @@ def train_leg(dev, world, rank, D=32, N=10_000_000, nbatches=100, pairs=4, steps
         med = lambda xs: float(np.median(xs))
         if fused or (dp_fused and comm is not None):
             phases = {"fused_step_ms": med([e[0].elapsed_time(e[3]) for e in evp]),
-                      "launches": "enf_whitening_step: gradient kernel + slice sums + tail (3 launches)" if fused else
-                                  "enf_whitening_step_dp: gradient kernel + slice sums + RCCL all-reduce + tail"}
+                      "launches": "enf_whitening_step: gradient kernel + one reduction/update launch (a batch that fits "
+                                              "one block: a single fused launch)" if fused else
+                                  "enf_whitening_step_dp: gradient kernel + block-partial sum + RCCL all-reduce of "
+                                  "1 + nparams doubles + update"}
         else:
             phases = {"gradient_ms": med([e[0].elapsed_time(e[1]) for e in evp]),
                       "allreduce_ms": med([e[1].elapsed_time(e[2]) for e in evp]),
                       "update_ms": med([e[2].elapsed_time(e[3]) for e in evp]),
                       "step_ms": med([e[0].elapsed_time(e[3]) for e in evp]),
-                      "launches": "gradient: out.zero_ + gradient kernel + slice sums + finalize; all-reduce: RCCL; "
+                      "launches": "gradient: out.zero_ + gradient kernel + one reduction launch; all-reduce: RCCL; "
                                   "update: enf_whitening_apply (1 launch)"}
         phases["mode"] = "eager, HIP events between the phases (median over the steps)"
     negll = [float(h) for h in hist_vals]

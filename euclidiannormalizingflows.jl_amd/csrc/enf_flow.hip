@@ -105,13 +105,15 @@ struct InterpBody {
 
 // OCC: minimum waves per SIMD the register allocation must allow (launch-bounds occupancy hint).
 // PAD: the padded fragment path (a.dk = D > a.D, enf_internal.h frag_pad_dim).
-template <typename T, int D, int U, int LM, int OCC, int DBG = 0, int OPS = kOpsAll, bool PAD = false>
+// PW (round 5, D <= 2): every wave builds its own records (build_program_wave) in its own LDS slice of
+// a.img_off elements, with no block barrier.
+template <typename T, int D, int U, int LM, int OCC, int DBG = 0, int OPS = kOpsAll, bool PAD = false, bool PW = false>
 __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* stepc = reinterpret_cast<double*>(smem);
   double* ctotp = stepc + kMaxSteps;
   T* stage = reinterpret_cast<T*>(smem + kLdsScalars) + (threadIdx.x >> 6) * kStagePerWave;
-  T* rec = reinterpret_cast<T*>(smem + kLdsHeader);
+  T* rec = reinterpret_cast<T*>(smem + kLdsHeader) + (PW ? (size_t)(threadIdx.x >> 6) * a.img_off : 0);
   (void)ctotp;
   ENF_KARG_CHECK(a);
   if constexpr (DBG == 5) {  // diagnostics: nothing (the launch floor of the grid)
@@ -127,7 +129,8 @@ __global__ __launch_bounds__(256, OCC) void flow_frag_kernel(FlowArgs a) {
   // the prologue runs after the wave's first tile loads are issued (frag_stream), so the HBM latency
   // of the first tile overlaps the parameter loads and record construction
   frag_stream<T, D, U, LM, DBG >= 4 ? 0 : DBG, PAD>(a, body, [&]() {
-    body.ctot = (T)build_program<T, D, Frag<T, D>::V>(a, rec, stepc);
+    if constexpr (PW) body.ctot = (T)build_program_wave<T, Frag<T, D>::V>(a, rec);
+    else body.ctot = (T)build_program<T, D, Frag<T, D>::V>(a, rec, stepc);
   });
 }
 
@@ -341,6 +344,39 @@ static hipError_t launch_frag(const FlowArgs& a, size_t lds, hipStream_t st, con
   return hipGetLastError();
 }
 
+// D <= 2 with per-wave records (PW): the records' LDS is per wave (img_off = the elements of one copy)
+template <typename T, int D, int U, int LM, int OPS = kOpsAll>
+static hipError_t launch_frag_pw(const FlowArgs& a, size_t lds, hipStream_t st, const DeviceInfo& dev) {
+  using F = Frag<T, D>;
+  const size_t elem = sizeof(T);
+  const size_t rec_bytes = (lds - kLdsHeader + 15) / 16 * 16;
+  FlowArgs b = a;
+  b.img_off = (int32_t)(rec_bytes / elem);
+#if ENF_BOUNDS
+  b.csum = flow_args_csum(b);
+#endif
+  const size_t ldsw = kLdsHeader + 4 * rec_bytes;
+  const void* k = reinterpret_cast<const void*>(&flow_frag_kernel<T, D, U, LM, 1, 0, OPS, false, true>);
+  int64_t blocks = 0;
+  hipError_t e = frag_grid(k, a.N, (int64_t)F::COLS_PER_INSTR * U * 4, ldsw, dev, &blocks);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((flow_frag_kernel<T, D, U, LM, 1, 0, OPS, false, true>), dim3((unsigned)blocks), dim3(256), ldsw,
+                     st, b);
+  return hipGetLastError();
+}
+
+// the per-wave prologue applies: D <= 2, one lane per (step, row). Measured and NOT taken (round 5, diagnostics
+// knob ENF_SMALL_PW=1): at D = 2, N = 1e6, fp64 the kernel times under rocprofv3 were J o C 21.7 vs 20.4 us, K o H o S
+// 18.6 vs 17.8, J 14.5 vs 13.3, S 9.9 vs 9.9 with the block prologue (profiles/r05/d2_small_pw_ab.txt): the
+// per-lane parameter loads and logs of every wave cost more than the block barrier saves.
+static bool pw_eligible(const FlowArgs& a) {
+  static const int pw = ENF_KNOB("ENF_SMALL_PW", 0);
+  if (!pw || a.dk || a.wy || (a.D != 1 && a.D != 2) || a.nsteps * a.D > 64) return false;
+  for (int s = 0; s < a.nsteps; ++s)
+    if (a.steps[s].op == OP_DENSE) return false;
+  return true;
+}
+
 // The padded fragment path (a.dk = the power-of-two layout of a.D rows): every op has neutral
 // parameters that map 0 to 0 with ladj 0 (enf_steps.h neutral_values).
 constexpr int kOpsPad = kOpsAll;
@@ -437,6 +473,11 @@ static hipError_t dispatch_D(const FlowArgs& a, size_t lds, hipStream_t st, cons
     if (fdbg == 5) return launch_frag<T, 2, 4, LADJ, 1, 5, kOpsHJ>(a, lds, st, dev);
   }
 #endif
+  if (pw_eligible(a)) {  // D <= 2: per-wave records, no block barrier (round 5)
+    if ((flow_ops(a) & ~kOpsHJ) == 0)
+      return a.D == 1 ? launch_frag_pw<T, 1, 4, LADJ, kOpsHJ>(a, lds, st, dev) : launch_frag_pw<T, 2, 4, LADJ, kOpsHJ>(a, lds, st, dev);
+    return a.D == 1 ? launch_frag_pw<T, 1, 4, LADJ>(a, lds, st, dev) : launch_frag_pw<T, 2, 4, LADJ>(a, lds, st, dev);
+  }
   if ((flow_ops(a) & ~kOpsHJ) == 0) {  // reflections and Johnson layers only (configs 2-5)
 #if ENF_DIAG
     static const int hju = ENF_KNOB("ENF_FRAG_HJU", 4);

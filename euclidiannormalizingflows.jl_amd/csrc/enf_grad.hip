@@ -65,6 +65,7 @@ struct GradArgs {
   const void* dl;
   void* dX;
   int64_t lddx;
+  int32_t diag_ts;  // diagnostics build (ENF_SMALL_TS): the one-block step's thread 0 prints its phase clocks
 };
 
 // values per lane of the generic gradient kernel at kernel rows D: a 16-byte fragment, or D/64 rows
@@ -229,8 +230,11 @@ __device__ __forceinline__ T bwd_elem(int op, T x, T g, const T* p, T* dp, T cl)
   }
 }
 
-template <typename T, int D, bool VJP>
-__global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
+// STEP (round 5): the single-block fused optimize_whitening step -- the grid is one block, and instead of writing
+// its partial row the block sums its waves into LDS and runs the update itself (block_step_update): one launch per
+// minibatch step where the two-launch path costs two kernel boundaries (the examples' B = 100 / 1000 steps).
+template <typename T, int D, bool VJP, bool STEP = false>
+__device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceArgs* rs, const StepArgs* ss) {
   // values per lane: one 16-byte fragment, or D/64 rows when a column needs more than 64 fragments (round 4:
   // kernel rows up to 1024, a column then spans the whole wave)
   constexpr int V = grad_lane_values<T>(D);
@@ -239,8 +243,8 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
   constexpr int SEG = D >= V ? V : D;
   constexpr int COLS = 64 / G * CPF;  // columns per wave tile (one fragment per lane)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // LDS: [grad accumulators: nw waves x nparams doubles][loss: nw (<= 4) waves x double][records][activations]
-  // (nw = blockDim.x / 64: 4, or fewer when D > 64 makes the per-wave accumulators large)
+  // LDS: [grad accumulators: nw waves x nparams doubles][loss: nw (<= 8) waves x double][records][activations]
+  // (nw = blockDim.x / 64: 4, fewer when D > 64 makes the per-wave accumulators large, 8 for a one-block batch)
   const int nw = blockDim.x >> 6;
   const int gbytes = ((a.nparams * 8 + 15) / 16) * 16;
   double* gacc = reinterpret_cast<double*>(smem + (threadIdx.x >> 6) * gbytes);  // this wave's
@@ -251,6 +255,9 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
   T* act = rec + ((nrec + 3) / 4) * 4 + (threadIdx.x >> 6) * (a.nsteps * 64 * V);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#if ENF_DIAG
+  const long long ts0 = STEP && a.diag_ts ? (long long)clock64() : 0;
+#endif
   for (int i = lane; i < a.nparams; i += 64) gacc[i] = 0.0;
   // raw parameter records, layout [group][param][element] as the forward kernel (RV = V)
   for (int s = 0; s < a.nsteps; ++s) {
@@ -285,6 +292,9 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
     }
   }
   __syncthreads();
+#if ENF_DIAG
+  const long long ts1 = STEP && a.diag_ts ? (long long)clock64() : 0;
+#endif
 
   const int r0 = D >= V ? V * (lane % G) : 0;
   const int grp = D >= V ? lane % G : 0;
@@ -417,9 +427,45 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
     }
   }
   // ---- block partials
+#if ENF_DIAG
+  const long long ts2 = STEP && a.diag_ts ? (long long)clock64() : 0;
+#endif
   for (int m = 32; m >= 1; m >>= 1) lossp += __shfl_xor(lossp, m);
   if (lane == 0) lossw[wave] = lossp;
   __syncthreads();
+  if constexpr (STEP) {
+    // the block's row into LDS past the activations (the same sums as the row below), then the update
+    const size_t act_end = reinterpret_cast<size_t>(rec + ((nrec + 3) / 4) * 4 + nw * (a.nsteps * 64 * V));
+    double* tot = reinterpret_cast<double*>((act_end + 15) / 16 * 16);
+    unsigned char* scratch = reinterpret_cast<unsigned char*>(tot + ((1 + a.nparams + 1) / 2) * 2);
+    if (tid == 0) {
+      double l = lossw[0];
+      for (int w = 1; w < nw; ++w) l += lossw[w];
+      tot[0] = l;
+    }
+    const double* g0 = reinterpret_cast<const double*>(smem);
+    const int w8 = gbytes / 8;
+    for (int i = tid; i < a.nparams; i += blockDim.x) {
+      double v = g0[i];
+      for (int w = 1; w < nw; ++w) v += g0[w * w8 + i];
+      tot[1 + i] = v;
+    }
+    __syncthreads();
+#if ENF_DIAG
+    const long long ts3 = a.diag_ts ? (long long)clock64() : 0;
+#endif
+    block_step_update<T>(tot, a.nparams, a.D, *rs, *ss, scratch);
+#if ENF_DIAG
+    if (a.diag_ts) {  // (uniform)
+      __syncthreads();
+      const long long ts4 = (long long)clock64();
+      if (tid == 0)
+        printf("ENF_SMALL_TS prologue %lld tiles %lld partials %lld update %lld (shader clocks)\n", ts1 - ts0,
+               ts2 - ts1, ts3 - ts2, ts4 - ts3);
+    }
+#endif
+    return;
+  }
   if (!a.partial) return;  // enf_flow_vjp without parameter cotangents
   double* out = (double*)a.partial + (int64_t)blockIdx.x * (1 + a.nparams);
   if (tid == 0) {  // the waves' values in wave order (deterministic)
@@ -435,6 +481,17 @@ __global__ __launch_bounds__(256) void negll_grad_kernel(GradArgs a) {
     out[1 + i] = v;
   }
 }
+
+template <typename T, int D, bool VJP>
+__global__ __launch_bounds__(512) void negll_grad_kernel(GradArgs a) {
+  negll_grad_impl<T, D, VJP, false>(a, nullptr, nullptr);
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(512) void whitening_step_small_kernel(GradArgs a, ReduceArgs r, StepArgs s) {
+  negll_grad_impl<T, D, false, true>(a, &r, &s);
+}
+static_assert(sizeof(GradArgs) + sizeof(ReduceArgs) + sizeof(StepArgs) <= 4096, "kernel arguments over 4 KB");
 
 // The update half of a data-parallel step (enf_whitening_apply): the same loss / ADAGrad /
 // re-normalisation as whitening_tail_kernel, reading the cross-rank sum g (1 + nparams values of T,
@@ -459,10 +516,13 @@ __global__ __launch_bounds__(256) void whitening_apply_kernel(const T* __restric
 // ---------------------------------------------------------------------------------------------
 namespace {
 
+constexpr int kSmallMaxWaves = 8;  // the generic kernels' blocks have 4 waves, or 8 for a one-block batch
+
 struct Plan {
   GradArgs ga;
   ReduceArgs ra;
   size_t lds = 0;
+  size_t small_lds = 0;  // the single-block fused step's LDS (lds + the block's row and the update's scratch)
   int blocks = 0;   // blocks (partial rows) of the generic kernel
   int ws_rows = 0;  // partial rows the workspace reserves: the generic kernel's or the fused (J o H)^n kernel's
   int nw = 4;  // waves per block of the generic kernel
@@ -533,7 +593,17 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
   P.lds = P.nw * (gbytes + abytes) + 64 + rbytes;  // generic kernel; checked where it is launched
   const int cols = (int)(64 / (Dp >= V ? Dp / V : 1) * (Dp >= V ? 1 : V / Dp));
   const int64_t tiles = (N + cols - 1) / cols;
+  // a batch of at most kSmallMaxWaves tiles runs as ONE block with one tile per wave (8 waves when their LDS
+  // fits): one partial row, and the single-rank step then runs its update in the same launch (round 5). Two
+  // tiles per wave in one block lost to two blocks: a tile of an fp64 flow is a long dependent chain (the 1d
+  // example's J o K o J o K, B = 1000: 16.4k against 26.8k steps/s, profiles/r05/example_1d_v2.json)
+  if (tiles > P.nw && tiles <= kSmallMaxWaves && P.nw == 4 &&
+      (size_t)kSmallMaxWaves * (gbytes + abytes) + 64 + rbytes <= kGradLdsMax) {
+    P.nw = kSmallMaxWaves;
+    P.lds = P.nw * (gbytes + abytes) + 64 + rbytes;
+  }
   int64_t blocks = (tiles + P.nw - 1) / P.nw;
+  P.small_lds = P.lds + 16 + ((size_t)goff + 2) * 8 + (size_t)goff * (8 + 2 * esz + 4) + 16;
   DeviceInfo dev;
   if (current_device_info(&dev) != ENF_OK) return ENF_ERR_HIP;
   // blocks per CU (2: what the fused kernel's LDS lets stay resident; measured best at config 5)
@@ -552,8 +622,37 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
   return ENF_OK;
 }
 
+#if ENF_DIAG
+// diagnostics (ENF_RED_DBG): the reduction's launch floor -- 1: the same grid and arguments, returning at once;
+// 2: one dependent round trip (the loss row's first value to loss_out / tot)
+template <typename T, int MODE, int KIND>
+__global__ __launch_bounds__(kRedThreads) void reduce_probe_kernel(ReduceArgs r, StepArgs s) {
+  if (KIND == 2 && blockIdx.x == 0 && threadIdx.x == 0) {
+    if (MODE == MODE_STEP) *s.loss_out = r.partial[0];
+    else if (MODE == MODE_SUM) r.tot[0] = r.partial[0];
+  }
+}
+// 3: the same grid with an 8-byte argument (does the ~2 KB argument block cost launch time?)
+__global__ __launch_bounds__(kRedThreads) void reduce_probe_small_kernel(double* p) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && p) p[0] = 0.0;
+}
+#endif
+
 template <typename T, int MODE>
 hipError_t launch_reduce(const ReduceArgs& r, const StepArgs& s, hipStream_t st) {
+#if ENF_DIAG
+  static const int dbg = ENF_KNOB("ENF_RED_DBG", 0);
+  if (dbg == 3) {
+    hipLaunchKernelGGL(reduce_probe_small_kernel, dim3(reduce_grid(r.D, r.nparams)), dim3(kRedThreads), 0, st,
+                       (double*)nullptr);
+    return hipGetLastError();
+  }
+  if (dbg == 1 || dbg == 2) {
+    if (dbg == 1) hipLaunchKernelGGL((reduce_probe_kernel<T, MODE, 1>), dim3(reduce_grid(r.D, r.nparams)), dim3(kRedThreads), 0, st, r, s);
+    else hipLaunchKernelGGL((reduce_probe_kernel<T, MODE, 2>), dim3(reduce_grid(r.D, r.nparams)), dim3(kRedThreads), 0, st, r, s);
+    return hipGetLastError();
+  }
+#endif
   hipLaunchKernelGGL((grad_reduce_kernel<T, MODE>), dim3(reduce_grid(r.D, r.nparams)), dim3(kRedThreads), 0, st, r, s);
   return hipGetLastError();
 }
@@ -583,6 +682,36 @@ hipError_t launch_grad_D(const Plan& P, hipStream_t st) {
   }
   hipLaunchKernelGGL((negll_grad_kernel<T, DD, VJP>), dim3(P.blocks), dim3(64 * P.nw), P.lds, st, P.ga);
   return hipGetLastError();
+}
+
+template <typename T, int DD>
+hipError_t launch_step_small_D(const Plan& P, const StepArgs& sa, hipStream_t st) {
+  if (P.small_lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)whitening_step_small_kernel<T, DD>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.small_lds);
+    if (e != hipSuccess) return e;
+  }
+#if ENF_DIAG
+  static const int ts = ENF_KNOB("ENF_SMALL_TS", 0);
+  if (ts) {
+    GradArgs ga = P.ga;
+    ga.diag_ts = 1;
+    hipLaunchKernelGGL((whitening_step_small_kernel<T, DD>), dim3(1), dim3(64 * P.nw), P.small_lds, st, ga, P.ra, sa);
+    return hipGetLastError();
+  }
+#endif
+  hipLaunchKernelGGL((whitening_step_small_kernel<T, DD>), dim3(1), dim3(64 * P.nw), P.small_lds, st, P.ga, P.ra, sa);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_step_small(const Plan& P, const StepArgs& sa, hipStream_t st) {
+  switch (P.ga.Dp) {
+#define ENF_S(DD) case DD: return launch_step_small_D<T, DD>(P, sa, st);
+    ENF_S(1) ENF_S(2) ENF_S(4) ENF_S(8) ENF_S(16) ENF_S(32) ENF_S(64) ENF_S(128) ENF_S(256) ENF_S(512) ENF_S(1024)
+#undef ENF_S
+    default: return hipErrorInvalidValue;
+  }
 }
 
 template <typename T, bool VJP = false>
@@ -763,6 +892,16 @@ enf_status whitening_step_single(bool f64, int64_t D, int64_t N, const void* X, 
       return set_error(ENF_ERR_INVALID, "enf_whitening_step: Householder batch columns must start at multiples of D");
   }
   const size_t n1 = 1 + (size_t)P.ga.nparams;
+  // one rank, a batch of one block, not the fused (J o H)^n kernel: gradient and update in ONE launch (round 5)
+  static const int small_ok = ENF_KNOB("ENF_STEP_SMALL", 1);
+  if (small_ok && !ar && N > 0 && P.blocks == 1 && P.small_lds <= kGradLdsMax &&
+      (f64 || !hj_grad_eligible(D, ldx, X, layers, nlayers))) {
+    P.ga.X = X;
+    P.ga.ldx = ldx;
+    P.ga.partial = nullptr;
+    hipError_t e = f64 ? launch_step_small<double>(P, a, st) : launch_step_small<float>(P, a, st);
+    return e == hipSuccess ? ENF_OK : set_error(ENF_ERR_HIP, hipGetErrorString(e));
+  }
   if (N > 0) {
     s = grad_parts(f64, D, N, X, ldx, layers, nlayers, workspace, workspace_bytes, st, P);
     if (s != ENF_OK) return s;

@@ -426,7 +426,9 @@ __device__ __forceinline__ void grad_load_reg(const HJGradArgs& a, int64_t col0,
   }
 }
 
-template <int D, int V, int KU, int NP, bool TAIL>
+// RC (recompute): the backward re-derives sqrt(1 + z^2) and asinh(z) from z instead of keeping them from the
+// forward (2 V KU NP fewer VGPRs, two transcendentals and the asinh merge more per element-pair)
+template <int D, int V, int KU, int NP, bool TAIL, bool RC = false>
 __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0, int lane, const float* __restrict__ rec,
                                               const float (&xin)[KU][V], float (&acc)[NP][5][V], double& lossp,
                                               int& nvalid) {
@@ -443,7 +445,8 @@ __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0,
     for (int e = 0; e < V; ++e) x[u][e] = xin[u][e];
   }
   float zs[NP][KU][V], ds[NP][KU];
-  float ss[NP][KU][V], ls[NP][KU][V];  // sqrt(1 + z^2) and asinh(z)/ln2 of the forward, for the backward
+  // sqrt(1 + z^2) and asinh(z)/ln2 of the forward, for the backward (RC: not kept)
+  float ss[RC ? 1 : NP][KU][V], ls[RC ? 1 : NP][KU][V];
   float lad[KU] = {};
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
@@ -468,9 +471,13 @@ __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0,
       for (int e = 0; e < V; ++e) {
         zs[p][u][e] = fmaf(fmaf(-ds[p][u], vh[e], x[u][e]), il[e], nxil[e]);
         q[e] = fmaf(zs[p][u][e], zs[p][u][e], 1.f);
-        ss[p][u][e] = hw_sqrt(q[e]);
-        ls[p][u][e] = asinh2_f32(zs[p][u][e], q[e], ss[p][u][e], csign);
-        x[u][e] = fmaf(dl2[e], ls[p][u][e], gam[e]);
+        const float sq = hw_sqrt(q[e]);
+        const float lz = asinh2_f32(zs[p][u][e], q[e], sq, csign);
+        if constexpr (!RC) {
+          ss[p][u][e] = sq;
+          ls[p][u][e] = lz;
+        }
+        x[u][e] = fmaf(dl2[e], lz, gam[e]);
       }
       lad[u] = fmaf(-0.5f, hw_log2(prod_rows<V>(q)), lad[u]);
     }
@@ -506,9 +513,18 @@ __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0,
     for (int u = 0; u < KU; ++u) {
 #pragma unroll
       for (int e = 0; e < V; ++e) {
-        const float z = zs[p][u][e];
-        const float rs = hw_rcp(ss[p][u][e]);
-        const float Lz = ls[p][u][e];
+        float z = zs[p][u][e];
+        float sq, Lz;
+        if constexpr (RC) {
+          asm volatile("" : "+v"(z));  // an opaque copy: the compiler would otherwise reuse the forward's values
+          const float q = fmaf(z, z, 1.f);
+          sq = hw_sqrt(q);
+          Lz = asinh2_f32(z, q, sq, csign);
+        } else {
+          sq = ss[p][u][e];
+          Lz = ls[p][u][e];
+        }
+        const float rs = hw_rcp(sq);
         acc[p][1][e] += g[u][e];
         acc[p][2][e] = fmaf(g[u][e], Lz, acc[p][2][e]);
         const float dz = fmaf(g[u][e] * del[e], rs, z * (rs * rs) * vm[u]);
@@ -533,7 +549,7 @@ __device__ __forceinline__ void grad_tile_reg(const HJGradArgs& a, int64_t col0,
   }
 }
 
-template <int D, int V, int KU, int NP, int W>
+template <int D, int V, int KU, int NP, int W, bool RC = false>
 __global__ __launch_bounds__(64 * W) void hj_grad_reg_kernel(HJGradArgs a) {
   using L = GL<D, V, KU>;
   constexpr int G = L::G;
@@ -567,8 +583,8 @@ __global__ __launch_bounds__(64 * W) void hj_grad_reg_kernel(HJGradArgs a) {
   const int64_t stride = (int64_t)(gridDim.x - 1) * W;
   for (int64_t t = wave_id; t < ntiles; t += stride) {
     if (t + stride < ntiles) grad_load_reg<D, V, KU>(a, (t + stride) * L::TC, lane, xn);
-    if (t < full) grad_tile_reg<D, V, KU, NP, false>(a, t * L::TC, lane, rec, xc, acc, lossp, nvalid);
-    else grad_tile_reg<D, V, KU, NP, true>(a, t * L::TC, lane, rec, xc, acc, lossp, nvalid);
+    if (t < full) grad_tile_reg<D, V, KU, NP, false, RC>(a, t * L::TC, lane, rec, xc, acc, lossp, nvalid);
+    else grad_tile_reg<D, V, KU, NP, true, RC>(a, t * L::TC, lane, rec, xc, acc, lossp, nvalid);
 #pragma unroll
     for (int u = 0; u < KU; ++u)
 #pragma unroll
@@ -600,29 +616,33 @@ size_t hj_grad_lds(int n) {
 }
 
 // ---- variant table: (V rows per lane, KU fragments per tile, W waves per block) of the register kernel.
-// The product uses kProd; the diagnostics build can select the others (ENF_HJG_VARIANT) for A/B runs.
+// The product uses 0 or 1 by batch size (product_variant); the diagnostics build can force any (ENF_HJG_VARIANT).
 struct RegVariant {
-  int V, KU, W;
+  int V, KU, W, RC;
 };
 constexpr RegVariant kRegVariants[] = {
-    {2, 2, 8},   // 0: the product (round 5)
-    {4, 1, 4},   // 1: round 4's kernel shape (16-byte fragments, 4 waves per block)
-    {4, 1, 8},   // 2
-    {2, 2, 4},   // 3
-    {1, 2, 8},   // 4
-    {1, 2, 16},  // 5
-    {2, 1, 8},   // 6
+    {2, 2, 8, 0},   // 0: the product (round 5) up to kLargeBatch columns
+    {4, 1, 4, 0},   // 1: round 4's kernel shape (16-byte fragments, 4 waves per block): the product above it
+    {4, 1, 8, 0},   // 2
+    {2, 2, 4, 0},   // 3
+    {1, 2, 8, 0},   // 4
+    {1, 2, 16, 0},  // 5
+    {2, 1, 8, 0},   // 6
+    {2, 2, 4, 1},   // 7: recomputing sqrt / asinh in the backward (fewer registers, more waves)
+    {2, 2, 8, 1},   // 8
+    {4, 1, 4, 1},   // 9
 };
 constexpr int kNumRegVariants = ENF_DIAG ? (int)(sizeof(kRegVariants) / sizeof(kRegVariants[0])) : 1;
+constexpr int kLargeVariant = 1;  // the product's shape for large batches (product_variant)
 
 int reg_variant() {
   static const int v = ENF_KNOB("ENF_HJG_VARIANT", 0);
   return (v >= 0 && v < kNumRegVariants) ? v : 0;
 }
 
-template <int D, int V, int KU, int NP, int W>
+template <int D, int V, int KU, int NP, int W, bool RC>
 const void* reg_kernel_ptr() {
-  return reinterpret_cast<const void*>(&hj_grad_reg_kernel<D, V, KU, NP, W>);
+  return reinterpret_cast<const void*>(&hj_grad_reg_kernel<D, V, KU, NP, W, RC>);
 }
 
 // (kernel, LDS bytes, columns per wave tile, waves per block) of the register kernel for (D, n pairs, variant)
@@ -632,16 +652,16 @@ struct KSel {
   int tc = 0, w = 0;
 };
 
-template <int D, int V, int KU, int W>
+template <int D, int V, int KU, int W, bool RC = false>
 KSel sel_np(int n) {
   KSel s;
   s.tc = GL<D, V, KU>::TC;
   s.w = W;
   switch (n) {
-    case 1: s.k = reg_kernel_ptr<D, V, KU, 1, W>(); s.lds = hj_grad_reg_lds<D, 1, W>(); break;
-    case 2: s.k = reg_kernel_ptr<D, V, KU, 2, W>(); s.lds = hj_grad_reg_lds<D, 2, W>(); break;
-    case 3: s.k = reg_kernel_ptr<D, V, KU, 3, W>(); s.lds = hj_grad_reg_lds<D, 3, W>(); break;
-    default: s.k = reg_kernel_ptr<D, V, KU, 4, W>(); s.lds = hj_grad_reg_lds<D, 4, W>(); break;
+    case 1: s.k = reg_kernel_ptr<D, V, KU, 1, W, RC>(); s.lds = hj_grad_reg_lds<D, 1, W>(); break;
+    case 2: s.k = reg_kernel_ptr<D, V, KU, 2, W, RC>(); s.lds = hj_grad_reg_lds<D, 2, W>(); break;
+    case 3: s.k = reg_kernel_ptr<D, V, KU, 3, W, RC>(); s.lds = hj_grad_reg_lds<D, 3, W>(); break;
+    default: s.k = reg_kernel_ptr<D, V, KU, 4, W, RC>(); s.lds = hj_grad_reg_lds<D, 4, W>(); break;
   }
   return s;
 }
@@ -650,19 +670,31 @@ template <int D>
 KSel select_reg(int n, int variant) {
   switch (variant) {
 #if ENF_DIAG
-    case 1: return sel_np<D, 4, 1, 4>(n);
     case 2: return sel_np<D, 4, 1, 8>(n);
     case 3: return sel_np<D, 2, 2, 4>(n);
     case 4: return sel_np<D, 1, 2, 8>(n);
     case 5: return sel_np<D, 1, 2, 16>(n);
     case 6: return sel_np<D, 2, 1, 8>(n);
+    case 7: return sel_np<D, 2, 2, 4, true>(n);
+    case 8: return sel_np<D, 2, 2, 8, true>(n);
+    case 9: return sel_np<D, 4, 1, 4, true>(n);
 #endif
+    case kLargeVariant: return sel_np<D, 4, 1, 4>(n);
     default: return sel_np<D, 2, 2, 8>(n);
   }
 }
 
-KSel select_kernel(int64_t D, int n) {
-  if (n <= 4) return D == 32 ? select_reg<32>(n, reg_variant()) : select_reg<64>(n, reg_variant());
+// The product's register kernel by batch size: {2, 2, 8} up to kLargeBatch columns (the 8-rank share of config 5,
+// 12 500 columns: 21.3 us per step against 26.6 for {4, 1, 4}), {4, 1, 4} above (B = 1e5: 39.4 against 41.2 us;
+// profiles/r05/c5_variants_v3.jsonl). The crossover between the two measured sizes is not measured.
+constexpr int64_t kLargeBatch = 50000;
+int product_variant(int64_t N) {
+  const int v = reg_variant();
+  return v != 0 ? v : (N >= kLargeBatch ? kLargeVariant : 0);
+}
+
+KSel select_kernel(int64_t D, int n, int64_t N) {
+  if (n <= 4) return D == 32 ? select_reg<32>(n, product_variant(N)) : select_reg<64>(n, product_variant(N));
   static const int ku = ENF_KNOB("ENF_GRAD_U", 2) == 1 ? 1 : 2;  // 2: measured 72 vs 93 us at config 5
   KSel s;
   s.w = 4;
@@ -709,7 +741,7 @@ bool hj_grad_eligible(int64_t D, int64_t ldx, const void* X, const enf_layer* la
   return ldx == D && (((uintptr_t)X) & 15) == 0 && hj_grad_shape_ok(D, layers, nlayers);
 }
 
-int hj_grad_blocks(int64_t D, int64_t N, int32_t npairs) { return blocks_for(select_kernel(D, npairs), N); }
+int hj_grad_blocks(int64_t D, int64_t N, int32_t npairs) { return blocks_for(select_kernel(D, npairs, N), N); }
 
 hipError_t launch_hj_grad(int64_t D, int64_t N, const void* X, const enf_layer* layers, int32_t nlayers,
                           int32_t nparams, double* partial, double* ctot_out, int* nblocks, hipStream_t st) {
@@ -737,7 +769,7 @@ hipError_t launch_hj_grad(int64_t D, int64_t N, const void* X, const enf_layer* 
     off += 4 * (int32_t)D;
   }
   if (off != nparams) return hipErrorInvalidValue;
-  const KSel s = select_kernel(D, a.n);
+  const KSel s = select_kernel(D, a.n, N);
   const int blocks = blocks_for(s, N);
   *nblocks = blocks;
   if (s.lds > 64 * 1024) {

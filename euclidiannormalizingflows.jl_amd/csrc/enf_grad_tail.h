@@ -162,6 +162,54 @@ __device__ __forceinline__ void normalize_lds(T* __restrict__ v, int D, int lane
   for (int d = lane; d < D; d += 64) v[d] *= inv;
 }
 
+// The update of a whole flow by ONE block (the single-block fused step, round 5): tot (LDS: 1 + np doubles, the
+// block's loss and gradient sums) -> loss, Householder projection, ADAGrad, re-normalisation -- the operations and
+// roundings of grad_reduce_kernel's MODE_STEP over one partial row, so the one-launch and the two-launch steps agree
+// bit for bit. scratch (LDS, 16-byte aligned): np doubles + 2 np T + np ints.
+template <typename T>
+__device__ void block_step_update(double* __restrict__ tot, int64_t np, int D, const ReduceArgs& r, const StepArgs& s,
+                                  unsigned char* __restrict__ scratch) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6, NT = blockDim.x;
+  double* vcol = reinterpret_cast<double*>(scratch);
+  T* thl = reinterpret_cast<T*>(vcol + np);
+  T* acl = thl + np;
+  int* flags = reinterpret_cast<int*>(acl + np);
+  double* gl = tot + 1;
+  if (tid == 0) *s.loss_out = (double)((T)tot[0] / (T)s.nsamp);
+  for (int64_t i = tid; i < np; i += NT) {
+    const int64_t uo = (i / D) * D;
+    const int h = unit_householder(r, uo);
+    vcol[i] = h >= 0 ? (double)((const T*)r.hcol[h])[i % D] : 0.0;
+    int f = 0;
+    for (int q = 0; q < s.nruns; ++q) f |= (i >= s.runs[q][0] && i < s.runs[q][1]) ? 1 : 0;
+    for (int q = 0; q < s.nhb; ++q) {
+      const int64_t rel = uo - s.hb[q][0];
+      if (rel >= 0 && rel % s.hb[q][2] == 0 && rel / s.hb[q][2] < s.hb[q][1]) f |= 2;
+    }
+    flags[i] = f;
+    thl[i] = f ? ((const T*)s.theta)[i] : (T)0;
+    acl[i] = (f & 1) ? ((const T*)s.acc)[i] : (T)0;
+  }
+  __syncthreads();
+  const int64_t units = np / D;
+  for (int64_t u = wave; u < units; u += nw)
+    if (unit_householder(r, u * D) >= 0) project_column(gl + u * D, vcol + u * D, D, lane);  // wave-uniform
+  __syncthreads();
+  for (int64_t i = tid; i < np; i += NT)
+    if (flags[i] & 1) adagrad_update<T>(thl[i], acl[i], (T)gl[i], (T)s.scale, (T)s.eta, (T)s.eps);
+  __syncthreads();
+  for (int64_t u = wave; u < units; u += nw)
+    if (flags[u * D] & 2) normalize_lds<T>(thl + u * D, D, lane);  // wave-uniform
+  __syncthreads();
+  T* th = (T*)s.theta;
+  T* ac = (T*)s.acc;
+  for (int64_t i = tid; i < np; i += NT) {
+    const int f = flags[i];
+    if (f) th[i] = thl[i];
+    if (f & 1) ac[i] = acl[i];
+  }
+}
+
 template <typename T, int MODE>
 __global__ __launch_bounds__(kRedThreads) void grad_reduce_kernel(ReduceArgs r, StepArgs s) {
   __shared__ double red[kRedThreads];

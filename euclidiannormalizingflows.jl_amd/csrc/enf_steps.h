@@ -184,6 +184,56 @@ __device__ double build_program(const FlowArgs& a, T* __restrict__ rec, double* 
   return c;
 }
 
+// Per-wave prologue of the small-D fragment kernels (round 5; D <= 2 and nsteps * D <= 64): the same records and
+// the same constant as build_program, built by ONE wave into its own LDS slice with no block barrier -- lane
+// s * D + d handles row d of step s (its parameter loads, the double logs, the reflection's v'v over the D
+// adjacent lanes) -- so no wave waits for the others, and the steps' global round trips overlap instead of
+// running one step per wave. The fp64 log table is written by every wave (the same values to the same
+// addresses: no barrier needed either).
+template <typename T, int RV>
+__device__ double build_program_wave(const FlowArgs& a, T* __restrict__ rec) {
+  const int lane = threadIdx.x & 63;
+  const int D = a.D;  // 1 or 2 (no padded layout here)
+  if constexpr (std::is_same_v<T, double>)
+    for (int i = lane; i < 3 * kLogTabN; i += 64) g_logtab[i] = kLogTab[i];
+  const int s = lane / D, d = lane % D;
+  const bool live = s < a.nsteps;
+  const Step st = a.steps[live ? s : 0];
+  const LayerDesc& L = a.layers[st.layer];
+  double part = 0.0;
+  if (live) {
+    if (st.op == OP_HOUSEHOLDER) {
+      const double v = (double)((const T*)L.p[0])[(int64_t)st.col * D + d];
+      part = v * v;
+    } else if (st.op == OP_SCALESHIFT) {
+      if (L.k != 1 || d == 0) part = log(fabs((double)((const T*)L.p[0])[d]));
+    } else if (st.op == OP_JOHNSON || st.op == OP_JOHNSON_INV) {
+      const double c = log(fabs((double)((const T*)L.p[1])[d])) - log(fabs((double)((const T*)L.p[3])[d]));
+      part = st.op == OP_JOHNSON ? c : -c;
+    }
+  }
+  if (D == 2) part += __shfl_xor(part, 1);  // the step's two rows, as build_program's one butterfly stage
+  const double hscale = (live && st.op == OP_HOUSEHOLDER) ? sqrt(2.0 / part) : 0.0;
+  if (live && st.op != OP_DENSE) {
+    const int W = record_width(st.op);
+    T* r = rec + st.off;
+    T vals[8];
+    param_values<T>(st.op, L, st.col, D, d, hscale, vals);
+    for (int e = d; e < RV; e += D)  // D < RV: the row's value fills every element e with e % D == d
+      for (int q = 0; q < W; ++q) r[q * RV + e] = vals[q];
+  }
+  const double cs = (live && (st.op == OP_SCALESHIFT || st.op == OP_JOHNSON || st.op == OP_JOHNSON_INV)) ? part : 0.0;
+  // the constants summed in step order (lane s * D holds step s's): uniform loop of readlanes
+  double c = 0.0;
+  for (int k = 0; k < a.nsteps; ++k) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, cs);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, k * D), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), k * D);
+    c += __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's LDS writes land before its reads
+  __builtin_amdgcn_wave_barrier();
+  return c;
+}
 
 // y = x - vh (vh'x), vh = v*sqrt(2/v'v): householder_trafo!(y, v, x) (householder_trafo.jl:8-11)
 template <typename T, int D, int U>

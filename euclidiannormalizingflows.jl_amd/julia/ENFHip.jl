@@ -465,7 +465,10 @@ function optimize_whitening(smpls::HipMatrix{T}, initial_trafo::Function, optimi
     np = length(host)
     out = HipMatrix{R}(1 + np, 1)
     zero_out = zeros(R, 1 + np, 1)
-    fused = world == 1 && isempty(tied)
+    # the one-launch update takes at most 64 trainable runs and 16 Householder batches (enf_whitening_step /
+    # _step_dp / _apply: ENF_ERR_UNSUPPORTED beyond); past that the update runs as the separate calls
+    limits_ok = length(runs) ÷ 2 <= 64 && length(hb) ÷ 3 <= 16
+    fused = world == 1 && isempty(tied) && limits_ok
     s = 0
     GC.@preserve X theta acc layers runs hb ws hist out zero_out begin
         for _ in 1:nepochs, b0 in starts
@@ -480,7 +483,7 @@ function optimize_whitening(smpls::HipMatrix{T}, initial_trafo::Function, optimi
                             _dt(R), D, B, X.buf.ptr + b0 * D * sizeof(R), D, layers, length(layers), theta.buf.ptr,
                             acc.buf.ptr, runs, length(runs) ÷ 2, hb, length(hb) ÷ 3, rule.eta, rule.epsilon,
                             loss_ptr, ws.ptr, ws.bytes, C_NULL))
-            elseif isempty(tied)  # data-parallel: gradient, RCCL sum of the slice totals, tail (enf_whitening_step_dp)
+            elseif isempty(tied) && limits_ok  # data-parallel: gradient, RCCL sum of the rank's totals, update (enf_whitening_step_dp)
                 check(ccall((:enf_whitening_step_dp, libenf), Cint,
                             (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Ptr{EnfLayer}, Int32, Ptr{Cvoid}, Ptr{Cvoid},
                              Ptr{Int64}, Int32, Ptr{Int64}, Int32, Cdouble, Cdouble, Int64, Ptr{Cdouble}, Ptr{Cvoid},
@@ -499,11 +502,29 @@ function optimize_whitening(smpls::HipMatrix{T}, initial_trafo::Function, optimi
                     end
                     GC.@preserve g _memcpy(out.buf.ptr, Ptr{Cvoid}(pointer(g)), sizeof(g), MEMCPY_H2D)
                 end
-                check(ccall((:enf_whitening_apply, libenf), Cint,
-                            (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Int64}, Int32,
-                             Ptr{Int64}, Int32, Cdouble, Cdouble, Ptr{Cdouble}, Ptr{Cvoid}),
-                            _dt(R), D, np, out.buf.ptr, B, theta.buf.ptr, acc.buf.ptr, runs, length(runs) ÷ 2,
-                            hb, length(hb) ÷ 3, rule.eta, rule.epsilon, loss_ptr, C_NULL))
+                if limits_ok
+                    check(ccall((:enf_whitening_apply, libenf), Cint,
+                                (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Int64}, Int32,
+                                 Ptr{Int64}, Int32, Cdouble, Cdouble, Ptr{Cdouble}, Ptr{Cvoid}),
+                                _dt(R), D, np, out.buf.ptr, B, theta.buf.ptr, acc.buf.ptr, runs, length(runs) ÷ 2,
+                                hb, length(hb) ÷ 3, rule.eta, rule.epsilon, loss_ptr, C_NULL))
+                else  # the separate calls: loss, ADAGrad per run, re-normalisation per batch (same arithmetic)
+                    g = Array(out)
+                    lossv = Float64[Float64(g[1] / R(B))]
+                    GC.@preserve lossv _memcpy(Ptr{Cvoid}(loss_ptr), Ptr{Cvoid}(pointer(lossv)), sizeof(lossv), MEMCPY_H2D)
+                    for q in 1:2:length(runs)
+                        a0, a1 = runs[q], runs[q+1]
+                        check(ccall((:enf_adagrad_step, libenf), Cint,
+                                    (Cint, Int64, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cdouble, Cdouble, Cdouble, Ptr{Cvoid}),
+                                    _dt(R), a1 - a0, theta.buf.ptr + a0 * sizeof(R), acc.buf.ptr + a0 * sizeof(R),
+                                    out.buf.ptr + (1 + a0) * sizeof(R), 1.0 / B, rule.eta, rule.epsilon, C_NULL))
+                    end
+                    for q in 1:3:length(hb)
+                        check(ccall((:enf_householder_normalize_strided, libenf), Cint,
+                                    (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
+                                    _dt(R), D, hb[q+1], theta.buf.ptr + hb[q] * sizeof(R), hb[q+2], C_NULL))
+                    end
+                end
             end
             s += 1
         end

@@ -185,9 +185,11 @@ enf_status enf_adagrad_step(enf_dtype dtype, int64_t count, void* params, void* 
  * point into theta), then *loss_out = negll / N (device double), ADAGrad (eta, epsilon) with
  * g = gradient / N on the nruns ranges [runs[2i], runs[2i+1]) of theta, and the re-normalisation
  * of the nhb Householder column batches (hbatches[3i..3i+2] = offset in theta, column count, column
- * stride). Identical arithmetic to enf_flow_negll_grad + enf_adagrad_step per range +
- * enf_householder_normalize_strided per batch on one rank, in three launches instead of eight.
- * Multi-GPU training: enf_flow_negll_grad, the all-reduce, then enf_whitening_apply. */
+ * stride; every column must start at a multiple of D in theta, as the parameter layout puts it). Identical
+ * arithmetic to enf_flow_negll_grad + enf_adagrad_step per range + enf_householder_normalize_strided per batch
+ * on one rank, in two launches (round 5: the gradient kernel, then one reduction launch in which every
+ * parameter vector is summed over the gradient blocks, projected, updated and re-normalised by a block of its
+ * own). Multi-GPU training: enf_whitening_step_dp (or enf_flow_negll_grad, the all-reduce, enf_whitening_apply). */
 enf_status enf_whitening_step(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
                               const enf_layer* layers, int32_t nlayers, void* theta, void* acc,
                               const int64_t* runs, int32_t nruns, const int64_t* hbatches, int32_t nhb,
@@ -264,11 +266,13 @@ enf_status enf_allreduce_sum(enf_comm comm, void* buf, int64_t count, enf_dtype 
 
 /* One rank's DATA-PARALLEL optimize_whitening minibatch step in one call (round 4; src/optimize_whitening.jl:36-42):
  * the loss / gradient sums of this rank's N columns X (its share of a minibatch of B columns in all; N may be 0),
- * the cross-rank sum over `comm` (RCCL on hip_stream, of the kernels' double slice totals -- before any rounding
- * to the dtype; NULL comm: one rank, no all-reduce), then *loss_out = negll (sum / B), ADAGrad on the runs with
- * gradient / B and the Householder re-normalisation, as enf_whitening_step. Replaces enf_flow_negll_grad +
- * enf_allreduce_sum + enf_whitening_apply (and the zeroing of their buffer) with gradient + all-reduce + one tail
- * launch; on one rank (comm NULL or a 1-rank communicator, B = N) identical to enf_whitening_step. workspace:
+ * the cross-rank sum over `comm` (RCCL on hip_stream, of this rank's 1 + nparams double totals -- before any
+ * rounding to the dtype; NULL comm: one rank, no all-reduce), then *loss_out = negll (sum / B), ADAGrad on the
+ * runs with gradient / B and the Householder re-normalisation, as enf_whitening_step. Replaces
+ * enf_flow_negll_grad + enf_allreduce_sum + enf_whitening_apply (and the zeroing of their buffer) with gradient +
+ * totals + all-reduce + one update launch; on one rank (comm NULL or a 1-rank communicator, B = N) identical to
+ * enf_whitening_step. A flow beyond one gradient launch's bounds (the chunked path of enf_flow_negll_grad) sums
+ * each rank's gradient in the dtype before the all-reduce (its chunks accumulate into a buffer of T). workspace:
  * enf_flow_negll_grad_workspace(N) bytes. Every rank must call it with the same B, runs and batches. */
 enf_status enf_whitening_step_dp(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
                                  const enf_layer* layers, int32_t nlayers, void* theta, void* acc, const int64_t* runs,
