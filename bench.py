@@ -706,6 +706,14 @@ def train_leg(dev, world, rank):
             res["rank_share_of_8"]["separate_calls"] = {k: u8[k] for k in ("value", "ms_per_step", "step", "phases")}
         except Exception as e:  # noqa: BLE001
             res["rank_share_of_8"] = {"error": f"{type(e).__name__}: {e}"}
+        # the reference's own example training loops (examples/nf_example_1d.jl, nf_example_2d.jl: fp64, their
+        # flows, minibatch sizes and step counts), each beside the oracle's loop on one host thread
+        res["reference_examples"] = {}
+        for ex in ("1d", "2d"):
+            try:
+                res["reference_examples"][ex] = bench_train.example_leg(dev, ex)
+            except Exception as e:  # noqa: BLE001
+                res["reference_examples"][ex] = {"error": f"{type(e).__name__}: {e}"}
     return res
 
 

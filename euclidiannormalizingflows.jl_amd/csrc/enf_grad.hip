@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdint>
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -36,6 +37,7 @@
 #include "enf_grad_hj.h"
 #include "enf_grad_tail.h"
 #include "enf_internal.h"
+#include "enf_math64.h"
 #include "enf_train.h"
 
 namespace enf {
@@ -106,17 +108,203 @@ __device__ __forceinline__ T gsum(T x) {
 // same row (all column slots of the wave) are summed with cross-lane shuffles first, then one lane
 // per row does a plain (non-atomic) read-modify-write -- every address has exactly one writer.
 // D >= V (CPF == 1): lanes with equal lane % G share rows; D < V: every lane holds all D rows.
+// Round 5: the stages within a 16-lane row are DPP moves (quad_perm xor 1 / xor 2, row_ror 4 / 8 -- shifts by a
+// multiple of the class size keep lanes in their class), only the two cross-row stages are ds_bpermute; a
+// bpermute round trip is several times a DPP move's latency and the examples' one-block steps are chains of these.
+template <int CTRL, typename T>
+__device__ __forceinline__ T wdpp(T x) {
+  if constexpr (std::is_same_v<T, float>) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, true);
+    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+  }
+}
 template <int G, int CPF, int SEG, typename T>
 __device__ __forceinline__ void wave_accumulate(double* __restrict__ acc, int row, T v, int lane, int nrows) {
   (void)CPF;
   (void)SEG;
-#pragma unroll
-  for (int m = G; m < 64; m <<= 1) v += __shfl_xor(v, m);
+  if constexpr (G < 2) v += wdpp<0xB1>(v);   // quad_perm(1,0,3,2): lane ^ 1
+  if constexpr (G < 4) v += wdpp<0x4E>(v);   // quad_perm(2,3,0,1): lane ^ 2
+  if constexpr (G < 8) v += wdpp<0x124>(v);  // row_ror:4
+  if constexpr (G < 16) v += wdpp<0x128>(v); // row_ror:8
+  if constexpr (G < 32) v += __shfl_xor(v, 16);
+  if constexpr (G < 64) v += __shfl_xor(v, 32);
   if (lane < G && row < nrows) acc[row] += (double)v;  // padded rows (row >= D) have no parameter
 }
 
 template <typename T>
 __device__ __forceinline__ T sigm(T t) { return (T)1 / ((T)1 + exp(-t)); }
+
+// ---- fp64 in-range forms of the elementwise steps (round 5; VERDICT r04 item 4, the reference examples'
+// optimize_whitening steps at D <= 2 are one dependent chain per column through these steps). ocml's fp64 exp /
+// log are ~42 / ~98 VALU instructions and a division ~12: the literal CenterContract forward + backward took 8
+// exp, 5 log and ~10 divisions per element, the Johnson step two asinh / log1p and ~8 divisions. Here, with the
+// row constants the block prologue derives once (rec_extra below) and enf_math64.h's table log / expm1 / div64
+// (as the flow kernels' fp64 steps, enf_steps.h): a wave whose elements are all in range (grad_fast_ok, a
+// wave vote) takes these forms, any other wave the literal ones (fwd_elem / bwd_elem).
+// Row constants after the np parameters (fp64, kernel rows <= 64):
+//   ScaleShift   {log|a|, 1/a}
+//   Johnson      {1/lambda, 1/delta, log|delta/lambda|}
+//   Center*      {exp(b a), exp(-b a), exp(2 b a), 1/b}
+__host__ __device__ constexpr int rec_extra(int op) {
+  return op == OP_SCALESHIFT ? 2 : op == OP_JOHNSON ? 3 : (op == OP_CENTER_STRETCH || op == OP_CENTER_CONTRACT) ? 4 : 0;
+}
+constexpr int kFastMaxD = 64;
+template <typename T, int D>
+__host__ __device__ constexpr bool grad_fast_rows() { return std::is_same_v<T, double> && D <= kFastMaxD; }
+// record values per row of a step: the parameters, then (fast rows) the constants
+__host__ __device__ constexpr int rec_nparams(int op, bool fast) {
+  return (op == OP_HOUSEHOLDER ? 1 : op == OP_SCALESHIFT ? 2 : (op == OP_JOHNSON || op == OP_JOHNSON_INV) ? 4 : 3) +
+         (fast ? rec_extra(op) : 0);
+}
+
+// the row constants of a step, from its parameters just written to the record r (value q of the row at r[q V]);
+// the same double operations as the per-element expressions they replace
+template <int V>
+__device__ __forceinline__ void rec_extra_store(int op, double* r) {
+  if (op == OP_SCALESHIFT) {
+    const double a = r[0];
+    r[2 * V] = log(fabs(a));
+    r[3 * V] = 1.0 / a;
+  } else if (op == OP_JOHNSON) {
+    const double dl = r[V], lm = r[3 * V];
+    r[4 * V] = 1.0 / lm;
+    r[5 * V] = 1.0 / dl;
+    r[6 * V] = log(fabs(dl / lm));
+  } else if (op == OP_CENTER_STRETCH || op == OP_CENTER_CONTRACT) {
+    const double a = r[0], b = r[V];
+    r[3 * V] = exp(b * a);
+    r[4 * V] = exp(-b * a);
+    r[5 * V] = exp(2.0 * b * a);
+    r[6 * V] = 1.0 / b;
+  }
+}
+
+__device__ __forceinline__ bool center_moderate(double b, double E1) {
+  return fabs(b) >= 1e-100 && fabs(b) <= 1e100 && E1 >= 1e-50 && E1 <= 1e50;
+}
+
+// Does the in-range form apply to this element (forward: x the step's input; backward also y its output)?
+__device__ __forceinline__ bool grad_fast_ok(int op, double x, double y, const double* p, const double* xr, bool bwd) {
+  switch (op) {
+    case OP_SCALESHIFT: return true;
+    case OP_JOHNSON: {
+      // |z| < 2^26 with margin (asinh64_tab_fin), the parameters and their reciprocals normal and finite
+      const double zq = (x - p[2]) * xr[0];
+      return fabs(zq) < 3.0e7 && fabs(p[3]) >= 1e-300 && fabs(p[3]) <= 1e300 && fabs(p[1]) >= 1e-300 &&
+             fabs(p[1]) <= 1e300 && fabs(xr[2]) < 1e300;
+    }
+    case OP_CENTER_CONTRACT: return center_moderate(p[1], xr[0]) && fabs(p[1] * (x - p[2])) <= 200.0;
+    case OP_CENTER_STRETCH:
+      return center_moderate(p[1], xr[0]) && fabs(p[1] * x) <= 200.0 && (!bwd || fabs(p[1] * (y - p[2])) <= 200.0);
+    default: return false;
+  }
+}
+
+// the logistic pair of t = b xu, u = |t|: with P = e^u, D1 = P + E1, D2 = 1 + P E1 (E1 = e^(b a)) and ONE
+// division, sigmoid(t - b a) and sigmoid(-t - b a) with their complements (s1, 1 - s1, s2, 1 - s2), each a
+// product of positive terms (no cancellation): P/D1, E1/D1 and 1/D2, P E1/D2, swapped for t < 0.
+struct Logistic2 {
+  double s1, c1, s2, c2;
+};
+__device__ __forceinline__ Logistic2 logistic2(double t, double E1) {
+  const double P = 1.0 + expm1_64_in(fabs(t));
+  const double D1 = P + E1, D2 = fma(P, E1, 1.0);
+  const double rr = div64(1.0, D1 * D2);
+  const double sa = P * D2 * rr, ca = E1 * D2 * rr, sb = D1 * rr, cb = P * E1 * D1 * rr;
+  const bool neg = t < 0.0;
+  return {neg ? sb : sa, neg ? cb : ca, neg ? sa : sb, neg ? ca : cb};
+}
+
+// forward of one element, in-range form; adds the ladj term (natural log) to lad. tab: the log table (LDS).
+__device__ __forceinline__ double fwd_fast(int op, double x, const double* p, const double* xr, double& lad,
+                                           const double* __restrict__ tab) {
+  switch (op) {
+    case OP_SCALESHIFT: lad += xr[0]; return fma(x, p[0], p[1]);  // scale_shift_trafo.jl:15-22
+    case OP_JOHNSON: {  // johnson_trafo.jl:29-32, 39-42
+      const double z = div64(x - p[2], p[3]);
+      lad += xr[2] - 0.5 * log1p64_tab(z * z, tab);
+      return fma(p[1], asinh64_tab_fin(z, tab), p[0]);
+    }
+    case OP_CENTER_CONTRACT: {  // center_stretch.jl:11-15, 17-22 (enf_steps.h step_center_contract's form)
+      const double E1 = xr[0], Ei = xr[1], ib = xr[3];
+      const double t = p[1] * (x - p[2]);
+      const double em = expm1_64_in(fabs(t));
+      const double P = 1.0 + em;
+      const double arg = div64(Ei * (em * (2.0 + em)), P + Ei);
+      const double pe = fma(P, E1, 1.0), pi = P + E1;
+      lad += log64_tab(div64(fma(P, pe, pi), pi * pe), 0, tab);
+      return (__builtin_copysign(log1p64_tab(arg, tab), t) + 0.0) * ib;
+    }
+    default: {  // OP_CENTER_STRETCH, center_stretch.jl:4-8, 41-42 (enf_steps.h step_center_stretch's form)
+      const double bv = p[1], c = p[2], E1 = xr[0], E2 = xr[2], ib = xr[3];
+      const double ex = exp64_in(fabs(bv * x));
+      const double ome = 1.0 - ex;
+      const double inner = (sqrt64_ge1(ome * ome * E2 + 4.0 * ex) - ome * E1) / 2.0;
+      const double pe = fma(E1, inner, 1.0), ie = inner + E1;
+      lad -= log64_tab(div64(fma(inner, pe, ie), ie * pe), 0, tab);
+      return fma(__builtin_copysign(log64_tab(inner, 0, tab), x), ib, c);
+    }
+  }
+}
+
+// backward of one element, in-range form (bwd_elem's derivatives): x the step's input, y its output (the next
+// step's stored input, or the flow's output), g = dS/dy, cl = dS/dladj; adds dS/dparam into dp, returns dS/dx
+__device__ __forceinline__ double bwd_fast(int op, double x, double y, double g, const double* p, const double* xr,
+                                           double* dp, double cl, const double* __restrict__ tab) {
+  switch (op) {
+    case OP_SCALESHIFT:
+      dp[0] += g * x + cl * xr[1];
+      dp[1] += g;
+      return g * p[0];
+    case OP_JOHNSON: {
+      const double dl = p[1], il = xr[0];
+      const double z = div64(x - p[2], p[3]);
+      const double s2 = fma(z, z, 1.0);
+      double rs = __builtin_amdgcn_rsq(s2);  // 1/sqrt(1 + z^2): seed + two Newton steps
+      rs = fma(0.5 * rs, fma(-s2 * rs, rs, 1.0), rs);
+      rs = fma(0.5 * rs, fma(-s2 * rs, rs, 1.0), rs);
+      const double A = dl * il * rs;       // dl / (lm s)
+      const double Bc = z * il * rs * rs;  // z / (lm s2)
+      dp[0] += g;
+      dp[1] += fma(g, asinh64_tab_fin(z, tab), cl * xr[1]);
+      dp[2] += -g * A + cl * Bc;
+      dp[3] += (-g * A * z - cl * il) + cl * (Bc * z);
+      return g * A - cl * Bc;
+    }
+    case OP_CENTER_CONTRACT: {
+      const double a = p[0], b = p[1], xu = x - p[2], ib = xr[3];
+      const Logistic2 L = logistic2(b * xu, xr[0]);
+      const double ss = L.s1 + L.s2, iss = div64(1.0, ss);
+      const double q1 = L.s1 * L.c1, q2 = L.s2 * L.c2;
+      const double dyda = L.s2 - L.s1, dydb = (L.s1 * (xu - a) + L.s2 * (xu + a) - y) * ib;
+      const double dldx = (q1 * b - q2 * b) * iss, dlda = -(q1 + q2) * b * iss, dldb = (q1 * (xu - a) - q2 * (xu + a)) * iss;
+      dp[0] += g * dyda + cl * dlda;
+      dp[1] += g * dydb + cl * dldb;
+      dp[2] += -(g * ss + cl * dldx);
+      return g * ss + cl * dldx;
+    }
+    default: {  // OP_CENTER_STRETCH: y = cs(x) = s(x) + c and cc(y) = f(y - c) = x (bwd_elem's derivation, its ccv = x)
+      const double a = p[0], b = p[1], c = p[2], ib = xr[3];
+      const double yu = y - c;
+      const Logistic2 L = logistic2(b * yu, xr[0]);
+      const double ss = L.s1 + L.s2, iss = div64(1.0, ss);
+      const double q1 = L.s1 * L.c1, q2 = L.s2 * L.c2;
+      const double cc_a = L.s2 - L.s1, cc_b = (L.s1 * (yu - a) + L.s2 * (yu + a) - x) * ib;
+      const double lcc_y = (q1 * b - q2 * b) * iss, lcc_a = -(q1 + q2) * b * iss,
+                   lcc_b = (q1 * (yu - a) - q2 * (yu + a)) * iss;
+      const double dyda = -cc_a * iss, dydb = -cc_b * iss;
+      const double dlda = -(lcc_y * dyda + lcc_a), dldb = -(lcc_y * dydb + lcc_b);
+      dp[0] += g * dyda + cl * dlda;
+      dp[1] += g * dydb + cl * dldb;
+      dp[2] += g;  // dy/dc = 1, dl/dc = 0
+      return g * iss - cl * (lcc_y * iss);
+    }
+  }
+}
 
 // Per-element forward of one step (accurate form). Returns the output; adds the element's ladj
 // term (natural log) to lad.
@@ -230,6 +418,75 @@ __device__ __forceinline__ T bwd_elem(int op, T x, T g, const T* p, T* dp, T cl)
   }
 }
 
+// The in-range forms of one step over the lane's V values (FAST rows): loads the step's records with compile-time
+// offsets, votes over the wave, and returns false (nothing done) when some element is out of range.
+template <int OP, int V>
+__device__ __forceinline__ void fast_rec(const double* __restrict__ r, int e, double (&p)[4], double (&xr)[4]) {
+  constexpr int np = grad_nparams(OP), nx = rec_extra(OP);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) p[q] = q < np ? r[q * V + e] : 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) xr[q] = q < nx ? r[(np + q) * V + e] : 0.0;
+}
+
+template <int OP, int V, int SEG, int CPF>
+__device__ __forceinline__ bool fwd_fast_step(double (&x)[V], double (&lad)[CPF], const double* __restrict__ r, bool ss1,
+                                              int r0, const double* __restrict__ tab) {
+  bool ok = true;
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    double p[4], xr[4];
+    fast_rec<OP, V>(r, e, p, xr);
+    ok = ok && grad_fast_ok(OP, x[e], 0.0, p, xr, false);
+  }
+  if (!__all(ok)) return false;
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    double p[4], xr[4];
+    fast_rec<OP, V>(r, e, p, xr);
+    double l = 0.0;
+    x[e] = fwd_fast(OP, x[e], p, xr, l, tab);
+    if (!ss1 || r0 + e % SEG == 0) lad[e / SEG] += l;
+  }
+  return true;
+}
+
+template <int OP, int V, int SEG, int G, int CPF>
+__device__ __forceinline__ bool bwd_fast_step(const double (&xin)[V], const double (&yout)[V], double (&g)[V],
+                                              const bool (&valid)[V], const double (&clv)[V], const double* __restrict__ r,
+                                              double* __restrict__ gacc, int r0, int lane, int Dr,
+                                              const double* __restrict__ tab) {
+  constexpr int np = grad_nparams(OP);
+  bool ok = true;
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    double p[4], xr[4];
+    fast_rec<OP, V>(r, e, p, xr);
+    ok = ok && grad_fast_ok(OP, xin[e], yout[e], p, xr, true);
+  }
+  if (!__all(ok)) return false;
+  // the lane's contributions per (parameter, row): its CPF columns summed in the lane first, then one wave sum each
+  double dsum[4][SEG];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int k = 0; k < SEG; ++k) dsum[q][k] = 0.0;
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    double p[4], xr[4], dp[4] = {0, 0, 0, 0};
+    fast_rec<OP, V>(r, e, p, xr);
+    const double gx = bwd_fast(OP, xin[e], yout[e], g[e], p, xr, dp, clv[e], tab);
+#pragma unroll
+    for (int q = 0; q < np; ++q) dsum[q][e % SEG] += valid[e] ? dp[q] : 0.0;
+    g[e] = valid[e] ? gx : 0.0;
+  }
+#pragma unroll
+  for (int q = 0; q < np; ++q)
+#pragma unroll
+    for (int k = 0; k < SEG; ++k) wave_accumulate<G, CPF, SEG>(gacc + q * Dr, r0 + k, dsum[q][k], lane, Dr);
+  return true;
+}
+
 // STEP (round 5): the single-block fused optimize_whitening step -- the grid is one block, and instead of writing
 // its partial row the block sums its waves into LDS and runs the update itself (block_step_update): one launch per
 // minibatch step where the two-launch path costs two kernel boundaries (the examples' B = 100 / 1000 steps).
@@ -250,44 +507,99 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
   double* gacc = reinterpret_cast<double*>(smem + (threadIdx.x >> 6) * gbytes);  // this wave's
   double* lossw = reinterpret_cast<double*>(smem + nw * gbytes);
   T* rec = reinterpret_cast<T*>(smem + nw * gbytes + 64);
+  constexpr bool FAST = grad_fast_rows<T, D>();  // (fp64, D <= 64: the row constants of rec_extra are recorded)
   int nrec = 0;
-  for (int s = 0; s < a.nsteps; ++s) nrec += grad_nparams(a.op[s]) * (D > V ? D : V);
+  for (int s = 0; s < a.nsteps; ++s) nrec += rec_nparams(a.op[s], FAST) * (D > V ? D : V);
   T* act = rec + ((nrec + 3) / 4) * 4 + (threadIdx.x >> 6) * (a.nsteps * 64 * V);
+  // the table log of the in-range forms (after the activations of the block's waves)
+  double* ltab = reinterpret_cast<double*>(rec + ((nrec + 3) / 4) * 4 + nw * (a.nsteps * 64 * V));
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #if ENF_DIAG
   const long long ts0 = STEP && a.diag_ts ? (long long)clock64() : 0;
 #endif
   for (int i = lane; i < a.nparams; i += 64) gacc[i] = 0.0;
-  // raw parameter records, layout [group][param][element] as the forward kernel (RV = V)
-  for (int s = 0; s < a.nsteps; ++s) {
-    const LayerDesc& L = a.layers[a.layer[s]];
-    const int np = grad_nparams(a.op[s]);
-    const int nent = D > V ? D : V;
-    for (int i = tid; i < nent; i += blockDim.x) {
-      const int g = D >= V ? i / V : 0, e = i % V;
-      const int row = D >= V ? i : e % D;
-      for (int q = 0; q < np; ++q) {
+  if constexpr (FAST)
+    for (int i = tid; i < 3 * kLogTabN; i += blockDim.x) ltab[i] = kLogTab[i];
+  // Records, layout [group][param][element] as the forward kernel (RV = V), in three passes (round 5: ONE round of
+  // global loads, where the step-by-step loop waited for each step's parameters, and each thread of a reflection
+  // loaded the whole column for its v'v):
+  //   (A) every raw parameter value of every step, an (entry, parameter) item per thread and step, all the steps'
+  //       loads in flight together (one_round; a larger flow loops);
+  //   (B) the reflections' v'v in double, one wave per Householder step (its lanes, then the xor tree);
+  //   (C) vh = v sqrt(2/v'v) (householder_trafo.jl:9-10) and, FAST, the row constants (rec_extra).
+  const int nent = D > V ? D : V;
+  const int NT = blockDim.x;
+  auto raw_item = [&](int s, int k, T& v) -> int {  // the raw value of item k of step s, and its record index
+    const int op = a.op[s], np = grad_nparams(op), rn = rec_nparams(op, FAST);
+    const int i = k / np, q = k - i * np;
+    const int g = D >= V ? i / V : 0, e = i % V;
+    const int row = D >= V ? i : e % D;
+    if (row >= a.D) {
+      // padded row (D not a power of two): parameters that map 0 to 0 with ladj 0 (ScaleShift
+      // a = 1, b = 0; Johnson gamma = xi = 0, delta = lambda = 1; Center a = c = 0, b = 1;
+      // reflection 0), so padded rows stay 0 and add nothing to the loss or the gradients
+      v = op == OP_HOUSEHOLDER ? (T)0
+          : op == OP_SCALESHIFT ? (q == 0 ? (T)1 : (T)0)
+          : (op == OP_JOHNSON || op == OP_JOHNSON_INV) ? ((q == 1 || q == 3) ? (T)1 : (T)0)
+          : (q == 1 ? (T)1 : (T)0);
+    } else if (op == OP_HOUSEHOLDER) {
+      v = ((const T*)a.layers[a.layer[s]].p[0])[(int64_t)a.col[s] * a.D + row];
+    } else {
+      v = ((const T*)a.layers[a.layer[s]].p[q])[row];
+    }
+    return a.roff[s] + (g * rn + q) * V + e;
+  };
+  bool one_round = true;
+  for (int s = 0; s < a.nsteps; ++s) one_round = one_round && nent * grad_nparams(a.op[s]) <= NT;
+  if (one_round) {
+    T buf[kMaxGradSteps];
+    int ix[kMaxGradSteps];
+#pragma unroll
+    for (int s = 0; s < kMaxGradSteps; ++s) {
+      ix[s] = -1;
+      if (s < a.nsteps && tid < nent * grad_nparams(a.op[s])) ix[s] = raw_item(s, tid, buf[s]);
+    }
+#pragma unroll
+    for (int s = 0; s < kMaxGradSteps; ++s)
+      if (ix[s] >= 0) rec[ix[s]] = buf[s];
+  } else {
+    for (int s = 0; s < a.nsteps; ++s)
+      for (int k = tid; k < nent * grad_nparams(a.op[s]); k += NT) {
         T v;
-        if (row >= a.D) {
-          // padded row (D not a power of two): parameters that map 0 to 0 with ladj 0 (ScaleShift
-          // a = 1, b = 0; Johnson gamma = xi = 0, delta = lambda = 1; Center a = c = 0, b = 1;
-          // reflection 0), so padded rows stay 0 and add nothing to the loss or the gradients
-          const int op = a.op[s];
-          v = op == OP_HOUSEHOLDER ? (T)0
-              : op == OP_SCALESHIFT ? (q == 0 ? (T)1 : (T)0)
-              : (op == OP_JOHNSON || op == OP_JOHNSON_INV) ? ((q == 1 || q == 3) ? (T)1 : (T)0)
-              : (q == 1 ? (T)1 : (T)0);
-        } else if (a.op[s] == OP_HOUSEHOLDER) {
-          // normalised reflection vector vh = v*sqrt(2/v'v) (computed per block, sum in double)
-          const T* vc = (const T*)L.p[0] + (int64_t)a.col[s] * a.D;
-          double vv = 0.0;
-          for (int d = 0; d < a.D; ++d) vv += (double)vc[d] * (double)vc[d];
-          v = (T)((double)vc[row] * sqrt(2.0 / vv));
-        } else {
-          v = ((const T*)L.p[q])[row];
-        }
-        rec[a.roff[s] + (g * np + q) * V + e] = v;
+        const int ix = raw_item(s, k, v);
+        rec[ix] = v;
+      }
+  }
+  __syncthreads();
+  // (B) into wave 0's activation area (not used before the tiles)
+  double* hsc = reinterpret_cast<double*>(rec + ((nrec + 3) / 4) * 4);
+  for (int s = wave; s < a.nsteps; s += nw) {
+    if (a.op[s] != OP_HOUSEHOLDER) continue;  // wave-uniform
+    constexpr int rn = rec_nparams(OP_HOUSEHOLDER, FAST);
+    double vv = 0.0;
+    for (int d = lane; d < a.D; d += 64) {
+      const int g = D >= V ? d / V : 0, e = D >= V ? d % V : d;  // (D < V: entry d holds row d)
+      const double v = (double)rec[a.roff[s] + g * rn * V + e];
+      vv += v * v;
+    }
+    vv = lane_sum(vv, a.D);
+    if (lane == 0) hsc[s] = sqrt(2.0 / vv);
+  }
+  __syncthreads();
+  // (C)
+  for (int s = 0; s < a.nsteps; ++s) {
+    const int op = a.op[s];
+    const bool hh = op == OP_HOUSEHOLDER;
+    if (!hh && !(FAST && rec_extra(op) > 0)) continue;  // uniform
+    const int rn = rec_nparams(op, FAST);
+    for (int i = tid; i < nent; i += NT) {
+      const int g = D >= V ? i / V : 0, e = i % V;
+      T* r = rec + a.roff[s] + g * rn * V + e;
+      if (hh) {
+        r[0] = (T)((double)r[0] * hsc[s]);
+      } else if constexpr (FAST) {
+        rec_extra_store<V>(op, (double*)r);
       }
     }
   }
@@ -296,6 +608,14 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
   const long long ts1 = STEP && a.diag_ts ? (long long)clock64() : 0;
 #endif
 
+  // the one-block step: the update's own loads (theta, ADAGrad state, Householder columns) issued now, consumed after
+  // the tiles (block_step_update)
+  StepPre<T> pre;
+  bool have_pre = false;
+  if constexpr (STEP) {
+    have_pre = a.nparams <= (int)blockDim.x;
+    if (have_pre && tid < a.nparams) pre = step_prefetch<T>(tid, a.D, *rs, *ss);
+  }
   const int r0 = D >= V ? V * (lane % G) : 0;
   const int grp = D >= V ? lane % G : 0;
   const int64_t ntiles = (a.N + COLS - 1) / COLS;
@@ -319,7 +639,7 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
 #pragma unroll
       for (int e = 0; e < V; ++e) as[e] = x[e];
       const int op = a.op[s];
-      const T* r = rec + a.roff[s] + grp * grad_nparams(op) * V;
+      const T* r = rec + a.roff[s] + grp * rec_nparams(op, FAST) * V;
       if (op == OP_HOUSEHOLDER) {
 #pragma unroll
         for (int c = 0; c < CPF; ++c) {
@@ -335,16 +655,31 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
         // ScaleShiftTrafo with a length-1 `a` (layer k = 1): its ladj constant log|a| counts once, on row 0
         // (scale_shift_trafo.jl:22 sums over a's own length)
         const bool ss1 = op == OP_SCALESHIFT && a.layers[a.layer[s]].k == 1;
+        bool done = false;
+        if constexpr (FAST) {
+          switch (op) {
+            case OP_SCALESHIFT: done = fwd_fast_step<OP_SCALESHIFT, V, SEG, CPF>(x, lad, r, ss1, r0, ltab); break;
+            case OP_JOHNSON: done = fwd_fast_step<OP_JOHNSON, V, SEG, CPF>(x, lad, r, ss1, r0, ltab); break;
+            case OP_CENTER_CONTRACT: done = fwd_fast_step<OP_CENTER_CONTRACT, V, SEG, CPF>(x, lad, r, ss1, r0, ltab); break;
+            case OP_CENTER_STRETCH: done = fwd_fast_step<OP_CENTER_STRETCH, V, SEG, CPF>(x, lad, r, ss1, r0, ltab); break;
+            default: break;
+          }
+        }
+        if (!done) {
 #pragma unroll
-        for (int e = 0; e < V; ++e) {
-          T p[4];
-          for (int q = 0; q < np; ++q) p[q] = r[q * V + e];
-          T l = 0;
-          x[e] = fwd_elem<T>(op, x[e], p, l);
-          if (!ss1 || r0 + e % SEG == 0) lad[e / SEG] += l;
+          for (int e = 0; e < V; ++e) {
+            T p[4];
+            for (int q = 0; q < np; ++q) p[q] = r[q * V + e];
+            T l = 0;
+            x[e] = fwd_elem<T>(op, x[e], p, l);
+            if (!ss1 || r0 + e % SEG == 0) lad[e / SEG] += l;
+          }
         }
       }
     }
+    T yfin[V];  // the flow's output (the last step's output for the backward's in-range forms)
+#pragma unroll
+    for (int e = 0; e < V; ++e) yfin[e] = x[e];
     // ---- loss: sum_d (y^2 + log 2pi)/2 - ladj (only valid columns)
     if constexpr (!VJP) {
       T part = 0;
@@ -380,7 +715,7 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
       for (int e = 0; e < V; ++e) xin[e] = as[e];
       const int op = a.op[s];
       const int np = grad_nparams(op);
-      const T* r = rec + a.roff[s] + grp * np * V;
+      const T* r = rec + a.roff[s] + grp * rec_nparams(op, FAST) * V;
       if (op == OP_HOUSEHOLDER) {
         // y = x - vh (vh'x): dS/dx = g - vh (vh'g); with w = vh/sqrt2 (unit), the direction
         // gradient dS/dw_d = -2 (g_d (w'x) + x_d (w'g)) = -sqrt2 (g_d (vh'x) + x_d (vh'g)); the
@@ -404,17 +739,48 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
         }
       } else {
         const bool ss1 = op == OP_SCALESHIFT && a.layers[a.layer[s]].k == 1;
+        // the step's output: the next step's stored input, or the flow's output
+        T yout[V];
+        {
+          const T* an = act + (s + 1) * 64 * V + lane * V;
 #pragma unroll
-        for (int e = 0; e < V; ++e) {
-          T p[4], dp[4] = {0, 0, 0, 0};
-          for (int q = 0; q < np; ++q) p[q] = r[q * V + e];
-          const int row = r0 + e % SEG;
-          // (ScaleShift's ladj cotangent only reaches its ladj term, which a length-1 `a` has on row 0 only)
-          const T clw = (ss1 && row != 0) ? (T)0 : (VJP ? cl[e / SEG] : (T)-1);
-          const T gx = bwd_elem<T>(op, xin[e], g[e], p, dp, clw);
-          for (int q = 0; q < np; ++q)
-            wave_accumulate<G, CPF, SEG>(gacc + a.goff[s] + q * a.D, row, valid[e] ? dp[q] : (T)0, lane, a.D);
-          g[e] = valid[e] ? gx : (T)0;
+          for (int e = 0; e < V; ++e) yout[e] = s + 1 < a.nsteps ? an[e] : yfin[e];
+        }
+        bool done = false;
+        if constexpr (FAST) {
+          double clv[V];
+#pragma unroll
+          for (int e = 0; e < V; ++e) clv[e] = (ss1 && r0 + e % SEG != 0) ? 0.0 : (VJP ? (double)cl[e / SEG] : -1.0);
+          double* ga = gacc + a.goff[s];
+          switch (op) {
+            case OP_SCALESHIFT:
+              done = bwd_fast_step<OP_SCALESHIFT, V, SEG, G, CPF>(xin, yout, g, valid, clv, r, ga, r0, lane, a.D, ltab);
+              break;
+            case OP_JOHNSON:
+              done = bwd_fast_step<OP_JOHNSON, V, SEG, G, CPF>(xin, yout, g, valid, clv, r, ga, r0, lane, a.D, ltab);
+              break;
+            case OP_CENTER_CONTRACT:
+              done = bwd_fast_step<OP_CENTER_CONTRACT, V, SEG, G, CPF>(xin, yout, g, valid, clv, r, ga, r0, lane, a.D, ltab);
+              break;
+            case OP_CENTER_STRETCH:
+              done = bwd_fast_step<OP_CENTER_STRETCH, V, SEG, G, CPF>(xin, yout, g, valid, clv, r, ga, r0, lane, a.D, ltab);
+              break;
+            default: break;
+          }
+        }
+        if (!done) {
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            T p[4], dp[4] = {0, 0, 0, 0};
+            for (int q = 0; q < np; ++q) p[q] = r[q * V + e];
+            const int row = r0 + e % SEG;
+            // (ScaleShift's ladj cotangent only reaches its ladj term, which a length-1 `a` has on row 0 only)
+            const T clw = (ss1 && row != 0) ? (T)0 : (VJP ? cl[e / SEG] : (T)-1);
+            const T gx = bwd_elem<T>(op, xin[e], g[e], p, dp, clw);
+            for (int q = 0; q < np; ++q)
+              wave_accumulate<G, CPF, SEG>(gacc + a.goff[s] + q * a.D, row, valid[e] ? dp[q] : (T)0, lane, a.D);
+            g[e] = valid[e] ? gx : (T)0;
+          }
         }
       }
     }
@@ -435,7 +801,7 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
   __syncthreads();
   if constexpr (STEP) {
     // the block's row into LDS past the activations (the same sums as the row below), then the update
-    const size_t act_end = reinterpret_cast<size_t>(rec + ((nrec + 3) / 4) * 4 + nw * (a.nsteps * 64 * V));
+    const size_t act_end = reinterpret_cast<size_t>(ltab + (FAST ? 3 * kLogTabN : 0));
     double* tot = reinterpret_cast<double*>((act_end + 15) / 16 * 16);
     unsigned char* scratch = reinterpret_cast<unsigned char*>(tot + ((1 + a.nparams + 1) / 2) * 2);
     if (tid == 0) {
@@ -454,7 +820,7 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
 #if ENF_DIAG
     const long long ts3 = a.diag_ts ? (long long)clock64() : 0;
 #endif
-    block_step_update<T>(tot, a.nparams, a.D, *rs, *ss, scratch);
+    block_step_update<T>(tot, a.nparams, a.D, *rs, *ss, scratch, pre, have_pre);
 #if ENF_DIAG
     if (a.diag_ts) {  // (uniform)
       __syncthreads();
@@ -554,6 +920,7 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
   const int64_t Dp = grad_Dp(D);
   const int V = f64 ? grad_lane_values<double>((int)Dp) : grad_lane_values<float>((int)Dp);
   const int nent = (int)(Dp > V ? Dp : V);
+  const bool fast = f64 && Dp <= kFastMaxD;  // grad_fast_rows: the row constants in the records, the log table
   int s = 0, goff = 0, roff = 0;
   for (int l = 0; l < nlayers; ++l) {
     P.ga.layers[l].op = layers[l].op;
@@ -572,7 +939,7 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
         P.ra.hcol[P.ra.nh] = (const char*)layers[l].p[0] + (size_t)c * D * (f64 ? 8 : 4);
         ++P.ra.nh;
       }
-      roff += grad_nparams(layers[l].op) * nent;
+      roff += rec_nparams(layers[l].op, fast) * nent;
       ++s;
     }
     goff += (int)D * (layers[l].op == OP_HOUSEHOLDER ? layers[l].k : grad_nparams(layers[l].op));
@@ -585,7 +952,8 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
   P.ga.nparams = goff;
   const size_t esz = f64 ? 8 : 4;
   const size_t gbytes = ((size_t)goff * 8 + 15) / 16 * 16;
-  const size_t rbytes = ((size_t)(roff + 3) / 4) * 4 * esz;
+  // records, and (fast) the log table after the waves' activations
+  const size_t rbytes = ((size_t)(roff + 3) / 4) * 4 * esz + (fast ? 3 * kLogTabN * sizeof(double) : 0);
   const size_t abytes = (size_t)s * 64 * V * esz;  // per wave
   // 4 waves per block, fewer when their per-wave gradient accumulators and activations do not fit
   P.nw = 4;

@@ -24,8 +24,12 @@
 //
 // Round 3 measured running the finalisation inside the gradient kernel (a ticket taken after a device-scope
 // fence, the last block runs the rest): slower, each device-scope fence writes back and invalidates the XCD's L2
-// (profiles/r03_train_sum_tail_ab.txt, r03_train_fused_tail_in_gradient_ab.txt). The reduction stays a launch
-// of its own.
+// (profiles/r03_train_sum_tail_ab.txt, r03_train_fused_tail_in_gradient_ab.txt). Round 5 measured it again without
+// any fence: rows stored write-through at agent scope, per-row epoch flags, the reduction's blocks reading flags and
+// rows with agent-scope loads. Waiting alone cost nothing (32.7 us per config-5 step at B = 1e5, no reduction), the
+// reduction alone 5.7 us (38.4, not waiting), both together 61.6 against 40.3 for the two launches
+// (profiles/r05/c5_fuse_ab_v2.jsonl): the agent-scope loads of rows other XCDs have just written are slow, and the
+// best case (38.4) would save 2 us. The reduction stays a launch of its own.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -101,30 +105,35 @@ __device__ __forceinline__ double rows_sum(const double* __restrict__ P, int nb,
   return ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
 }
 
-// Sums entries [e0, e0 + E) of the rows (column offset c0 + i) into gl[0 .. E) (LDS), block-wide: J threads per
-// entry over interleaved rows, then the J partial sums in order. nblocks == 1: the row itself.
+// Sums entries [e0, e0 + E) of the rows (column offset c0 + i) into gl[0 .. E) (LDS), block-wide: J = kRedThreads / E
+// lanes per entry over interleaved rows, then the J partial sums in order. The lanes are kRedThreads virtual threads
+// whatever the block size (a block of fewer threads runs several), so every caller sums in the same order.
+// nblocks == 1: the row itself.
 __device__ __forceinline__ void block_sums(const ReduceArgs& r, int64_t c0, int E, double* __restrict__ gl,
                                            double* __restrict__ red) {
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, NT = blockDim.x;
   const int64_t n = 1 + (int64_t)r.nparams;
   const double* P = r.partial;
   if (r.nblocks == 1) {
-    for (int i = tid; i < E; i += kRedThreads) gl[i] = P[c0 + i];
+    for (int i = tid; i < E; i += NT) gl[i] = P[c0 + i];
     __syncthreads();
     return;
   }
   if (2 * E <= kRedThreads) {
     const int J = kRedThreads / E;
-    const int i = tid % E, j = tid / E;
-    if (j < J) red[j * E + i] = rows_sum(P, r.nblocks, n, c0 + i, j, J);
+#pragma unroll 1
+    for (int vt = tid; vt < kRedThreads; vt += NT) {
+      const int i = vt % E, j = vt / E;
+      if (j < J) red[j * E + i] = rows_sum(P, r.nblocks, n, c0 + i, j, J);
+    }
     __syncthreads();
-    if (tid < E) {
-      double s = red[tid];
-      for (int q = 1; q < J; ++q) s += red[q * E + tid];
-      gl[tid] = s;
+    for (int i = tid; i < E; i += NT) {
+      double s = red[i];
+      for (int q = 1; q < J; ++q) s += red[q * E + i];
+      gl[i] = s;
     }
   } else {
-    for (int i = tid; i < E; i += kRedThreads) gl[i] = rows_sum(P, r.nblocks, n, c0 + i, 0, 1);
+    for (int i = tid; i < E; i += NT) gl[i] = rows_sum(P, r.nblocks, n, c0 + i, 0, 1);
   }
   __syncthreads();
 }
@@ -142,11 +151,11 @@ __device__ __forceinline__ int unit_householder(const ReduceArgs& r, int64_t off
 __device__ __forceinline__ void project_column(double* __restrict__ g, const double* __restrict__ vc, int D, int lane) {
   double vv = 0.0;
   for (int d = lane; d < D; d += 64) vv += vc[d] * vc[d];
-  for (int m = 32; m >= 1; m >>= 1) vv += __shfl_xor(vv, m);
+  vv = lane_sum(vv, D);
   const double nrm = sqrt(vv);
   double wd = 0.0;
   for (int d = lane; d < D; d += 64) wd += -1.4142135623730951 * g[d] * (vc[d] / nrm);
-  for (int m = 32; m >= 1; m >>= 1) wd += __shfl_xor(wd, m);
+  wd = lane_sum(wd, D);
   for (int d = lane; d < D; d += 64) g[d] = (-1.4142135623730951 * g[d] - (vc[d] / nrm) * wd) / nrm;
 }
 
@@ -157,7 +166,7 @@ template <typename T>
 __device__ __forceinline__ void normalize_lds(T* __restrict__ v, int D, int lane) {
   double ss = 0.0;
   for (int d = lane; d < D; d += 64) ss += (double)v[d] * (double)v[d];
-  for (int m = 32; m >= 1; m >>= 1) ss += __shfl_xor(ss, m);
+  ss = lane_sum(ss, D);
   const T inv = (T)(1.0 / sqrt(ss));
   for (int d = lane; d < D; d += 64) v[d] *= inv;
 }
@@ -166,9 +175,36 @@ __device__ __forceinline__ void normalize_lds(T* __restrict__ v, int D, int lane
 // block's loss and gradient sums) -> loss, Householder projection, ADAGrad, re-normalisation -- the operations and
 // roundings of grad_reduce_kernel's MODE_STEP over one partial row, so the one-launch and the two-launch steps agree
 // bit for bit. scratch (LDS, 16-byte aligned): np doubles + 2 np T + np ints.
+// What the update of entry i reads that does not depend on the gradient: the Householder column value, the
+// entry's flags (bit 0 trainable, bit 1 in a normalised column), theta and the ADAGrad state. The one-block step
+// loads it for i = threadIdx.x before its tiles (round 5), so the loads' round trip is off the step's critical path.
 template <typename T>
-__device__ void block_step_update(double* __restrict__ tot, int64_t np, int D, const ReduceArgs& r, const StepArgs& s,
-                                  unsigned char* __restrict__ scratch) {
+struct StepPre {
+  double hv = 0.0;
+  T th = (T)0, ac = (T)0;
+  int f = 0;
+};
+template <typename T>
+__device__ __forceinline__ StepPre<T> step_prefetch(int64_t i, int D, const ReduceArgs& r, const StepArgs& s) {
+  StepPre<T> p;
+  const int64_t uo = (i / D) * D;
+  const int h = unit_householder(r, uo);
+  if (h >= 0) p.hv = (double)((const T*)r.hcol[h])[i % D];
+  for (int q = 0; q < s.nruns; ++q) p.f |= (i >= s.runs[q][0] && i < s.runs[q][1]) ? 1 : 0;
+  for (int q = 0; q < s.nhb; ++q) {
+    const int64_t rel = uo - s.hb[q][0];
+    if (rel >= 0 && rel % s.hb[q][2] == 0 && rel / s.hb[q][2] < s.hb[q][1]) p.f |= 2;
+  }
+  if (p.f) p.th = ((const T*)s.theta)[i];
+  if (p.f & 1) p.ac = ((const T*)s.acc)[i];
+  return p;
+}
+
+// pre: this thread's step_prefetch(threadIdx.x) when have_pre (np <= blockDim.x), else loaded here
+template <typename T>
+__device__ __forceinline__ void block_step_update(double* __restrict__ tot, int64_t np, int D, const ReduceArgs& r,
+                                                  const StepArgs& s, unsigned char* __restrict__ scratch,
+                                                  const StepPre<T>& pre, bool have_pre) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6, NT = blockDim.x;
   double* vcol = reinterpret_cast<double*>(scratch);
   T* thl = reinterpret_cast<T*>(vcol + np);
@@ -177,18 +213,11 @@ __device__ void block_step_update(double* __restrict__ tot, int64_t np, int D, c
   double* gl = tot + 1;
   if (tid == 0) *s.loss_out = (double)((T)tot[0] / (T)s.nsamp);
   for (int64_t i = tid; i < np; i += NT) {
-    const int64_t uo = (i / D) * D;
-    const int h = unit_householder(r, uo);
-    vcol[i] = h >= 0 ? (double)((const T*)r.hcol[h])[i % D] : 0.0;
-    int f = 0;
-    for (int q = 0; q < s.nruns; ++q) f |= (i >= s.runs[q][0] && i < s.runs[q][1]) ? 1 : 0;
-    for (int q = 0; q < s.nhb; ++q) {
-      const int64_t rel = uo - s.hb[q][0];
-      if (rel >= 0 && rel % s.hb[q][2] == 0 && rel / s.hb[q][2] < s.hb[q][1]) f |= 2;
-    }
-    flags[i] = f;
-    thl[i] = f ? ((const T*)s.theta)[i] : (T)0;
-    acl[i] = (f & 1) ? ((const T*)s.acc)[i] : (T)0;
+    const StepPre<T> p = have_pre ? pre : step_prefetch<T>(i, D, r, s);
+    vcol[i] = p.hv;
+    flags[i] = p.f;
+    thl[i] = p.th;
+    acl[i] = p.ac;
   }
   __syncthreads();
   const int64_t units = np / D;
@@ -210,18 +239,39 @@ __device__ void block_step_update(double* __restrict__ tot, int64_t np, int D, c
   }
 }
 
+// LDS of one reduction block: red[kRedThreads] doubles, then gl / vcol (E doubles each), thl / acl (E T each,
+// MODE_STEP), flags (E ints); red_lds_bytes(E) in all
+template <typename T>
+struct RedLds {
+  double* red;
+  double* gl;
+  double* vcol;
+  T* thl;
+  T* acl;
+  int* flags;
+  __device__ static RedLds at(unsigned char* base, int E) {
+    RedLds l;
+    l.red = reinterpret_cast<double*>(base);
+    l.gl = l.red + kRedThreads;
+    l.vcol = l.gl + E;
+    l.thl = reinterpret_cast<T*>(l.vcol + E);
+    l.acl = l.thl + E;
+    l.flags = reinterpret_cast<int*>(l.acl + E);
+    return l;
+  }
+};
+template <typename T>
+__host__ __device__ constexpr size_t red_lds_bytes(int E) {
+  return (size_t)kRedThreads * 8 + (size_t)E * (16 + 2 * sizeof(T) + 4);
+}
+
+// Reduction block `bid` of the grid described in the file comment, any block size >= 64 (the entry sums are fixed
+// trees of kRedThreads virtual lanes, block_sums). Returns after its last store; no grid synchronisation.
 template <typename T, int MODE>
-__global__ __launch_bounds__(kRedThreads) void grad_reduce_kernel(ReduceArgs r, StepArgs s) {
-  __shared__ double red[kRedThreads];
-  __shared__ double gl[kRedMaxEntries];
-  __shared__ double vcol[kRedMaxEntries];
-  __shared__ T thl[MODE == MODE_STEP ? kRedMaxEntries : 1];
-  __shared__ T acl[MODE == MODE_STEP ? kRedMaxEntries : 1];
-  __shared__ int flags[kRedMaxEntries];  // MODE_STEP: bit 0 trainable, bit 1 normalised column
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int kWaves = kRedThreads / 64;
+__device__ __forceinline__ void reduce_block(const ReduceArgs& r, const StepArgs& s, int bid, const RedLds<T>& L) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, NT = blockDim.x, nw = NT >> 6;
   const int64_t n = 1 + (int64_t)r.nparams;
-  if (blockIdx.x == 0) {  // the loss entry: one wave
+  if (bid == 0) {  // the loss entry: one wave
     if (tid < 64) {
       double v;
       if (r.nblocks == 1) {
@@ -244,10 +294,15 @@ __global__ __launch_bounds__(kRedThreads) void grad_reduce_kernel(ReduceArgs r, 
   }
   const int D = r.D;
   const int64_t units = r.nparams / D;
-  const int64_t u0 = (int64_t)(blockIdx.x - 1) * r.upb;
+  const int64_t u0 = (int64_t)(bid - 1) * r.upb;
   const int64_t u1 = u0 + r.upb < units ? u0 + r.upb : units;
   const int64_t e0 = u0 * D;  // first gradient entry of the block
   const int E = (int)((u1 - u0) * D);
+  double* __restrict__ gl = L.gl;
+  double* __restrict__ vcol = L.vcol;
+  T* __restrict__ thl = L.thl;
+  T* __restrict__ acl = L.acl;
+  int* __restrict__ flags = L.flags;
   // What does not depend on the sums is loaded first, into registers (one entry per thread when E <= the block's
   // threads), so its round trip overlaps the sums' loads: the Householder columns, theta and the ADAGrad state.
   auto prefetch = [&](int i, double& hv, T& thv, T& acv, int& f) {
@@ -277,31 +332,31 @@ __global__ __launch_bounds__(kRedThreads) void grad_reduce_kernel(ReduceArgs r, 
     }
   };
   if constexpr (MODE == MODE_SUM) {
-    block_sums(r, 1 + e0, E, gl, red);
-  } else if (E <= kRedThreads) {  // (block-uniform) the prefetched values are staged after the sums' loads
+    block_sums(r, 1 + e0, E, gl, L.red);
+  } else if (E <= NT) {  // (block-uniform) the prefetched values are staged after the sums' loads
     double hv = 0.0;
     T thv = (T)0, acv = (T)0;
     int f = 0;
     if (tid < E) prefetch(tid, hv, thv, acv, f);
-    block_sums(r, 1 + e0, E, gl, red);
+    block_sums(r, 1 + e0, E, gl, L.red);
     if (tid < E) stage(tid, hv, thv, acv, f);
   } else {
-    for (int i = tid; i < E; i += kRedThreads) {
+    for (int i = tid; i < E; i += NT) {
       double hv;
       T thv, acv;
       int f;
       prefetch(i, hv, thv, acv, f);
       stage(i, hv, thv, acv, f);
     }
-    block_sums(r, 1 + e0, E, gl, red);
+    block_sums(r, 1 + e0, E, gl, L.red);
   }
   if constexpr (MODE == MODE_SUM) {
-    for (int i = tid; i < E; i += kRedThreads) r.tot[1 + e0 + i] = gl[i];
+    for (int i = tid; i < E; i += NT) r.tot[1 + e0 + i] = gl[i];
     return;
   }
   __syncthreads();  // (the staged values)
   // Householder direction projection, one wave per column unit
-  for (int64_t u = u0 + wave; u < u1; u += kWaves) {
+  for (int64_t u = u0 + wave; u < u1; u += nw) {
     if (unit_householder(r, u * D) < 0) continue;  // wave-uniform
     const int o = (int)((u - u0) * D);
     project_column(gl + o, vcol + o, D, lane);
@@ -310,26 +365,33 @@ __global__ __launch_bounds__(kRedThreads) void grad_reduce_kernel(ReduceArgs r, 
   if constexpr (MODE == MODE_OUT) {
     T* out = (T*)r.out;
     const int64_t base = r.skip_loss ? 0 : 1;
-    for (int i = tid; i < E; i += kRedThreads) out[base + e0 + i] += (T)gl[i];
+    for (int i = tid; i < E; i += NT) out[base + e0 + i] += (T)gl[i];
     return;
   }
   if constexpr (MODE == MODE_STEP) {
-    for (int i = tid; i < E; i += kRedThreads)
+    for (int i = tid; i < E; i += NT)
       if (flags[i] & 1) adagrad_update<T>(thl[i], acl[i], (T)gl[i], (T)s.scale, (T)s.eta, (T)s.eps);
     __syncthreads();
-    for (int64_t u = u0 + wave; u < u1; u += kWaves) {
+    for (int64_t u = u0 + wave; u < u1; u += nw) {
       const int o = (int)((u - u0) * D);
       if (flags[o] & 2) normalize_lds<T>(thl + o, D, lane);  // wave-uniform
     }
     __syncthreads();
     T* th = (T*)s.theta;
     T* ac = (T*)s.acc;
-    for (int i = tid; i < E; i += kRedThreads) {
+    for (int i = tid; i < E; i += NT) {
       const int f = flags[i];
       if (f) th[e0 + i] = thl[i];
       if (f & 1) ac[e0 + i] = acl[i];
     }
   }
+}
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(kRedThreads) void grad_reduce_kernel(ReduceArgs r, StepArgs s) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[red_lds_bytes<T>(kRedMaxEntries)];
+  const int upb_e = r.D * r.upb;  // entries of a full block
+  reduce_block<T, MODE>(r, s, blockIdx.x, RedLds<T>::at(lds, upb_e));
 }
 
 }  // namespace enf

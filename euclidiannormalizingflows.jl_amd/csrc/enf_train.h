@@ -70,13 +70,27 @@ __device__ __forceinline__ void adagrad_update(T& p, T& acc, T g, T scale, T eta
   p = p - dx * eta / (sqrt(a) + eps);
 }
 
+// The sum over a wave's lanes of values held as d = lane, lane + 64, ... < D (lanes >= D hold zeros): the xor
+// tree from half the smallest power of two >= min(D, 64) down; the strides it leaves out would only add zeros, so
+// the value is that of the full 64-lane tree (round 5: 1 stage instead of 6 at D = 2). Every lane < D gets it.
+__device__ __forceinline__ double lane_sum(double v, int64_t D) {
+  int m = 32;
+  if (D < 64) {
+    m = 1;
+    while (m < D) m <<= 1;
+    m >>= 1;
+  }
+  for (; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
 // LinearAlgebra.normalize! of one column by one wave (src/householder_trafo.jl:135-139), the sum
 // of squares in double.
 template <typename T>
 __device__ __forceinline__ void normalize_column(T* __restrict__ v, int64_t D, int lane) {
   double ss = 0.0;
   for (int64_t d = lane; d < D; d += 64) ss += (double)v[d] * (double)v[d];
-  for (int m = 32; m >= 1; m >>= 1) ss += __shfl_xor(ss, m);
+  ss = lane_sum(ss, D);
   const T inv = (T)(1.0 / sqrt(ss));
   for (int64_t d = lane; d < D; d += 64) v[d] *= inv;
 }
