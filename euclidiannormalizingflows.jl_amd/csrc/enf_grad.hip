@@ -161,25 +161,35 @@ __host__ __device__ constexpr int rec_nparams(int op, bool fast) {
          (fast ? rec_extra(op) : 0);
 }
 
-// the row constants of a step, from its parameters just written to the record r (value q of the row at r[q V]);
-// the same double operations as the per-element expressions they replace
+// the row constants of a step, from its parameters just written to the record r (value q of the row at r[q V]).
+// Round 5: on the table log / exp64_in / div64 of the in-range forms where their arguments allow (ocml's exp and log
+// otherwise): the ocml forms made this pass ~40 % of the examples' block prologue (profiles/r05/small_ts_v5.txt).
+__device__ __forceinline__ double gx_log_abs(double v, const double* __restrict__ tab) {
+  const double a = fabs(v);
+  return (a >= 1e-300 && a <= 1e300) ? log64_tab(a, 0, tab) : log(a);
+}
+__device__ __forceinline__ double gx_exp(double w) { return fabs(w) <= 700.0 ? exp64_in(w) : exp(w); }
+__device__ __forceinline__ double gx_rcp(double d) {
+  return (fabs(d) >= 1e-300 && fabs(d) <= 1e300) ? div64(1.0, d) : 1.0 / d;
+}
 template <int V>
-__device__ __forceinline__ void rec_extra_store(int op, double* r) {
+__device__ __forceinline__ void rec_extra_store(int op, double* r, const double* __restrict__ tab) {
   if (op == OP_SCALESHIFT) {
     const double a = r[0];
-    r[2 * V] = log(fabs(a));
-    r[3 * V] = 1.0 / a;
+    r[2 * V] = gx_log_abs(a, tab);
+    r[3 * V] = gx_rcp(a);
   } else if (op == OP_JOHNSON) {
     const double dl = r[V], lm = r[3 * V];
-    r[4 * V] = 1.0 / lm;
-    r[5 * V] = 1.0 / dl;
-    r[6 * V] = log(fabs(dl / lm));
+    const double il = gx_rcp(lm);
+    r[4 * V] = il;
+    r[5 * V] = gx_rcp(dl);
+    r[6 * V] = gx_log_abs(dl / lm, tab);
   } else if (op == OP_CENTER_STRETCH || op == OP_CENTER_CONTRACT) {
     const double a = r[0], b = r[V];
-    r[3 * V] = exp(b * a);
-    r[4 * V] = exp(-b * a);
-    r[5 * V] = exp(2.0 * b * a);
-    r[6 * V] = 1.0 / b;
+    r[3 * V] = gx_exp(b * a);
+    r[4 * V] = gx_exp(-b * a);
+    r[5 * V] = gx_exp(2.0 * b * a);
+    r[6 * V] = gx_rcp(b);
   }
 }
 
@@ -490,11 +500,14 @@ __device__ __forceinline__ bool bwd_fast_step(const double (&xin)[V], const doub
 // STEP (round 5): the single-block fused optimize_whitening step -- the grid is one block, and instead of writing
 // its partial row the block sums its waves into LDS and runs the update itself (block_step_update): one launch per
 // minibatch step where the two-launch path costs two kernel boundaries (the examples' B = 100 / 1000 steps).
-template <typename T, int D, bool VJP, bool STEP = false>
+// VL (round 5): values per lane other than the default -- VL = 1 for fp64 D = 2 batches of at most 256 columns (the
+// 2-D example's B = 100): one row per lane, so a column's two elements run on two lanes instead of one after the
+// other in a single lane, and the batch's one block has twice the waves (make_plan grad_vl).
+template <typename T, int D, bool VJP, bool STEP = false, int VL = 0>
 __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceArgs* rs, const StepArgs* ss) {
   // values per lane: one 16-byte fragment, or D/64 rows when a column needs more than 64 fragments (round 4:
   // kernel rows up to 1024, a column then spans the whole wave)
-  constexpr int V = grad_lane_values<T>(D);
+  constexpr int V = VL ? VL : grad_lane_values<T>(D);
   constexpr int G = D >= V ? D / V : 1;
   constexpr int CPF = D >= V ? 1 : V / D;
   constexpr int SEG = D >= V ? V : D;
@@ -524,15 +537,16 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
   // Records, layout [group][param][element] as the forward kernel (RV = V), in three passes (round 5: ONE round of
   // global loads, where the step-by-step loop waited for each step's parameters, and each thread of a reflection
   // loaded the whole column for its v'v):
-  //   (A) every raw parameter value of every step, an (entry, parameter) item per thread and step, all the steps'
-  //       loads in flight together (one_round; a larger flow loops);
+  //   (A) every raw parameter value of every step: one (step, parameter) pair per wave at a time, lanes on the
+  //       entries, up to four pairs per wave loaded before any is stored (a larger flow loops);
   //   (B) the reflections' v'v in double, one wave per Householder step (its lanes, then the xor tree);
   //   (C) vh = v sqrt(2/v'v) (householder_trafo.jl:9-10) and, FAST, the row constants (rec_extra).
   const int nent = D > V ? D : V;
   const int NT = blockDim.x;
-  auto raw_item = [&](int s, int k, T& v) -> int {  // the raw value of item k of step s, and its record index
-    const int op = a.op[s], np = grad_nparams(op), rn = rec_nparams(op, FAST);
-    const int i = k / np, q = k - i * np;
+  // the raw value of parameter q of entry i of step s, and its record index (s and q wave-uniform: the parameter
+  // pointer is a scalar)
+  auto raw_item = [&](int s, int i, int q, T& v) -> int {
+    const int op = a.op[s], rn = rec_nparams(op, FAST);
     const int g = D >= V ? i / V : 0, e = i % V;
     const int row = D >= V ? i : e % D;
     if (row >= a.D) {
@@ -550,28 +564,48 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
     }
     return a.roff[s] + (g * rn + q) * V + e;
   };
-  bool one_round = true;
-  for (int s = 0; s < a.nsteps; ++s) one_round = one_round && nent * grad_nparams(a.op[s]) <= NT;
-  if (one_round) {
-    T buf[kMaxGradSteps];
-    int ix[kMaxGradSteps];
+  // (A) item j = the j-th (step, parameter) pair: wave w takes items w, w + nw, ... with its lanes on the entries;
+  // up to four items per wave are loaded before any is stored
+  {
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    int nitems = 0;
+    for (int s = 0; s < a.nsteps; ++s) nitems += grad_nparams(a.op[s]);
+    if (nent <= 64 && nitems <= 4 * nw) {
+      T vb[4];
+      int ib[4];
 #pragma unroll
-    for (int s = 0; s < kMaxGradSteps; ++s) {
-      ix[s] = -1;
-      if (s < a.nsteps && tid < nent * grad_nparams(a.op[s])) ix[s] = raw_item(s, tid, buf[s]);
-    }
-#pragma unroll
-    for (int s = 0; s < kMaxGradSteps; ++s)
-      if (ix[s] >= 0) rec[ix[s]] = buf[s];
-  } else {
-    for (int s = 0; s < a.nsteps; ++s)
-      for (int k = tid; k < nent * grad_nparams(a.op[s]); k += NT) {
-        T v;
-        const int ix = raw_item(s, k, v);
-        rec[ix] = v;
+      for (int m = 0; m < 4; ++m) {
+        ib[m] = -1;
+        const int j = wv + m * nw;
+        if (j < nitems) {
+          int s = 0, q = j;
+          while (q >= grad_nparams(a.op[s])) {
+            q -= grad_nparams(a.op[s]);
+            ++s;
+          }
+          if (lane < nent) ib[m] = raw_item(s, lane, q, vb[m]);
+        }
       }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        if (ib[m] >= 0) rec[ib[m]] = vb[m];
+    } else {
+      int j = 0;
+      for (int s = 0; s < a.nsteps; ++s)
+        for (int q = 0; q < grad_nparams(a.op[s]); ++q, ++j) {
+          if (j % nw != wv) continue;
+          for (int i = lane; i < nent; i += 64) {
+            T v;
+            const int ix = raw_item(s, i, q, v);
+            rec[ix] = v;
+          }
+        }
+    }
   }
   __syncthreads();
+#if ENF_DIAG
+  const long long tsA = STEP && a.diag_ts ? (long long)clock64() : 0;
+#endif
   // (B) into wave 0's activation area (not used before the tiles)
   double* hsc = reinterpret_cast<double*>(rec + ((nrec + 3) / 4) * 4);
   for (int s = wave; s < a.nsteps; s += nw) {
@@ -587,6 +621,9 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
     if (lane == 0) hsc[s] = sqrt(2.0 / vv);
   }
   __syncthreads();
+#if ENF_DIAG
+  const long long tsB = STEP && a.diag_ts ? (long long)clock64() : 0;
+#endif
   // (C)
   for (int s = 0; s < a.nsteps; ++s) {
     const int op = a.op[s];
@@ -599,7 +636,7 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
       if (hh) {
         r[0] = (T)((double)r[0] * hsc[s]);
       } else if constexpr (FAST) {
-        rec_extra_store<V>(op, (double*)r);
+        rec_extra_store<V>(op, (double*)r, ltab);
       }
     }
   }
@@ -826,8 +863,8 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
       __syncthreads();
       const long long ts4 = (long long)clock64();
       if (tid == 0)
-        printf("ENF_SMALL_TS prologue %lld tiles %lld partials %lld update %lld (shader clocks)\n", ts1 - ts0,
-               ts2 - ts1, ts3 - ts2, ts4 - ts3);
+        printf("ENF_SMALL_TS prologue %lld (loads %lld, v'v %lld, records %lld) tiles %lld partials %lld update %lld "
+               "(shader clocks)\n", ts1 - ts0, tsA - ts0, tsB - tsA, ts1 - tsB, ts2 - ts1, ts3 - ts2, ts4 - ts3);
     }
 #endif
     return;
@@ -848,14 +885,14 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
   }
 }
 
-template <typename T, int D, bool VJP>
+template <typename T, int D, bool VJP, int VL = 0>
 __global__ __launch_bounds__(512) void negll_grad_kernel(GradArgs a) {
-  negll_grad_impl<T, D, VJP, false>(a, nullptr, nullptr);
+  negll_grad_impl<T, D, VJP, false, VL>(a, nullptr, nullptr);
 }
 
-template <typename T, int D>
+template <typename T, int D, int VL = 0>
 __global__ __launch_bounds__(512) void whitening_step_small_kernel(GradArgs a, ReduceArgs r, StepArgs s) {
-  negll_grad_impl<T, D, false, true>(a, &r, &s);
+  negll_grad_impl<T, D, false, true, VL>(a, &r, &s);
 }
 static_assert(sizeof(GradArgs) + sizeof(ReduceArgs) + sizeof(StepArgs) <= 4096, "kernel arguments over 4 KB");
 
@@ -892,6 +929,7 @@ struct Plan {
   int blocks = 0;   // blocks (partial rows) of the generic kernel
   int ws_rows = 0;  // partial rows the workspace reserves: the generic kernel's or the fused (J o H)^n kernel's
   int nw = 4;  // waves per block of the generic kernel
+  int vl = 0;  // values per lane other than the default (negll_grad_impl VL): 1 for fp64 D = 2 batches of <= 256 columns
 };
 
 // Kernel rows Dp (D rounded up to a power of two) up to 1024: up to 256 fp32 / 128 fp64 a column is a group of
@@ -918,7 +956,9 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
     return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: D must be <= 1024");
   if (nlayers > kMaxGradLayers) return set_error(ENF_ERR_UNSUPPORTED, "enf_flow_negll_grad: more than 16 layers");
   const int64_t Dp = grad_Dp(D);
-  const int V = f64 ? grad_lane_values<double>((int)Dp) : grad_lane_values<float>((int)Dp);
+  // one row per lane for fp64 D = 2 batches that then still fit one block (<= kSmallMaxWaves tiles of 32 columns)
+  P.vl = (f64 && Dp == 2 && N <= 32 * kSmallMaxWaves) ? 1 : 0;
+  const int V = P.vl ? P.vl : f64 ? grad_lane_values<double>((int)Dp) : grad_lane_values<float>((int)Dp);
   const int nent = (int)(Dp > V ? Dp : V);
   const bool fast = f64 && Dp <= kFastMaxD;  // grad_fast_rows: the row constants in the records, the log table
   int s = 0, goff = 0, roff = 0;
@@ -1041,21 +1081,27 @@ void plan_bind_workspace(Plan& P, void* workspace) {
 }
 double* plan_ctot_slot(const Plan& P) { return P.ra.tot + 1 + P.ga.nparams; }
 
-template <typename T, int DD, bool VJP>
+template <typename T, int DD, bool VJP, int VL = 0>
 hipError_t launch_grad_D(const Plan& P, hipStream_t st) {
+  if constexpr (VL == 0 && DD == 2 && std::is_same_v<T, double>) {
+    if (P.vl == 1) return launch_grad_D<T, DD, VJP, 1>(P, st);
+  }
   if (P.lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)negll_grad_kernel<T, DD, VJP>,
+    hipError_t e = hipFuncSetAttribute((const void*)negll_grad_kernel<T, DD, VJP, VL>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((negll_grad_kernel<T, DD, VJP>), dim3(P.blocks), dim3(64 * P.nw), P.lds, st, P.ga);
+  hipLaunchKernelGGL((negll_grad_kernel<T, DD, VJP, VL>), dim3(P.blocks), dim3(64 * P.nw), P.lds, st, P.ga);
   return hipGetLastError();
 }
 
-template <typename T, int DD>
+template <typename T, int DD, int VL = 0>
 hipError_t launch_step_small_D(const Plan& P, const StepArgs& sa, hipStream_t st) {
+  if constexpr (VL == 0 && DD == 2 && std::is_same_v<T, double>) {
+    if (P.vl == 1) return launch_step_small_D<T, DD, 1>(P, sa, st);
+  }
   if (P.small_lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)whitening_step_small_kernel<T, DD>,
+    hipError_t e = hipFuncSetAttribute((const void*)whitening_step_small_kernel<T, DD, VL>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.small_lds);
     if (e != hipSuccess) return e;
   }
@@ -1064,11 +1110,13 @@ hipError_t launch_step_small_D(const Plan& P, const StepArgs& sa, hipStream_t st
   if (ts) {
     GradArgs ga = P.ga;
     ga.diag_ts = 1;
-    hipLaunchKernelGGL((whitening_step_small_kernel<T, DD>), dim3(1), dim3(64 * P.nw), P.small_lds, st, ga, P.ra, sa);
+    hipLaunchKernelGGL((whitening_step_small_kernel<T, DD, VL>), dim3(1), dim3(64 * P.nw), P.small_lds, st, ga, P.ra,
+                       sa);
     return hipGetLastError();
   }
 #endif
-  hipLaunchKernelGGL((whitening_step_small_kernel<T, DD>), dim3(1), dim3(64 * P.nw), P.small_lds, st, P.ga, P.ra, sa);
+  hipLaunchKernelGGL((whitening_step_small_kernel<T, DD, VL>), dim3(1), dim3(64 * P.nw), P.small_lds, st, P.ga, P.ra,
+                     sa);
   return hipGetLastError();
 }
 
