@@ -29,7 +29,7 @@ EXPORTED = (
     "enf_adagrad_step", "enf_householder_normalize", "enf_householder_normalize_strided", "enf_comm_unique_id", "enf_comm_init",
     "enf_comm_destroy", "enf_allreduce_sum", "enf_johnsonsu_eval", "enf_johnsonsu_sample",
     "enf_whitening_step", "enf_whitening_apply", "enf_flow_vjp", "enf_flow_apply_cpu", "enf_whitening_step_dp",
-    "enf_stream_copy",
+    "enf_stream_copy", "enf_whitening_epoch",
 )
 
 
@@ -86,6 +86,8 @@ _SIGS = {
     "enf_allreduce_sum": (ctypes.c_int, [_vp, _vp, _i64, ctypes.c_int, _vp]),
     "enf_whitening_step": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _vp, _i64, ctypes.POINTER(Layer), _i32, _vp, _vp,
                                           _vp, _i32, _vp, _i32, _dbl, _dbl, _vp, _vp, _sz, _vp]),
+    "enf_whitening_epoch": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _vp, _i64, _i64, ctypes.POINTER(Layer), _i32, _vp,
+                                           _vp, _vp, _i32, _vp, _i32, _dbl, _dbl, _vp, _vp, _sz, _vp]),
     "enf_whitening_apply": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _i32, _dbl,
                                            _dbl, _vp, _vp]),
     "enf_whitening_step_dp": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _vp, _i64, ctypes.POINTER(Layer), _i32, _vp,

@@ -634,6 +634,24 @@ enf_status enf_whitening_step(enf_dtype dtype, int64_t D, int64_t N, const void*
   ENF_CATCH
 }
 
+enf_status enf_whitening_epoch(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx, int64_t batchsize,
+                               const enf_layer* layers, int32_t nlayers, void* theta, void* acc, const int64_t* runs,
+                               int32_t nruns, const int64_t* hbatches, int32_t nhb, double eta, double epsilon,
+                               double* loss_out, void* workspace, size_t workspace_bytes, void* hip_stream) {
+  ENF_TRY
+  if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
+  if (D < 1 || N < 1 || batchsize < 1) return fail(ENF_ERR_INVALID, "D, N and batchsize must be >= 1");
+  if (ldx < D) return fail(ENF_ERR_INVALID, "ldx < D");
+  enf_status vs = validate_layers(D, layers, nlayers);
+  if (vs != ENF_OK) return vs;
+  if (!X || !theta || !acc || !loss_out) return fail(ENF_ERR_INVALID, "X, theta, acc or loss_out is NULL");
+  if ((nruns > 0 && !runs) || (nhb > 0 && !hbatches)) return fail(ENF_ERR_INVALID, "runs or hbatches is NULL");
+  return enf::whitening_epoch(dtype == ENF_F64, D, N, X, ldx, batchsize, layers, nlayers, theta, acc, runs, nruns,
+                              hbatches, nhb, eta, epsilon, loss_out, workspace, workspace_bytes,
+                              (hipStream_t)hip_stream);
+  ENF_CATCH
+}
+
 enf_status enf_whitening_apply(enf_dtype dtype, int64_t D, int64_t nparams, const void* g, int64_t B, void* theta,
                                void* acc, const int64_t* runs, int32_t nruns, const int64_t* hbatches, int32_t nhb,
                                double eta, double epsilon, double* loss_out, void* hip_stream) {

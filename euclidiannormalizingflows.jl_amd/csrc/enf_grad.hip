@@ -503,8 +503,19 @@ __device__ __forceinline__ bool bwd_fast_step(const double (&xin)[V], const doub
 // VL (round 5): values per lane other than the default -- VL = 1 for fp64 D = 2 batches of at most 256 columns (the
 // 2-D example's B = 100): one row per lane, so a column's two elements run on two lanes instead of one after the
 // other in a single lane, and the batch's one block has twice the waves (make_plan grad_vl).
+// The minibatch a launch of negll_grad_impl processes: its columns (X, N) and, for the one-block step, where its
+// loss goes and its ADAGrad gradient scale 1/B (the GradArgs / StepArgs values, or the epoch kernel's j-th batch).
+struct BatchCtx {
+  const void* X;
+  int64_t N;
+  double* loss_out;
+  int64_t nsamp;
+  double scale;
+};
+
 template <typename T, int D, bool VJP, bool STEP = false, int VL = 0>
-__device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceArgs* rs, const StepArgs* ss) {
+__device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceArgs* rs, const StepArgs* ss,
+                                                const BatchCtx& bc) {
   // values per lane: one 16-byte fragment, or D/64 rows when a column needs more than 64 fragments (round 4:
   // kernel rows up to 1024, a column then spans the whole wave)
   constexpr int V = VL ? VL : grad_lane_values<T>(D);
@@ -624,13 +635,14 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
 #if ENF_DIAG
   const long long tsB = STEP && a.diag_ts ? (long long)clock64() : 0;
 #endif
-  // (C)
-  for (int s = 0; s < a.nsteps; ++s) {
+  // (C) one (step, entry) item per thread: the steps' constants are computed side by side, not one step after another
+  for (int it = tid; it < a.nsteps * nent; it += NT) {
+    const int s = it / nent, i = it - s * nent;
     const int op = a.op[s];
     const bool hh = op == OP_HOUSEHOLDER;
-    if (!hh && !(FAST && rec_extra(op) > 0)) continue;  // uniform
+    if (!hh && !(FAST && rec_extra(op) > 0)) continue;
     const int rn = rec_nparams(op, FAST);
-    for (int i = tid; i < nent; i += NT) {
+    {
       const int g = D >= V ? i / V : 0, e = i % V;
       T* r = rec + a.roff[s] + g * rn * V + e;
       if (hh) {
@@ -655,7 +667,7 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
   }
   const int r0 = D >= V ? V * (lane % G) : 0;
   const int grp = D >= V ? lane % G : 0;
-  const int64_t ntiles = (a.N + COLS - 1) / COLS;
+  const int64_t ntiles = (bc.N + COLS - 1) / COLS;
   double lossp = 0.0;
   for (int64_t t = (int64_t)blockIdx.x * nw + wave; t < ntiles; t += (int64_t)gridDim.x * nw) {
     const int64_t c0 = t * COLS + (lane / G) * CPF;
@@ -664,8 +676,8 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       const int64_t c = c0 + e / SEG;
-      valid[e] = c < a.N;
-      x[e] = (valid[e] && r0 + e % SEG < a.D) ? ((const T*)a.X)[c * a.ldx + r0 + e % SEG] : (T)0;
+      valid[e] = c < bc.N;
+      x[e] = (valid[e] && r0 + e % SEG < a.D) ? ((const T*)bc.X)[c * a.ldx + r0 + e % SEG] : (T)0;
     }
     // ---- forward, storing each step's input
     T lad[CPF];
@@ -857,7 +869,7 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
 #if ENF_DIAG
     const long long ts3 = a.diag_ts ? (long long)clock64() : 0;
 #endif
-    block_step_update<T>(tot, a.nparams, a.D, *rs, *ss, scratch, pre, have_pre);
+    block_step_update<T>(tot, a.nparams, a.D, *rs, *ss, scratch, pre, have_pre, bc.loss_out, bc.nsamp, bc.scale);
 #if ENF_DIAG
     if (a.diag_ts) {  // (uniform)
       __syncthreads();
@@ -887,14 +899,34 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
 
 template <typename T, int D, bool VJP, int VL = 0>
 __global__ __launch_bounds__(512) void negll_grad_kernel(GradArgs a) {
-  negll_grad_impl<T, D, VJP, false, VL>(a, nullptr, nullptr);
+  negll_grad_impl<T, D, VJP, false, VL>(a, nullptr, nullptr, BatchCtx{a.X, a.N, nullptr, 0, 0.0});
 }
 
 template <typename T, int D, int VL = 0>
 __global__ __launch_bounds__(512) void whitening_step_small_kernel(GradArgs a, ReduceArgs r, StepArgs s) {
-  negll_grad_impl<T, D, false, true, VL>(a, &r, &s);
+  negll_grad_impl<T, D, false, true, VL>(a, &r, &s, BatchCtx{a.X, a.N, s.loss_out, s.nsamp, s.scale});
 }
-static_assert(sizeof(GradArgs) + sizeof(ReduceArgs) + sizeof(StepArgs) <= 4096, "kernel arguments over 4 KB");
+
+// The single-rank steps of a whole epoch in ONE launch (round 5, enf_whitening_epoch): a minibatch that fits one
+// block never needs a second block, so the block walks the minibatches [b0, b0 + bs) of the N columns in order
+// (src/optimize_whitening.jl:31-42, Iterators.partition), each step exactly as whitening_step_small_kernel, with
+// the parameters it updated visible to its next step's prologue after a workgroup fence and a barrier -- no launch
+// per step (the examples' per-step boundary cost) and no device-wide synchronisation. Step j's loss to
+// s.loss_out[j].
+template <typename T, int D, int VL = 0>
+__global__ __launch_bounds__(512) void whitening_epoch_small_kernel(GradArgs a, ReduceArgs r, StepArgs s, int64_t N,
+                                                                    int64_t bs) {
+  int64_t j = 0;
+  for (int64_t b0 = 0; b0 < N; b0 += bs, ++j) {
+    const int64_t B = N - b0 < bs ? N - b0 : bs;
+    negll_grad_impl<T, D, false, true, VL>(
+        a, &r, &s, BatchCtx{(const T*)a.X + b0 * a.ldx, B, s.loss_out + j, B, 1.0 / (double)B});
+    __threadfence_block();  // this step's theta / ADAGrad stores before the next step's prologue reads them
+    __syncthreads();
+  }
+}
+static_assert(sizeof(GradArgs) + sizeof(ReduceArgs) + sizeof(StepArgs) + 2 * sizeof(int64_t) <= 4096,
+              "kernel arguments over 4 KB");
 
 // The update half of a data-parallel step (enf_whitening_apply): the same loss / ADAGrad /
 // re-normalisation as whitening_tail_kernel, reading the cross-rank sum g (1 + nparams values of T,
@@ -1130,6 +1162,31 @@ hipError_t launch_step_small(const Plan& P, const StepArgs& sa, hipStream_t st) 
   }
 }
 
+template <typename T, int DD, int VL = 0>
+hipError_t launch_epoch_small_D(const Plan& P, const StepArgs& sa, int64_t N, int64_t bs, hipStream_t st) {
+  if constexpr (VL == 0 && DD == 2 && std::is_same_v<T, double>) {
+    if (P.vl == 1) return launch_epoch_small_D<T, DD, 1>(P, sa, N, bs, st);
+  }
+  if (P.small_lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)whitening_epoch_small_kernel<T, DD, VL>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.small_lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((whitening_epoch_small_kernel<T, DD, VL>), dim3(1), dim3(64 * P.nw), P.small_lds, st, P.ga, P.ra,
+                     sa, N, bs);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_epoch_small(const Plan& P, const StepArgs& sa, int64_t N, int64_t bs, hipStream_t st) {
+  switch (P.ga.Dp) {
+#define ENF_E(DD) case DD: return launch_epoch_small_D<T, DD>(P, sa, N, bs, st);
+    ENF_E(1) ENF_E(2) ENF_E(4) ENF_E(8) ENF_E(16) ENF_E(32) ENF_E(64) ENF_E(128) ENF_E(256) ENF_E(512) ENF_E(1024)
+#undef ENF_E
+    default: return hipErrorInvalidValue;
+  }
+}
+
 template <typename T, bool VJP = false>
 hipError_t launch_grad(const Plan& P, hipStream_t st) {
   hipError_t e0 = hipSuccess;
@@ -1266,16 +1323,11 @@ enf_status whitening_apply(bool f64, int64_t D, int64_t nparams, const void* g, 
 }
 
 namespace {
-// B: the global batch size the update normalises by (N on one rank); ar: the cross-rank sum of this rank's
-// totals (1 + nparams doubles, MODE_SUM) between the gradient and the update (enf_whitening_step_dp), or none
-enf_status whitening_step_single(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
-                                 int32_t nlayers, void* theta, void* acc, const int64_t* runs, int32_t nruns,
-                                 const int64_t* hb, int32_t nhb, double eta, double epsilon, double* loss_out,
-                                 void* workspace, size_t workspace_bytes, hipStream_t st, int64_t B, AllreduceFn ar,
-                                 void* ar_ctx) {
+// StepArgs of a single-rank step and their checks against the flow's parameter count np
+enf_status step_args(int64_t D, void* theta, void* acc, const int64_t* runs, int32_t nruns, const int64_t* hb,
+                     int32_t nhb, double eta, double epsilon, double* loss_out, int64_t B, int64_t np, StepArgs& a) {
   if (nruns < 0 || nruns > kMaxStepRuns || nhb < 0 || nhb > kMaxStepHB)
     return set_error(ENF_ERR_UNSUPPORTED, "enf_whitening_step: too many parameter runs or Householder batches");
-  StepArgs a;
   std::memset(&a, 0, sizeof a);
   a.theta = theta;
   a.acc = acc;
@@ -1290,23 +1342,34 @@ enf_status whitening_step_single(bool f64, int64_t D, int64_t N, const void* X, 
   for (int i = 0; i < nruns; ++i) {
     a.runs[i][0] = runs[2 * i];
     a.runs[i][1] = runs[2 * i + 1];
-  }
-  for (int i = 0; i < nhb; ++i)
-    for (int q = 0; q < 3; ++q) a.hb[i][q] = hb[3 * i + q];
-  Plan P;
-  enf_status s = make_plan(f64, D, N > 0 ? N : 1, layers, nlayers, P);
-  if (s != ENF_OK) return s;
-  for (int i = 0; i < nruns; ++i)
-    if (a.runs[i][0] < 0 || a.runs[i][1] < a.runs[i][0] || a.runs[i][1] > P.ga.nparams)
+    if (a.runs[i][0] < 0 || a.runs[i][1] < a.runs[i][0] || a.runs[i][1] > np)
       return set_error(ENF_ERR_INVALID, "enf_whitening_step: parameter run outside theta");
+  }
   for (int i = 0; i < nhb; ++i) {
+    for (int q = 0; q < 3; ++q) a.hb[i][q] = hb[3 * i + q];
     if (a.hb[i][0] < 0 || a.hb[i][1] < 0 || a.hb[i][2] < D ||
-        (a.hb[i][1] > 0 && a.hb[i][0] + (a.hb[i][1] - 1) * a.hb[i][2] + D > P.ga.nparams))
+        (a.hb[i][1] > 0 && a.hb[i][0] + (a.hb[i][1] - 1) * a.hb[i][2] + D > np))
       return set_error(ENF_ERR_INVALID, "enf_whitening_step: Householder batch outside theta");
     // (each column is one D-entry vector of the parameter layout: the reduction re-normalises it where it updates it)
     if (a.hb[i][0] % D != 0 || a.hb[i][2] % D != 0)
       return set_error(ENF_ERR_INVALID, "enf_whitening_step: Householder batch columns must start at multiples of D");
   }
+  return ENF_OK;
+}
+
+// B: the global batch size the update normalises by (N on one rank); ar: the cross-rank sum of this rank's
+// totals (1 + nparams doubles, MODE_SUM) between the gradient and the update (enf_whitening_step_dp), or none
+enf_status whitening_step_single(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
+                                 int32_t nlayers, void* theta, void* acc, const int64_t* runs, int32_t nruns,
+                                 const int64_t* hb, int32_t nhb, double eta, double epsilon, double* loss_out,
+                                 void* workspace, size_t workspace_bytes, hipStream_t st, int64_t B, AllreduceFn ar,
+                                 void* ar_ctx) {
+  Plan P;
+  enf_status s = make_plan(f64, D, N > 0 ? N : 1, layers, nlayers, P);
+  if (s != ENF_OK) return s;
+  StepArgs a;
+  s = step_args(D, theta, acc, runs, nruns, hb, nhb, eta, epsilon, loss_out, B, P.ga.nparams, a);
+  if (s != ENF_OK) return s;
   const size_t n1 = 1 + (size_t)P.ga.nparams;
   // one rank, a batch of one block, not the fused (J o H)^n kernel: gradient and update in ONE launch (round 5)
   static const int small_ok = ENF_KNOB("ENF_STEP_SMALL", 1);
@@ -1620,6 +1683,56 @@ enf_status whitening_step_dp(bool f64, int64_t D, int64_t N, const void* X, int6
     if (s != ENF_OK) return s;
   }
   return whitening_apply(f64, D, np, ws + w.g, B, theta, acc, runs, nruns, hb, nhb, eta, epsilon, loss_out, st);
+}
+
+// The single-rank steps of one epoch (enf_whitening_epoch): the minibatches [b0, b0 + bs) of the N columns in order,
+// step j's loss to loss_out[j]. While the batches fit the one-launch step (whitening_step_single's small-batch
+// path), all of them run in ONE launch of whitening_epoch_small_kernel -- the same arithmetic step by step, so the
+// result is enf_whitening_step's, bit for bit; a last, shorter batch with another layout and every other flow take
+// enf_whitening_step's path, one call per batch.
+enf_status whitening_epoch(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, int64_t bs,
+                           const enf_layer* layers, int32_t nlayers, void* theta, void* acc, const int64_t* runs,
+                           int32_t nruns, const int64_t* hb, int32_t nhb, double eta, double epsilon, double* loss_out,
+                           void* workspace, size_t workspace_bytes, hipStream_t st) {
+  if (N < 1 || bs < 1) return set_error(ENF_ERR_INVALID, "enf_whitening_epoch: N and batchsize must be >= 1");
+  if (bs > N) bs = N;
+  const size_t esz = f64 ? 8 : 4;
+  const int64_t nb = (N + bs - 1) / bs;
+  int64_t done = 0;  // batches run by the epoch kernel
+  static const int epoch_ok = ENF_KNOB("ENF_EPOCH_KERNEL", 1);
+  if (epoch_ok && fits_one_launch(f64, D, bs, layers, nlayers) && (f64 || !hj_grad_eligible(D, ldx, X, layers, nlayers))) {
+    Plan P;
+    enf_status s = make_plan(f64, D, bs, layers, nlayers, P);
+    if (s != ENF_OK) return s;
+    if (P.blocks == 1 && P.small_lds <= kGradLdsMax) {
+      int64_t ncols = (N / bs) * bs;
+      if (N > ncols) {  // the last batch in the same launch when its own plan has the same layout
+        Plan Q;
+        s = make_plan(f64, D, N - ncols, layers, nlayers, Q);
+        if (s != ENF_OK) return s;
+        if (Q.blocks == 1 && Q.vl == P.vl && Q.nw == P.nw) ncols = N;
+      }
+      StepArgs a;
+      s = step_args(D, theta, acc, runs, nruns, hb, nhb, eta, epsilon, loss_out, bs, P.ga.nparams, a);
+      if (s != ENF_OK) return s;
+      P.ga.X = X;
+      P.ga.ldx = ldx;
+      P.ga.partial = nullptr;
+      if (ncols > 0) {
+        hipError_t e = f64 ? launch_epoch_small<double>(P, a, ncols, bs, st) : launch_epoch_small<float>(P, a, ncols, bs, st);
+        if (e != hipSuccess) return set_error(ENF_ERR_HIP, hipGetErrorString(e));
+      }
+      done = (ncols + bs - 1) / bs;
+    }
+  }
+  for (int64_t j = done; j < nb; ++j) {
+    const int64_t b0 = j * bs, B = N - b0 < bs ? N - b0 : bs;
+    enf_status s = whitening_step_dp(f64, D, B, (const char*)X + (size_t)b0 * (size_t)ldx * esz, ldx, layers, nlayers,
+                                     theta, acc, runs, nruns, hb, nhb, eta, epsilon, B, loss_out + j, nullptr, nullptr,
+                                     workspace, workspace_bytes, st);
+    if (s != ENF_OK) return s;
+  }
+  return ENF_OK;
 }
 
 }  // namespace enf

@@ -200,18 +200,20 @@ __device__ __forceinline__ StepPre<T> step_prefetch(int64_t i, int D, const Redu
   return p;
 }
 
-// pre: this thread's step_prefetch(threadIdx.x) when have_pre (np <= blockDim.x), else loaded here
+// pre: this thread's step_prefetch(threadIdx.x) when have_pre (np <= blockDim.x), else loaded here. loss_out, nsamp
+// and scale: this minibatch's (s.loss_out / s.nsamp / s.scale for one step; the epoch kernel's j-th batch).
 template <typename T>
 __device__ __forceinline__ void block_step_update(double* __restrict__ tot, int64_t np, int D, const ReduceArgs& r,
                                                   const StepArgs& s, unsigned char* __restrict__ scratch,
-                                                  const StepPre<T>& pre, bool have_pre) {
+                                                  const StepPre<T>& pre, bool have_pre, double* loss_out,
+                                                  int64_t nsamp, double scale) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6, NT = blockDim.x;
   double* vcol = reinterpret_cast<double*>(scratch);
   T* thl = reinterpret_cast<T*>(vcol + np);
   T* acl = thl + np;
   int* flags = reinterpret_cast<int*>(acl + np);
   double* gl = tot + 1;
-  if (tid == 0) *s.loss_out = (double)((T)tot[0] / (T)s.nsamp);
+  if (tid == 0) *loss_out = (double)((T)tot[0] / (T)nsamp);
   for (int64_t i = tid; i < np; i += NT) {
     const StepPre<T> p = have_pre ? pre : step_prefetch<T>(i, D, r, s);
     vcol[i] = p.hv;
@@ -225,7 +227,7 @@ __device__ __forceinline__ void block_step_update(double* __restrict__ tot, int6
     if (unit_householder(r, u * D) >= 0) project_column(gl + u * D, vcol + u * D, D, lane);  // wave-uniform
   __syncthreads();
   for (int64_t i = tid; i < np; i += NT)
-    if (flags[i] & 1) adagrad_update<T>(thl[i], acl[i], (T)gl[i], (T)s.scale, (T)s.eta, (T)s.eps);
+    if (flags[i] & 1) adagrad_update<T>(thl[i], acl[i], (T)gl[i], (T)scale, (T)s.eta, (T)s.eps);
   __syncthreads();
   for (int64_t u = wave; u < units; u += nw)
     if (flags[u * D] & 2) normalize_lds<T>(thl + u * D, D, lane);  // wave-uniform

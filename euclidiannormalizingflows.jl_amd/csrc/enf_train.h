@@ -51,6 +51,11 @@ enf_status whitening_step_dp(bool f64, int64_t D, int64_t N, const void* X, int6
                              int32_t nlayers, void* theta, void* acc, const int64_t* runs, int32_t nruns,
                              const int64_t* hb, int32_t nhb, double eta, double epsilon, int64_t B, double* loss_out,
                              AllreduceFn ar, void* ar_ctx, void* workspace, size_t workspace_bytes, hipStream_t st);
+// The single-rank steps of one epoch over the minibatches [b0, b0 + bs) of N columns (enf_whitening_epoch)
+enf_status whitening_epoch(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, int64_t bs,
+                           const enf_layer* layers, int32_t nlayers, void* theta, void* acc, const int64_t* runs,
+                           int32_t nruns, const int64_t* hb, int32_t nhb, double eta, double epsilon, double* loss_out,
+                           void* workspace, size_t workspace_bytes, hipStream_t st);
 // Update half of a data-parallel step after the all-reduce (enf_whitening_apply): g = 1 + nparams
 // summed values of T, B = global batch size.
 enf_status whitening_apply(bool f64, int64_t D, int64_t nparams, const void* g, int64_t B, void* theta, void* acc,

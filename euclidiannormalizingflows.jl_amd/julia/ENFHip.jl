@@ -471,7 +471,20 @@ function optimize_whitening(smpls::HipMatrix{T}, initial_trafo::Function, optimi
     fused = world == 1 && isempty(tied) && limits_ok
     s = 0
     GC.@preserve X theta acc layers runs hb ws hist out zero_out begin
-        for _ in 1:nepochs, b0 in starts
+        if fused  # one rank: each epoch in ONE call (enf_whitening_epoch: one launch for one-block minibatches)
+            for _ in 1:nepochs
+                loss_ptr = Ptr{Cdouble}(hist.buf.ptr + s * sizeof(Float64))
+                check(ccall((:enf_whitening_epoch, libenf), Cint,
+                            (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Int64, Ptr{EnfLayer}, Int32, Ptr{Cvoid}, Ptr{Cvoid},
+                             Ptr{Int64}, Int32, Ptr{Int64}, Int32, Cdouble, Cdouble, Ptr{Cdouble}, Ptr{Cvoid},
+                             Csize_t, Ptr{Cvoid}),
+                            _dt(R), D, N, X.buf.ptr, D, batchsize, layers, length(layers), theta.buf.ptr,
+                            acc.buf.ptr, runs, length(runs) ÷ 2, hb, length(hb) ÷ 3, rule.eta, rule.epsilon,
+                            loss_ptr, ws.ptr, ws.bytes, C_NULL))
+                s += length(starts)
+            end
+        end
+        for _ in 1:(fused ? 0 : nepochs), b0 in starts
             B = min(b0 + batchsize, N) - b0
             lo, hi = b0 + (B * rank) ÷ world, b0 + (B * (rank + 1)) ÷ world
             loss_ptr = Ptr{Cdouble}(hist.buf.ptr + s * sizeof(Float64))

@@ -363,7 +363,8 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
                        negll_history: Optional[List[float]] = None, process_group=None,
                        similar_fill_quirk: bool = False, graph: bool = False, comm=None,
                        data_parallel: bool = False,
-                       _dp_step: bool = False, _separate_update: bool = False) -> WhiteningResult:
+                       _dp_step: bool = False, _separate_update: bool = False,
+                       _per_step: bool = False) -> WhiteningResult:
     """src/optimize_whitening.jl:25-45 on the device (see module docstring). similar_fill_quirk=True
     records the negll the reference records under Zygote (ScaleShiftTrafo's primal ladj taken as 0,
     src/abstract_trafo.jl:30-33: + sum log|a| per sample); the updates are the same either way.
@@ -382,9 +383,13 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
     loop (same kernels in the same order). With several ranks this needs comm= (the RCCL all-reduce
     is captured into the graph); a torch.distributed group stays eager.
 
+    One rank (round 5): each epoch is ONE enf_whitening_epoch call -- a single launch when the minibatches fit the
+    one-launch step (the reference examples' B = 100 / 1000 at D <= 2), else the per-step path inside the library.
+
     Test hooks: _dp_step=True runs the data-parallel step (gradient, all-reduce, enf_whitening_apply)
     on one rank; _separate_update=True replaces enf_whitening_apply by the separate
-    enf_adagrad_step / enf_householder_normalize_strided calls (identical arithmetic)."""
+    enf_adagrad_step / enf_householder_normalize_strided calls (identical arithmetic); _per_step=True
+    runs one enf_whitening_step call per minibatch instead of enf_whitening_epoch (identical arithmetic)."""
     import torch.distributed as dist
 
     M, _, _ = _to_device_matrix(smpls)
@@ -424,6 +429,14 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
         fused = False
     def one_epoch(hbuf: torch.Tensor, stream: int) -> None:
         """Enqueue the steps of one epoch on `stream`; the loss of step j goes to hbuf[j]."""
+        if fused and not similar_fill_quirk and not _per_step:
+            # the whole epoch in one call (enf_whitening_epoch: one launch when the minibatches fit the one-launch
+            # step, else enf_whitening_step per batch; the same result bit for bit)
+            _lib.check(L.enf_whitening_epoch(
+                dt, D, N, M.data_ptr(), _ld(M), batchsize, state.layers(), len(state.trafos), state.theta.data_ptr(),
+                state.acc.data_ptr(), runs.ctypes.data, len(segs), hbs.ctypes.data, len(hbatches), optimizer.eta,
+                optimizer.epsilon, hbuf.data_ptr(), ws.data_ptr(), ws.numel() * 8, stream))
+            return
         for j, (B, lo, hi) in enumerate(plan):
             if fused and hi > lo:
                 q = []

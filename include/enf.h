@@ -195,6 +195,18 @@ enf_status enf_whitening_step(enf_dtype dtype, int64_t D, int64_t N, const void*
                               const int64_t* runs, int32_t nruns, const int64_t* hbatches, int32_t nhb,
                               double eta, double epsilon, double* loss_out, void* workspace,
                               size_t workspace_bytes, void* hip_stream);
+/* The single-GPU optimize_whitening steps of ONE EPOCH (src/optimize_whitening.jl:31-42: the minibatches
+ * Iterators.partition(1:N, batchsize) in order, each an enf_whitening_step): step j covers columns
+ * [j*batchsize, min((j+1)*batchsize, N)) of X and writes its loss to loss_out[j] (device, ceil(N/batchsize) doubles).
+ * Identical arithmetic to that sequence of enf_whitening_step calls, bit for bit. Round 5: while a minibatch fits the
+ * one-launch step (a batch of one gradient block, e.g. the reference examples' B = 100 / 1000 at D <= 2), the whole
+ * epoch is ONE launch -- one block walks the minibatches, no launch per step; other flows and batch sizes run the
+ * per-step path. workspace: enf_flow_negll_grad_workspace(batchsize) bytes. */
+enf_status enf_whitening_epoch(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx, int64_t batchsize,
+                               const enf_layer* layers, int32_t nlayers, void* theta, void* acc,
+                               const int64_t* runs, int32_t nruns, const int64_t* hbatches, int32_t nhb,
+                               double eta, double epsilon, double* loss_out, void* workspace,
+                               size_t workspace_bytes, void* hip_stream);
 /* The update half of a DATA-PARALLEL optimize_whitening minibatch step (src/optimize_whitening.jl:38-41),
  * run on every rank after the cross-GPU sum (enf_allreduce_sum / RCCL) of enf_flow_negll_grad's out
  * buffer g (1 + nparams values of the dtype, nparams = enf_flow_param_count): *loss_out = g[0] / B

@@ -208,3 +208,93 @@ def test_examples_training_vs_oracle(enf, gpu, oracle, example):
     assert np.allclose(hist, hist_ref, rtol=1e-9, atol=0), np.abs(hist - hist_ref).max()
     th = r.optimizer_state.theta.cpu().numpy()
     assert np.allclose(th, th_ref, rtol=1e-9, atol=1e-12), np.abs(th - th_ref).max()
+
+
+def _example_flows(example, rng):
+    if example == "1d":
+        init = [(2, [np.array([0.0]), np.array([1.0]), np.array([0.0])]),
+                (3, [np.array([0.0]), np.array([5.0]), np.array([0.0]), np.array([5.0])]),
+                (2, [np.array([0.0]), np.array([1.0]), np.array([0.0])]),
+                (3, [np.array([0.0]), np.array([5.0]), np.array([0.0]), np.array([5.0])])]
+        return 1, init
+    init = [(0, [np.array([1.0, 1.0]), np.array([0.0, 0.0])]),
+            (5, [rng.standard_normal(2)]),
+            (2, [np.array([0.0, 0.0]), np.array([1.0, 1.0]), np.array([0.0, 0.0])])]
+    return 2, init
+
+
+@pytest.mark.parametrize("case", ["1d_B1000", "2d_B100", "2d_ragged", "f64_D5_multiblock", "hj_f32"])
+def test_whitening_epoch_equals_steps(enf, gpu, case):
+    """enf_whitening_epoch (round 5: an epoch of one-block minibatch steps in ONE launch, the batches walked by one
+    block; other flows / sizes on the per-step path) equals the sequence of enf_whitening_step calls over the same
+    minibatches bit for bit: parameters, ADAGrad state and every step's loss, over two epochs. Cases: the reference
+    examples' flows at their batch sizes (the single-launch path; 2d takes the one-row-per-lane layout), a ragged
+    last batch with another layout (mixed path), a multi-block fp64 flow and the fused fp32 (J o H)^2 kernel
+    (per-step path inside the call)."""
+    import torch
+
+    from euclidiannormalizingflows_jl_amd import _lib
+    from euclidiannormalizingflows_jl_amd.train import FlowState, _workspace, householder_batches, trainable_runs
+
+    rng = np.random.default_rng(5600)
+    if case in ("1d_B1000", "2d_B100", "2d_ragged"):
+        D, layers = _example_flows(case[:2], rng)
+        dtype = np.float64
+        N, bs = {"1d_B1000": (5000, 1000), "2d_B100": (1000, 100), "2d_ragged": (1000, 300)}[case]
+    elif case == "f64_D5_multiblock":
+        D, dtype, N, bs = 5, np.float64, 6000, 2000
+        layers = [(0, rand_params(rng, 0, D, dtype)), (5, rand_params(rng, 5, D, dtype)),
+                  (3, rand_params(rng, 3, D, dtype)), (2, rand_params(rng, 2, D, dtype))]
+    else:
+        D, dtype, N, bs = 32, np.float32, 40_000, 10_000
+        layers = []
+        for _ in range(2):
+            layers += [(5, rand_params(rng, 5, D, dtype)), (3, rand_params(rng, 3, D, dtype))]
+    X = colmajor_cuda((0.8 * rng.standard_normal((D, N))).astype(dtype))
+    f = make_flow(enf, layers)
+    tdt = torch.float64 if dtype == np.float64 else torch.float32
+    L = _lib.lib()
+    dt = _lib.ENF_F64 if dtype == np.float64 else _lib.ENF_F32
+    opt = enf.ADAGrad()
+    sa, sb = [FlowState(f, D, tdt, X.device, opt) for _ in range(2)]
+    segs = trainable_runs(sa)
+    hb = householder_batches(sa)
+    runs = np.ascontiguousarray(np.array(segs, dtype=np.int64).reshape(-1))
+    hbs = np.ascontiguousarray(np.array(hb, dtype=np.int64).reshape(-1))
+    nb = (N + bs - 1) // bs
+    ws = _workspace(sa, bs)
+    la = torch.zeros(nb, dtype=torch.float64, device=X.device)
+    lb = torch.zeros(nb, dtype=torch.float64, device=X.device)
+    esz = 8 if dtype == np.float64 else 4
+    for ep in range(2):
+        _lib.check(L.enf_whitening_epoch(dt, D, N, X.data_ptr(), X.stride(1), bs, sa.layers(), len(sa.trafos),
+                                         sa.theta.data_ptr(), sa.acc.data_ptr(), runs.ctypes.data, len(segs),
+                                         hbs.ctypes.data, len(hb), opt.eta, opt.epsilon, la.data_ptr(), ws.data_ptr(),
+                                         ws.numel() * 8, None))
+        for j in range(nb):
+            b0 = j * bs
+            B = min(bs, N - b0)
+            _lib.check(L.enf_whitening_step(dt, D, B, X.data_ptr() + b0 * X.stride(1) * esz, X.stride(1), sb.layers(),
+                                            len(sb.trafos), sb.theta.data_ptr(), sb.acc.data_ptr(), runs.ctypes.data,
+                                            len(segs), hbs.ctypes.data, len(hb), opt.eta, opt.epsilon,
+                                            lb[j:].data_ptr(), ws.data_ptr(), ws.numel() * 8, None))
+        torch.cuda.synchronize()
+        assert torch.equal(la, lb), (ep, (la - lb).abs().max())
+        assert torch.equal(sa.theta, sb.theta), ep
+        assert torch.equal(sa.acc, sb.acc), ep
+    assert torch.isfinite(la).all()
+
+
+def test_optimize_whitening_epoch_equals_per_step(enf, gpu):
+    """optimize_whitening on one rank (each epoch one enf_whitening_epoch call) equals the per-step loop
+    (_per_step=True) bit for bit, eager and graph-captured, on the 2-D example's flow."""
+    rng = np.random.default_rng(5700)
+    D, init = _example_flows("2d", rng)
+    X = colmajor_cuda(np.asfortranarray(rng.standard_normal((D, 3000))))
+    res = []
+    for kw in ({}, {"_per_step": True}, {"graph": True}):
+        r = enf.optimize_whitening(X, make_flow(enf, init), enf.ADAGrad(), nbatches=30, nepochs=3, **kw)
+        res.append((r.optimizer_state.theta.cpu().numpy(), r.optimizer_state.acc.cpu().numpy(),
+                    np.asarray(r.negll_history)))
+    for t, a, h in res[1:]:
+        assert np.array_equal(res[0][0], t) and np.array_equal(res[0][1], a) and np.array_equal(res[0][2], h)

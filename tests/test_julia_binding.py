@@ -139,7 +139,7 @@ def test_every_ccall_matches_the_header():
 def test_the_binding_covers_the_compute_entry_points():
     bound = {c[0] for c in julia_ccalls()}
     for sym in ("enf_flow_apply", "enf_flow_apply_host", "enf_flow_param_count", "enf_flow_negll_grad_workspace",
-                "enf_flow_negll_grad", "enf_whitening_step", "enf_whitening_apply", "enf_johnsonsu_eval",
+                "enf_flow_negll_grad", "enf_whitening_step", "enf_whitening_epoch", "enf_whitening_apply", "enf_johnsonsu_eval",
                 "enf_johnsonsu_sample", "enf_comm_unique_id", "enf_comm_init", "enf_comm_destroy",
                 "enf_allreduce_sum", "enf_malloc", "enf_free", "enf_memcpy", "enf_last_error", "enf_flow_vjp"):
         assert sym in bound, sym

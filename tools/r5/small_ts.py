@@ -31,6 +31,6 @@ for ex in sys.argv[1:] or ["2d", "1d"]:
          5: lambda ps: enf.HouseholderTrafo(ps[0])}[op](ps) for op, ps in reversed(layers)])
     Xd = torch.from_numpy(np.ascontiguousarray(np.asarray(X).T)).to(dev).t()
     print(f"== example {ex}: D={D} B={B}", flush=True)
-    enf.optimize_whitening(Xd, mk(init), enf.ADAGrad(), nbatches=20, nepochs=1, graph=False)
+    enf.optimize_whitening(Xd, mk(init), enf.ADAGrad(), nbatches=20, nepochs=1, graph=False, _per_step=True)
     torch.cuda.synchronize()
     sys.stdout.flush()
