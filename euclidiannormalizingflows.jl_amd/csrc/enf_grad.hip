@@ -30,6 +30,7 @@
 #include <cstdint>
 #include <algorithm>
 #include <cstring>
+#include <initializer_list>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -503,6 +504,22 @@ __device__ __forceinline__ bool bwd_fast_step(const double (&xin)[V], const doub
 // VL (round 5): values per lane other than the default -- VL = 1 for fp64 D = 2 batches of at most 256 columns (the
 // 2-D example's B = 100): one row per lane, so a column's two elements run on two lanes instead of one after the
 // other in a single lane, and the batch's one block has twice the waves (make_plan grad_vl).
+// A compiled step sequence (round 5): the op of every step known at compile time, so the step loops unroll, each
+// step's op-dependent code is selected at compile time and its descriptors (offsets, parameter pointers) are loaded
+// once instead of per step. OpProg<> is the step-table interpreter (ops read from GradArgs at run time). Used for the
+// reference examples' flows at their dimension (make_plan grad_prog).
+template <int... Ops>
+struct OpProg {
+  static constexpr int n = (int)sizeof...(Ops);
+  __host__ __device__ static constexpr int at(int s) {
+    constexpr int ops[] = {Ops..., -1};
+    return ops[s];
+  }
+};
+using ProgInterp = OpProg<>;
+using ProgExample1d = OpProg<OP_CENTER_CONTRACT, OP_JOHNSON, OP_CENTER_CONTRACT, OP_JOHNSON>;  // nf_example_1d.jl:23-24
+using ProgExample2d = OpProg<OP_SCALESHIFT, OP_HOUSEHOLDER, OP_CENTER_CONTRACT>;                // nf_example_2d.jl:25-27
+
 // The minibatch a launch of negll_grad_impl processes: its columns (X, N) and, for the one-block step, where its
 // loss goes and its ADAGrad gradient scale 1/B (the GradArgs / StepArgs values, or the epoch kernel's j-th batch).
 struct BatchCtx {
@@ -513,7 +530,7 @@ struct BatchCtx {
   double scale;
 };
 
-template <typename T, int D, bool VJP, bool STEP = false, int VL = 0>
+template <typename T, int D, bool VJP, bool STEP = false, int VL = 0, class Prog = ProgInterp>
 __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceArgs* rs, const StepArgs* ss,
                                                 const BatchCtx& bc) {
   // values per lane: one 16-byte fragment, or D/64 rows when a column needs more than 64 fragments (round 4:
@@ -683,11 +700,10 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
     T lad[CPF];
 #pragma unroll
     for (int c = 0; c < CPF; ++c) lad[c] = (T)0;
-    for (int s = 0; s < a.nsteps; ++s) {
+    auto fwd_step = [&](const int s, const int op) {
       T* as = act + s * 64 * V + lane * V;
 #pragma unroll
       for (int e = 0; e < V; ++e) as[e] = x[e];
-      const int op = a.op[s];
       const T* r = rec + a.roff[s] + grp * rec_nparams(op, FAST) * V;
       if (op == OP_HOUSEHOLDER) {
 #pragma unroll
@@ -725,6 +741,12 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
           }
         }
       }
+    };
+    if constexpr (Prog::n > 0) {
+#pragma unroll
+      for (int s = 0; s < Prog::n; ++s) fwd_step(s, Prog::at(s));
+    } else {
+      for (int s = 0; s < a.nsteps; ++s) fwd_step(s, a.op[s]);
     }
     T yfin[V];  // the flow's output (the last step's output for the backward's in-range forms)
 #pragma unroll
@@ -757,12 +779,12 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
 #pragma unroll
       for (int e = 0; e < V; ++e) g[e] = valid[e] ? x[e] : (T)0;
     }
-    for (int s = a.nsteps - 1; s >= 0; --s) {
+    const int nst = Prog::n > 0 ? Prog::n : a.nsteps;
+    auto bwd_step = [&](const int s, const int op) {
       const T* as = act + s * 64 * V + lane * V;
       T xin[V];
 #pragma unroll
       for (int e = 0; e < V; ++e) xin[e] = as[e];
-      const int op = a.op[s];
       const int np = grad_nparams(op);
       const T* r = rec + a.roff[s] + grp * rec_nparams(op, FAST) * V;
       if (op == OP_HOUSEHOLDER) {
@@ -793,7 +815,7 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
         {
           const T* an = act + (s + 1) * 64 * V + lane * V;
 #pragma unroll
-          for (int e = 0; e < V; ++e) yout[e] = s + 1 < a.nsteps ? an[e] : yfin[e];
+          for (int e = 0; e < V; ++e) yout[e] = s + 1 < nst ? an[e] : yfin[e];
         }
         bool done = false;
         if constexpr (FAST) {
@@ -832,6 +854,12 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
           }
         }
       }
+    };
+    if constexpr (Prog::n > 0) {
+#pragma unroll
+      for (int s = Prog::n - 1; s >= 0; --s) bwd_step(s, Prog::at(s));
+    } else {
+      for (int s = a.nsteps - 1; s >= 0; --s) bwd_step(s, a.op[s]);
     }
     if constexpr (VJP) {  // dX = the cotangent after the first step
 #pragma unroll
@@ -902,9 +930,9 @@ __global__ __launch_bounds__(512) void negll_grad_kernel(GradArgs a) {
   negll_grad_impl<T, D, VJP, false, VL>(a, nullptr, nullptr, BatchCtx{a.X, a.N, nullptr, 0, 0.0});
 }
 
-template <typename T, int D, int VL = 0>
+template <typename T, int D, int VL = 0, class Prog = ProgInterp>
 __global__ __launch_bounds__(512) void whitening_step_small_kernel(GradArgs a, ReduceArgs r, StepArgs s) {
-  negll_grad_impl<T, D, false, true, VL>(a, &r, &s, BatchCtx{a.X, a.N, s.loss_out, s.nsamp, s.scale});
+  negll_grad_impl<T, D, false, true, VL, Prog>(a, &r, &s, BatchCtx{a.X, a.N, s.loss_out, s.nsamp, s.scale});
 }
 
 // The single-rank steps of a whole epoch in ONE launch (round 5, enf_whitening_epoch): a minibatch that fits one
@@ -913,13 +941,13 @@ __global__ __launch_bounds__(512) void whitening_step_small_kernel(GradArgs a, R
 // the parameters it updated visible to its next step's prologue after a workgroup fence and a barrier -- no launch
 // per step (the examples' per-step boundary cost) and no device-wide synchronisation. Step j's loss to
 // s.loss_out[j].
-template <typename T, int D, int VL = 0>
+template <typename T, int D, int VL = 0, class Prog = ProgInterp>
 __global__ __launch_bounds__(512) void whitening_epoch_small_kernel(GradArgs a, ReduceArgs r, StepArgs s, int64_t N,
                                                                     int64_t bs) {
   int64_t j = 0;
   for (int64_t b0 = 0; b0 < N; b0 += bs, ++j) {
     const int64_t B = N - b0 < bs ? N - b0 : bs;
-    negll_grad_impl<T, D, false, true, VL>(
+    negll_grad_impl<T, D, false, true, VL, Prog>(
         a, &r, &s, BatchCtx{(const T*)a.X + b0 * a.ldx, B, s.loss_out + j, B, 1.0 / (double)B});
     __threadfence_block();  // this step's theta / ADAGrad stores before the next step's prologue reads them
     __syncthreads();
@@ -962,6 +990,7 @@ struct Plan {
   int ws_rows = 0;  // partial rows the workspace reserves: the generic kernel's or the fused (J o H)^n kernel's
   int nw = 4;  // waves per block of the generic kernel
   int vl = 0;  // values per lane other than the default (negll_grad_impl VL): 1 for fp64 D = 2 batches of <= 256 columns
+  int prog = 0;  // one-block steps: 0 = the step-table interpreter, 1 / 2 = the compiled ProgExample1d / 2d
 };
 
 // Kernel rows Dp (D rounded up to a power of two) up to 1024: up to 256 fp32 / 128 fp64 a column is a group of
@@ -1020,6 +1049,17 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
   P.ga.Dp = (int32_t)Dp;
   P.ga.N = N;
   P.ga.nsteps = s;
+  // the reference examples' flows at their dimension run their one-block steps as compiled programs (OpProg)
+  auto ops_are = [&](std::initializer_list<int> ops) {
+    if ((int)ops.size() != s) return false;
+    int i = 0;
+    for (int op : ops)
+      if (P.ga.op[i++] != op) return false;
+    return true;
+  };
+  P.prog = 0;
+  if (f64 && Dp == 1 && P.vl == 0 && ops_are({OP_CENTER_CONTRACT, OP_JOHNSON, OP_CENTER_CONTRACT, OP_JOHNSON})) P.prog = 1;
+  if (f64 && Dp == 2 && P.vl == 1 && ops_are({OP_SCALESHIFT, OP_HOUSEHOLDER, OP_CENTER_CONTRACT})) P.prog = 2;
   P.ga.nlayers = nlayers;
   P.ga.nparams = goff;
   const size_t esz = f64 ? 8 : 4;
@@ -1127,13 +1167,19 @@ hipError_t launch_grad_D(const Plan& P, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <typename T, int DD, int VL = 0>
+template <typename T, int DD, int VL = 0, class Prog = ProgInterp>
 hipError_t launch_step_small_D(const Plan& P, const StepArgs& sa, hipStream_t st) {
-  if constexpr (VL == 0 && DD == 2 && std::is_same_v<T, double>) {
-    if (P.vl == 1) return launch_step_small_D<T, DD, 1>(P, sa, st);
+  if constexpr (VL == 0 && Prog::n == 0 && DD == 2 && std::is_same_v<T, double>) {
+    if (P.vl == 1) {
+      if (P.prog == 2) return launch_step_small_D<T, DD, 1, ProgExample2d>(P, sa, st);
+      return launch_step_small_D<T, DD, 1>(P, sa, st);
+    }
+  }
+  if constexpr (VL == 0 && Prog::n == 0 && DD == 1 && std::is_same_v<T, double>) {
+    if (P.prog == 1) return launch_step_small_D<T, DD, 0, ProgExample1d>(P, sa, st);
   }
   if (P.small_lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)whitening_step_small_kernel<T, DD, VL>,
+    hipError_t e = hipFuncSetAttribute((const void*)whitening_step_small_kernel<T, DD, VL, Prog>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.small_lds);
     if (e != hipSuccess) return e;
   }
@@ -1142,12 +1188,12 @@ hipError_t launch_step_small_D(const Plan& P, const StepArgs& sa, hipStream_t st
   if (ts) {
     GradArgs ga = P.ga;
     ga.diag_ts = 1;
-    hipLaunchKernelGGL((whitening_step_small_kernel<T, DD, VL>), dim3(1), dim3(64 * P.nw), P.small_lds, st, ga, P.ra,
+    hipLaunchKernelGGL((whitening_step_small_kernel<T, DD, VL, Prog>), dim3(1), dim3(64 * P.nw), P.small_lds, st, ga, P.ra,
                        sa);
     return hipGetLastError();
   }
 #endif
-  hipLaunchKernelGGL((whitening_step_small_kernel<T, DD, VL>), dim3(1), dim3(64 * P.nw), P.small_lds, st, P.ga, P.ra,
+  hipLaunchKernelGGL((whitening_step_small_kernel<T, DD, VL, Prog>), dim3(1), dim3(64 * P.nw), P.small_lds, st, P.ga, P.ra,
                      sa);
   return hipGetLastError();
 }
@@ -1162,17 +1208,23 @@ hipError_t launch_step_small(const Plan& P, const StepArgs& sa, hipStream_t st) 
   }
 }
 
-template <typename T, int DD, int VL = 0>
+template <typename T, int DD, int VL = 0, class Prog = ProgInterp>
 hipError_t launch_epoch_small_D(const Plan& P, const StepArgs& sa, int64_t N, int64_t bs, hipStream_t st) {
-  if constexpr (VL == 0 && DD == 2 && std::is_same_v<T, double>) {
-    if (P.vl == 1) return launch_epoch_small_D<T, DD, 1>(P, sa, N, bs, st);
+  if constexpr (VL == 0 && Prog::n == 0 && DD == 2 && std::is_same_v<T, double>) {
+    if (P.vl == 1) {
+      if (P.prog == 2) return launch_epoch_small_D<T, DD, 1, ProgExample2d>(P, sa, N, bs, st);
+      return launch_epoch_small_D<T, DD, 1>(P, sa, N, bs, st);
+    }
+  }
+  if constexpr (VL == 0 && Prog::n == 0 && DD == 1 && std::is_same_v<T, double>) {
+    if (P.prog == 1) return launch_epoch_small_D<T, DD, 0, ProgExample1d>(P, sa, N, bs, st);
   }
   if (P.small_lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)whitening_epoch_small_kernel<T, DD, VL>,
+    hipError_t e = hipFuncSetAttribute((const void*)whitening_epoch_small_kernel<T, DD, VL, Prog>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.small_lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((whitening_epoch_small_kernel<T, DD, VL>), dim3(1), dim3(64 * P.nw), P.small_lds, st, P.ga, P.ra,
+  hipLaunchKernelGGL((whitening_epoch_small_kernel<T, DD, VL, Prog>), dim3(1), dim3(64 * P.nw), P.small_lds, st, P.ga, P.ra,
                      sa, N, bs);
   return hipGetLastError();
 }
