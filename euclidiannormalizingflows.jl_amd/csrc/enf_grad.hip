@@ -519,6 +519,13 @@ struct OpProg {
 using ProgInterp = OpProg<>;
 using ProgExample1d = OpProg<OP_CENTER_CONTRACT, OP_JOHNSON, OP_CENTER_CONTRACT, OP_JOHNSON>;  // nf_example_1d.jl:23-24
 using ProgExample2d = OpProg<OP_SCALESHIFT, OP_HOUSEHOLDER, OP_CENTER_CONTRACT>;                // nf_example_2d.jl:25-27
+// parameter items (step, parameter vector) of a compiled program
+template <class Prog>
+__host__ __device__ constexpr int prog_items() {
+  int n = 0;
+  for (int s = 0; s < Prog::n; ++s) n += grad_nparams(Prog::at(s));
+  return n;
+}
 
 // The minibatch a launch of negll_grad_impl processes: its columns (X, N) and, for the one-block step, where its
 // loss goes and its ADAGrad gradient scale 1/B (the GradArgs / StepArgs values, or the epoch kernel's j-th batch).
@@ -528,6 +535,7 @@ struct BatchCtx {
   double* loss_out;
   int64_t nsamp;
   double scale;
+  bool fill_ltab;  // false: the table log is already in LDS (the epoch kernel's steps after its first)
 };
 
 template <typename T, int D, bool VJP, bool STEP = false, int VL = 0, class Prog = ProgInterp>
@@ -561,7 +569,8 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
 #endif
   for (int i = lane; i < a.nparams; i += 64) gacc[i] = 0.0;
   if constexpr (FAST)
-    for (int i = tid; i < 3 * kLogTabN; i += blockDim.x) ltab[i] = kLogTab[i];
+    if (bc.fill_ltab)
+      for (int i = tid; i < 3 * kLogTabN; i += blockDim.x) ltab[i] = kLogTab[i];
   // Records, layout [group][param][element] as the forward kernel (RV = V), in three passes (round 5: ONE round of
   // global loads, where the step-by-step loop waited for each step's parameters, and each thread of a reflection
   // loaded the whole column for its v'v):
@@ -570,7 +579,6 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
   //   (B) the reflections' v'v in double, one wave per Householder step (its lanes, then the xor tree);
   //   (C) vh = v sqrt(2/v'v) (householder_trafo.jl:9-10) and, FAST, the row constants (rec_extra).
   const int nent = D > V ? D : V;
-  const int NT = blockDim.x;
   // the raw value of parameter q of entry i of step s, and its record index (s and q wave-uniform: the parameter
   // pointer is a scalar)
   auto raw_item = [&](int s, int i, int q, T& v) -> int {
@@ -593,8 +601,34 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
     return a.roff[s] + (g * rn + q) * V + e;
   };
   // (A) item j = the j-th (step, parameter) pair: wave w takes items w, w + nw, ... with its lanes on the entries;
-  // up to four items per wave are loaded before any is stored
-  {
+  // up to four items per wave are loaded before any is stored. A compiled program (one step per layer, column 0)
+  // knows every item's step and parameter at compile time: its loads are independent (one scalar load of the
+  // parameter pointer each, no walk over the step table and no layer indirection) and all are in flight before
+  // the first store.
+  if constexpr (Prog::n > 0) {
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    constexpr int NI = prog_items<Prog>();
+    T vb[NI];
+    int ib[NI];
+    int j = 0;
+#pragma unroll
+    for (int s = 0; s < Prog::n; ++s) {
+      const int op = Prog::at(s), rn = rec_nparams(op, FAST);
+#pragma unroll
+      for (int q = 0; q < grad_nparams(op); ++q, ++j) {
+        ib[j] = -1;
+        if (j % nw == wv && lane < nent) {
+          const int g = D >= V ? lane / V : 0, e = lane % V;
+          const int row = D >= V ? lane : e % D;
+          vb[j] = ((const T*)a.layers[s].p[op == OP_HOUSEHOLDER ? 0 : q])[row];
+          ib[j] = a.roff[s] + (g * rn + q) * V + e;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NI; ++k)
+      if (ib[k] >= 0) rec[ib[k]] = vb[k];
+  } else {
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     int nitems = 0;
     for (int s = 0; s < a.nsteps; ++s) nitems += grad_nparams(a.op[s]);
@@ -634,42 +668,49 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
 #if ENF_DIAG
   const long long tsA = STEP && a.diag_ts ? (long long)clock64() : 0;
 #endif
-  // (B) into wave 0's activation area (not used before the tiles)
-  double* hsc = reinterpret_cast<double*>(rec + ((nrec + 3) / 4) * 4);
-  for (int s = wave; s < a.nsteps; s += nw) {
-    if (a.op[s] != OP_HOUSEHOLDER) continue;  // wave-uniform
-    constexpr int rn = rec_nparams(OP_HOUSEHOLDER, FAST);
-    double vv = 0.0;
-    for (int d = lane; d < a.D; d += 64) {
-      const int g = D >= V ? d / V : 0, e = D >= V ? d % V : d;  // (D < V: entry d holds row d)
-      const double v = (double)rec[a.roff[s] + g * rn * V + e];
-      vv += v * v;
+  // (B) one step per wave (its op wave-uniform, so no lane runs another op's branch): a reflection's v'v in double
+  // over its lanes, then vh = v sqrt(2/v'v) (householder_trafo.jl:9-10) written by the same wave; FAST, the other
+  // steps' row constants (rec_extra) -- the reflections' chains and the exp / log chains run side by side, one
+  // barrier for both
+  auto step_consts = [&](const int s, const int op) {
+    const int rn = rec_nparams(op, FAST);
+    if (op == OP_HOUSEHOLDER) {
+      double vv = 0.0;
+      for (int d = lane; d < a.D; d += 64) {
+        const int g = D >= V ? d / V : 0, e = D >= V ? d % V : d;  // (D < V: entry d holds row d)
+        const double v = (double)rec[a.roff[s] + g * rn * V + e];
+        vv += v * v;
+      }
+      vv = lane_sum(vv, a.D);
+      // lane 0's sum for every lane (lane_sum leaves it in lanes < D; D < V has entries past D)
+      const uint64_t vb = __builtin_bit_cast(uint64_t, vv);
+      vv = __builtin_bit_cast(double, ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(vb >> 32)) << 32) |
+                                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)vb));
+      const double hs = sqrt(2.0 / vv);
+      for (int i = lane; i < nent; i += 64) {
+        T* r = rec + a.roff[s] + (D >= V ? i / V : 0) * rn * V + i % V;
+        r[0] = (T)((double)r[0] * hs);
+      }
+    } else if constexpr (FAST) {
+      if (rec_extra(op) > 0)
+        for (int i = lane; i < nent; i += 64)
+          rec_extra_store<V>(op, (double*)(rec + a.roff[s] + (D >= V ? i / V : 0) * rn * V + i % V), ltab);
     }
-    vv = lane_sum(vv, a.D);
-    if (lane == 0) hsc[s] = sqrt(2.0 / vv);
+  };
+  {
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    if constexpr (Prog::n > 0) {
+#pragma unroll
+      for (int s = 0; s < Prog::n; ++s)
+        if (s % nw == wv) step_consts(s, Prog::at(s));
+    } else {
+      for (int s = wv; s < a.nsteps; s += nw) step_consts(s, a.op[s]);
+    }
   }
   __syncthreads();
 #if ENF_DIAG
-  const long long tsB = STEP && a.diag_ts ? (long long)clock64() : 0;
+  const long long tsB = tsA;
 #endif
-  // (C) one (step, entry) item per thread: the steps' constants are computed side by side, not one step after another
-  for (int it = tid; it < a.nsteps * nent; it += NT) {
-    const int s = it / nent, i = it - s * nent;
-    const int op = a.op[s];
-    const bool hh = op == OP_HOUSEHOLDER;
-    if (!hh && !(FAST && rec_extra(op) > 0)) continue;
-    const int rn = rec_nparams(op, FAST);
-    {
-      const int g = D >= V ? i / V : 0, e = i % V;
-      T* r = rec + a.roff[s] + g * rn * V + e;
-      if (hh) {
-        r[0] = (T)((double)r[0] * hsc[s]);
-      } else if constexpr (FAST) {
-        rec_extra_store<V>(op, (double*)r, ltab);
-      }
-    }
-  }
-  __syncthreads();
 #if ENF_DIAG
   const long long ts1 = STEP && a.diag_ts ? (long long)clock64() : 0;
 #endif
@@ -927,12 +968,12 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
 
 template <typename T, int D, bool VJP, int VL = 0>
 __global__ __launch_bounds__(512) void negll_grad_kernel(GradArgs a) {
-  negll_grad_impl<T, D, VJP, false, VL>(a, nullptr, nullptr, BatchCtx{a.X, a.N, nullptr, 0, 0.0});
+  negll_grad_impl<T, D, VJP, false, VL>(a, nullptr, nullptr, BatchCtx{a.X, a.N, nullptr, 0, 0.0, true});
 }
 
 template <typename T, int D, int VL = 0, class Prog = ProgInterp>
 __global__ __launch_bounds__(512) void whitening_step_small_kernel(GradArgs a, ReduceArgs r, StepArgs s) {
-  negll_grad_impl<T, D, false, true, VL, Prog>(a, &r, &s, BatchCtx{a.X, a.N, s.loss_out, s.nsamp, s.scale});
+  negll_grad_impl<T, D, false, true, VL, Prog>(a, &r, &s, BatchCtx{a.X, a.N, s.loss_out, s.nsamp, s.scale, true});
 }
 
 // The single-rank steps of a whole epoch in ONE launch (round 5, enf_whitening_epoch): a minibatch that fits one
@@ -948,7 +989,7 @@ __global__ __launch_bounds__(512) void whitening_epoch_small_kernel(GradArgs a, 
   for (int64_t b0 = 0; b0 < N; b0 += bs, ++j) {
     const int64_t B = N - b0 < bs ? N - b0 : bs;
     negll_grad_impl<T, D, false, true, VL, Prog>(
-        a, &r, &s, BatchCtx{(const T*)a.X + b0 * a.ldx, B, s.loss_out + j, B, 1.0 / (double)B});
+        a, &r, &s, BatchCtx{(const T*)a.X + b0 * a.ldx, B, s.loss_out + j, B, 1.0 / (double)B, j == 0});
     __threadfence_block();  // this step's theta / ADAGrad stores before the next step's prologue reads them
     __syncthreads();
   }
@@ -1224,6 +1265,16 @@ hipError_t launch_epoch_small_D(const Plan& P, const StepArgs& sa, int64_t N, in
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.small_lds);
     if (e != hipSuccess) return e;
   }
+#if ENF_DIAG
+  static const int ts = ENF_KNOB("ENF_SMALL_TS", 0);
+  if (ts) {
+    GradArgs ga = P.ga;
+    ga.diag_ts = 1;
+    hipLaunchKernelGGL((whitening_epoch_small_kernel<T, DD, VL, Prog>), dim3(1), dim3(64 * P.nw), P.small_lds, st, ga,
+                       P.ra, sa, N, bs);
+    return hipGetLastError();
+  }
+#endif
   hipLaunchKernelGGL((whitening_epoch_small_kernel<T, DD, VL, Prog>), dim3(1), dim3(64 * P.nw), P.small_lds, st, P.ga, P.ra,
                      sa, N, bs);
   return hipGetLastError();

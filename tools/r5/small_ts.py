@@ -1,5 +1,6 @@
 """Phase clocks of the one-block whitening step (diagnostics library, ENF_SMALL_TS=1): the reference examples'
-flows, 20 eager steps each; thread 0 of the kernel prints prologue / tiles / partials / update shader clocks."""
+flows, 20 eager steps each; thread 0 of the kernel prints prologue / tiles / partials / update shader clocks.
+--epoch: the 20 steps as one enf_whitening_epoch launch (one line per step) instead of 20 step launches."""
 import os
 import sys
 
@@ -19,7 +20,8 @@ from enf_pkg import load  # noqa: E402
 enf = load()
 enf._lib.use_diagnostics_library()
 dev = torch.device("cuda", 0)
-for ex in sys.argv[1:] or ["2d", "1d"]:
+epoch = "--epoch" in sys.argv
+for ex in [a for a in sys.argv[1:] if not a.startswith("--")] or ["2d", "1d"]:
     D, true, init, nbatches, _ = bench_train.example_flows(ex)
     B = 100_000 // nbatches
     N = 20 * B
@@ -30,7 +32,7 @@ for ex in sys.argv[1:] or ["2d", "1d"]:
          2: lambda ps: enf.CenterContract(*ps), 3: lambda ps: enf.JohnsonTrafo(*ps),
          5: lambda ps: enf.HouseholderTrafo(ps[0])}[op](ps) for op, ps in reversed(layers)])
     Xd = torch.from_numpy(np.ascontiguousarray(np.asarray(X).T)).to(dev).t()
-    print(f"== example {ex}: D={D} B={B}", flush=True)
-    enf.optimize_whitening(Xd, mk(init), enf.ADAGrad(), nbatches=20, nepochs=1, graph=False, _per_step=True)
+    print(f"== example {ex}: D={D} B={B} {'epoch kernel' if epoch else 'step launches'}", flush=True)
+    enf.optimize_whitening(Xd, mk(init), enf.ADAGrad(), nbatches=20, nepochs=1, graph=False, _per_step=not epoch)
     torch.cuda.synchronize()
     sys.stdout.flush()
