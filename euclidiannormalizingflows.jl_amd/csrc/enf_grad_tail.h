@@ -148,7 +148,25 @@ __device__ __forceinline__ int unit_householder(const ReduceArgs& r, int64_t off
 // dS/dv from the direction sums G of one column (in gl, D entries) and the column v (vc, double):
 //   dS/dw = -sqrt2 G, dS/dv = (dS/dw - w (dS/dw . w)) / |v|, w = v / |v|  (householder_trafo.jl:22-40)
 // by one wave (sums over the lanes: d = lane, lane + 64, ..., then the xor tree).
+// project_lane: the same for D <= 64 with this lane's entry (g, vc) in registers (zeros past the column): the column
+// is the group of lanes the xor tree of lane_sum(., D) spans, so a wave can hold several columns of a power-of-two D
+// side by side (block_step_update), and every caller runs these same operations
+__device__ __forceinline__ double project_lane(double g, double vc, int D) {
+  double vv = 0.0;
+  vv += vc * vc;
+  vv = lane_sum(vv, D);
+  const double nrm = sqrt(vv);
+  double wd = 0.0;
+  wd += -1.4142135623730951 * g * (vc / nrm);
+  wd = lane_sum(wd, D);
+  return (-1.4142135623730951 * g - (vc / nrm) * wd) / nrm;
+}
 __device__ __forceinline__ void project_column(double* __restrict__ g, const double* __restrict__ vc, int D, int lane) {
+  if (D <= 64) {
+    const double r = project_lane(lane < D ? g[lane] : 0.0, lane < D ? vc[lane] : 0.0, D);
+    if (lane < D) g[lane] = r;
+    return;
+  }
   double vv = 0.0;
   for (int d = lane; d < D; d += 64) vv += vc[d] * vc[d];
   vv = lane_sum(vv, D);
@@ -163,7 +181,20 @@ __device__ __forceinline__ void project_column(double* __restrict__ g, const dou
 // squares in double over d = lane, lane + 64, ..., the xor tree, then v *= (T)(1/sqrt) -- normalize_column's
 // arithmetic (enf_train.h), so the separate enf_householder_normalize call rounds the same
 template <typename T>
+__device__ __forceinline__ T normalize_lane(T v, int D) {  // D <= 64, as project_lane
+  double ss = 0.0;
+  ss += (double)v * (double)v;
+  ss = lane_sum(ss, D);
+  const T inv = (T)(1.0 / sqrt(ss));
+  return v * inv;
+}
+template <typename T>
 __device__ __forceinline__ void normalize_lds(T* __restrict__ v, int D, int lane) {
+  if (D <= 64) {
+    const T r = normalize_lane<T>(lane < D ? v[lane] : (T)0, D);
+    if (lane < D) v[lane] = r;
+    return;
+  }
   double ss = 0.0;
   for (int d = lane; d < D; d += 64) ss += (double)v[d] * (double)v[d];
   ss = lane_sum(ss, D);
@@ -214,6 +245,24 @@ __device__ __forceinline__ void block_step_update(double* __restrict__ tot, int6
   int* flags = reinterpret_cast<int*>(acl + np);
   double* gl = tot + 1;
   if (tid == 0) *loss_out = (double)((T)tot[0] / (T)nsamp);
+  if (have_pre && D <= 64 && (D & (D - 1)) == 0) {
+    // a power-of-two D: thread i holds entry i, so the D lanes of a column unit are one group of lane_sum's xor tree
+    // and each unit is finished by its own lanes -- projection, ADAGrad, re-normalisation and the stores -- with the
+    // operations of the phases below, and no block barrier
+    const int64_t i = tid;
+    const bool act = i < np;
+    double g = act ? gl[i] : 0.0;
+    const bool hh = act && unit_householder(r, (i / D) * D) >= 0;
+    const double gp = project_lane(g, pre.hv, D);
+    if (hh) g = gp;
+    T th = pre.th, ac = pre.ac;
+    if (act && (pre.f & 1)) adagrad_update<T>(th, ac, (T)g, (T)scale, (T)s.eta, (T)s.eps);
+    const T tn = normalize_lane<T>(th, D);
+    if (act && (pre.f & 2)) th = tn;
+    if (act && pre.f) ((T*)s.theta)[i] = th;
+    if (act && (pre.f & 1)) ((T*)s.acc)[i] = ac;
+    return;
+  }
   for (int64_t i = tid; i < np; i += NT) {
     const StepPre<T> p = have_pre ? pre : step_prefetch<T>(i, D, r, s);
     vcol[i] = p.hv;
