@@ -929,6 +929,29 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
     }
     const double* g0 = reinterpret_cast<const double*>(smem);
     const int w8 = gbytes / 8;
+    if (step_update_lanes(have_pre, a.D)) {
+      // thread i sums entry i over the waves itself and updates it: no row in LDS, no second barrier
+      double v = 0.0;
+      if (tid < a.nparams) {
+        v = g0[tid];
+        for (int w = 1; w < nw; ++w) v += g0[w * w8 + tid];
+      }
+      if (tid == 0) *bc.loss_out = (double)((T)tot[0] / (T)bc.nsamp);
+#if ENF_DIAG
+      const long long ts3 = a.diag_ts ? (long long)clock64() : 0;
+#endif
+      step_update_lane<T>(v, a.nparams, a.D, *rs, *ss, pre, bc.scale);
+#if ENF_DIAG
+      if (a.diag_ts) {  // (uniform)
+        __syncthreads();
+        const long long ts4 = (long long)clock64();
+        if (tid == 0)
+          printf("ENF_SMALL_TS prologue %lld (loads %lld, v'v %lld, records %lld) tiles %lld partials %lld update %lld "
+                 "(shader clocks)\n", ts1 - ts0, tsA - ts0, tsB - tsA, ts1 - tsB, ts2 - ts1, ts3 - ts2, ts4 - ts3);
+      }
+#endif
+      return;
+    }
     for (int i = tid; i < a.nparams; i += blockDim.x) {
       double v = g0[i];
       for (int w = 1; w < nw; ++w) v += g0[w * w8 + i];

@@ -231,6 +231,27 @@ __device__ __forceinline__ StepPre<T> step_prefetch(int64_t i, int D, const Redu
   return p;
 }
 
+// The update with one entry per thread (entry i = threadIdx.x) for a power-of-two D <= 64 (and np <= the block's
+// threads, have_pre): the D lanes of a column unit are one group of lane_sum's xor tree, so each unit is finished by
+// its own lanes -- projection, ADAGrad, re-normalisation and the stores -- with the operations of
+// block_step_update's phases and no block barrier. g: entry i's gradient sum (0 past np).
+__device__ __forceinline__ bool step_update_lanes(bool have_pre, int D) { return have_pre && D <= 64 && (D & (D - 1)) == 0; }
+template <typename T>
+__device__ __forceinline__ void step_update_lane(double g, int64_t np, int D, const ReduceArgs& r, const StepArgs& s,
+                                                 const StepPre<T>& pre, double scale) {
+  const int64_t i = threadIdx.x;
+  const bool act = i < np;
+  const bool hh = act && unit_householder(r, (i / D) * D) >= 0;
+  const double gp = project_lane(g, pre.hv, D);
+  if (hh) g = gp;
+  T th = pre.th, ac = pre.ac;
+  if (act && (pre.f & 1)) adagrad_update<T>(th, ac, (T)g, (T)scale, (T)s.eta, (T)s.eps);
+  const T tn = normalize_lane<T>(th, D);
+  if (act && (pre.f & 2)) th = tn;
+  if (act && pre.f) ((T*)s.theta)[i] = th;
+  if (act && (pre.f & 1)) ((T*)s.acc)[i] = ac;
+}
+
 // pre: this thread's step_prefetch(threadIdx.x) when have_pre (np <= blockDim.x), else loaded here. loss_out, nsamp
 // and scale: this minibatch's (s.loss_out / s.nsamp / s.scale for one step; the epoch kernel's j-th batch).
 template <typename T>
@@ -245,22 +266,8 @@ __device__ __forceinline__ void block_step_update(double* __restrict__ tot, int6
   int* flags = reinterpret_cast<int*>(acl + np);
   double* gl = tot + 1;
   if (tid == 0) *loss_out = (double)((T)tot[0] / (T)nsamp);
-  if (have_pre && D <= 64 && (D & (D - 1)) == 0) {
-    // a power-of-two D: thread i holds entry i, so the D lanes of a column unit are one group of lane_sum's xor tree
-    // and each unit is finished by its own lanes -- projection, ADAGrad, re-normalisation and the stores -- with the
-    // operations of the phases below, and no block barrier
-    const int64_t i = tid;
-    const bool act = i < np;
-    double g = act ? gl[i] : 0.0;
-    const bool hh = act && unit_householder(r, (i / D) * D) >= 0;
-    const double gp = project_lane(g, pre.hv, D);
-    if (hh) g = gp;
-    T th = pre.th, ac = pre.ac;
-    if (act && (pre.f & 1)) adagrad_update<T>(th, ac, (T)g, (T)scale, (T)s.eta, (T)s.eps);
-    const T tn = normalize_lane<T>(th, D);
-    if (act && (pre.f & 2)) th = tn;
-    if (act && pre.f) ((T*)s.theta)[i] = th;
-    if (act && (pre.f & 1)) ((T*)s.acc)[i] = ac;
+  if (step_update_lanes(have_pre, D)) {
+    step_update_lane<T>(tid < np ? gl[tid] : 0.0, np, D, r, s, pre, scale);
     return;
   }
   for (int64_t i = tid; i < np; i += NT) {
