@@ -100,8 +100,8 @@ __device__ __forceinline__ T gsum(T x) {
   if constexpr (G >= 4) x += gdpp<0x4E>(x);
   if constexpr (G >= 8) x += gdpp<0x141>(x);
   if constexpr (G >= 16) x += gdpp<0x140>(x);
-  if constexpr (G >= 32) x += __shfl_xor(x, 16);
-  if constexpr (G >= 64) x += __shfl_xor(x, 32);
+  if constexpr (G >= 32) x = add_xor_swap<16>(x);
+  if constexpr (G >= 64) x = add_xor_swap<32>(x);
   return x;
 }
 
@@ -131,8 +131,8 @@ __device__ __forceinline__ void wave_accumulate(double* __restrict__ acc, int ro
   if constexpr (G < 4) v += wdpp<0x4E>(v);   // quad_perm(2,3,0,1): lane ^ 2
   if constexpr (G < 8) v += wdpp<0x124>(v);  // row_ror:4
   if constexpr (G < 16) v += wdpp<0x128>(v); // row_ror:8
-  if constexpr (G < 32) v += __shfl_xor(v, 16);
-  if constexpr (G < 64) v += __shfl_xor(v, 32);
+  if constexpr (G < 32) v = add_xor_swap<16>(v);
+  if constexpr (G < 64) v = add_xor_swap<32>(v);
   if (lane < G && row < nrows) acc[row] += (double)v;  // padded rows (row >= D) have no parameter
 }
 
@@ -914,7 +914,7 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
 #if ENF_DIAG
   const long long ts2 = STEP && a.diag_ts ? (long long)clock64() : 0;
 #endif
-  for (int m = 32; m >= 1; m >>= 1) lossp += __shfl_xor(lossp, m);
+  lossp = xor_tree(lossp, 64);  // (the 64-lane xor butterfly)
   if (lane == 0) lossw[wave] = lossp;
   __syncthreads();
   if constexpr (STEP) {

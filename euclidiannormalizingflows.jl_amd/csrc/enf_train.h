@@ -75,18 +75,73 @@ __device__ __forceinline__ void adagrad_update(T& p, T& acc, T g, T scale, T eta
   p = p - dx * eta / (sqrt(a) + eps);
 }
 
+// Cross-lane moves without an LDS round trip (ds_bpermute, the __shfl_xor form, costs a round trip per stage on the
+// chains of the one-block steps). dpp_mov<CTRL>: a DPP row move (quad_perm / row_ror) of every lane's value.
+template <int CTRL, typename T>
+__device__ __forceinline__ T dpp_mov(T x) {
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, true);
+    return __builtin_bit_cast(T, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+  }
+}
+// x + (the value of lane ^ M), M = 16 or 32, by gfx950's v_permlane16_swap / v_permlane32_swap (VALU): with both
+// operands x the swap leaves x and its partner side by side, and their sum is x + __shfl_xor(x, M) bit for bit
+// (the two addends are the same, and addition commutes)
+template <int M, typename T>
+__device__ __forceinline__ T add_xor_swap(T x) {
+  static_assert(M == 16 || M == 32, "the permlane swaps pair lanes 16 or 32 apart");
+  // The instruction itself, not the builtin: hipcc 7.2 reads the builtin's second result from the first result's
+  // register for a 32-bit value (the swapped half added to itself; tools/r5/xt/xt.hip checks these against the
+  // shuffles on the GPU). Two wait states between the VALU writes of the operands and the swap.
+  struct Pair {
+    uint32_t a, b;
+  };
+  auto sw = [](uint32_t u) {
+    Pair p{u, u};
+    if constexpr (M == 32) asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(p.a), "+v"(p.b));
+    else asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(p.a), "+v"(p.b));
+    return p;
+  };
+  if constexpr (sizeof(T) == 4) {
+    const Pair r = sw(__builtin_bit_cast(uint32_t, x));
+    return __builtin_bit_cast(T, r.a) + __builtin_bit_cast(T, r.b);
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    const Pair lo = sw((uint32_t)u), hi = sw((uint32_t)(u >> 32));
+    return __builtin_bit_cast(T, ((uint64_t)hi.a << 32) | lo.a) + __builtin_bit_cast(T, ((uint64_t)hi.b << 32) | lo.b);
+  }
+}
+// The xor butterfly over the lanes of a group of P (power of two, <= 64) consecutive lanes, strides P/2 .. 1 in that
+// order: exactly `for (m = P / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m)`. Strides 32 and 16 are permlane swaps,
+// 8 is row_ror:8 (lane (l + 8) mod 16 of the row is l ^ 8), 4 is row_ror:4 once stride 8 has made every value equal
+// to its lane ^ 8 partner's (then (l + 4) mod 16 holds l ^ 4's value), 2 and 1 quad_perm; a stride-4 first stage
+// (P = 8) keeps the shuffle.
+template <typename T>
+__device__ __forceinline__ T xor_tree(T v, int P) {
+  if (P >= 64) v = add_xor_swap<32>(v);
+  if (P >= 32) v = add_xor_swap<16>(v);
+  if (P >= 16) v += dpp_mov<0x128>(v);  // row_ror:8
+  if (P >= 16) v += dpp_mov<0x124>(v);  // row_ror:4
+  else if (P >= 8) v += __shfl_xor(v, 4);
+  if (P >= 4) v += dpp_mov<0x4E>(v);    // quad_perm(2,3,0,1): lane ^ 2
+  if (P >= 2) v += dpp_mov<0xB1>(v);    // quad_perm(1,0,3,2): lane ^ 1
+  return v;
+}
+
 // The sum over a wave's lanes of values held as d = lane, lane + 64, ... < D (lanes >= D hold zeros): the xor
 // tree from half the smallest power of two >= min(D, 64) down; the strides it leaves out would only add zeros, so
 // the value is that of the full 64-lane tree (round 5: 1 stage instead of 6 at D = 2). Every lane < D gets it.
 __device__ __forceinline__ double lane_sum(double v, int64_t D) {
-  int m = 32;
+  int p = 64;
   if (D < 64) {
-    m = 1;
-    while (m < D) m <<= 1;
-    m >>= 1;
+    p = 1;
+    while (p < D) p <<= 1;
   }
-  for (; m >= 1; m >>= 1) v += __shfl_xor(v, m);
-  return v;
+  return xor_tree(v, p);
 }
 
 // LinearAlgebra.normalize! of one column by one wave (src/householder_trafo.jl:135-139), the sum
