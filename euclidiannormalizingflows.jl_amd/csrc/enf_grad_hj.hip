@@ -89,8 +89,11 @@ __device__ __forceinline__ float prod_rows(const float (&q)[V]) {
 // cross-slot sum: lanes with equal lane % G hold the same rows
 template <int G>
 __device__ __forceinline__ float slot_sum(float v) {
-#pragma unroll
-  for (int m = G; m < 64; m <<= 1) v += __shfl_xor(v, m);
+  // strides G, 2G, ... < 64 in that order, as `v += __shfl_xor(v, m)`, without LDS round trips (enf_train.h)
+  static_assert(G >= 8, "D >= 32, at most 4 rows per lane");
+  if constexpr (G == 8) v += dpp_mov<0x128>(v);  // row_ror:8 = lane ^ 8
+  if constexpr (G <= 16) v = add_xor_swap<16>(v);
+  if constexpr (G <= 32) v = add_xor_swap<32>(v);
   return v;
 }
 
@@ -328,10 +331,8 @@ __device__ __forceinline__ void grad_epilogue(const HJGradArgs& a, double* __res
                                               const float* __restrict__ acc0, size_t wstride, double lossp, int nvalid) {
   const int n = a.n;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int m = 32; m >= 1; m >>= 1) {
-    lossp += __shfl_xor(lossp, m);
-    nvalid += __shfl_xor(nvalid, m);
-  }
+  lossp = xor_tree(lossp, 64);  // the 64-lane xor butterfly (enf_train.h)
+  nvalid = xor_tree(nvalid, 64);
   double* wl = scr + 16;
   if (lane == 0) {
     wl[2 * wave] = lossp;
