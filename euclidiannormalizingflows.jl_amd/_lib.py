@@ -98,13 +98,14 @@ _SIGS = {
 }
 
 
-def use_diagnostics_library() -> None:
-    """Bind libenf_diag.so instead of libenf.so (A/B tools under tools/ only; bench.py, the tests
-    and the package never call this). Must run before the first lib() call."""
+def use_diagnostics_library(path: str | None = None) -> None:
+    """Bind libenf_diag.so (or another build of the same ABI at `path`, e.g. an earlier round's library for
+    an A/B) instead of libenf.so (tools under tools/ only; bench.py, the tests and the package never call
+    this). Must run before the first lib() call."""
     global LIB_PATH
     if _lib is not None:
         raise RuntimeError("libenf is already loaded")
-    LIB_PATH = DIAG_LIB_PATH
+    LIB_PATH = path or DIAG_LIB_PATH
 
 
 def loaded_path() -> str:

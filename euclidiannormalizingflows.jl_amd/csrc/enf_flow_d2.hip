@@ -28,9 +28,6 @@
 #include "enf_frag.h"
 #include "enf_internal.h"
 #include "enf_logtab.h"
-#if ENF_DIAG
-#include "enf_logtab_b78.h"  // the rejected B = 7 / 8 tables (ENF_D2_TABB A/B)
-#endif
 #include "enf_math64.h"
 
 namespace enf {
@@ -51,14 +48,8 @@ struct D2Args {
 constexpr int d2_tab_doubles(int B) { return 3 * ((1 << B) + 1); }
 template <int B>
 __device__ __forceinline__ const double* d2_tab_src() {
-#if ENF_DIAG
-  if constexpr (B == 8) return kLogTabB8;
-  else if constexpr (B == 7) return kLogTabB7;
-  else return kLogTab;
-#else
-  static_assert(B == kLogTabBits, "the product build has the B = 5 table only");
+  static_assert(B == kLogTabBits, "the B = 5 table only (the B = 7 / 8 variants were rejected, round 4)");
   return kLogTab;
-#endif
 }
 
 __device__ __forceinline__ double d2_readlane(double v, int l) {
@@ -358,17 +349,13 @@ static hipError_t launch_d2_lm(const D2Args& h, hipStream_t st, const DeviceInfo
   // ENF_D2_P: tiles in flight per wave
   static const int pf = ENF_KNOB("ENF_D2_P", 4);
   static const int pb = ENF_KNOB("ENF_D2_PB", 0);
-  // ENF_D2_TABB: log table index bits (5, 7, 8)
-  static const int tb = ENF_KNOB("ENF_D2_TABB", 5);
+  constexpr int tb = 5;  // log table index bits (B = 7 / 8: rejected in round 4, sources removed in round 6)
   // ENF_D2_LO=1: the first tile before the prologue, the rest after it
   static const int lo = ENF_KNOB("ENF_D2_LO", 0);
   if (lo == 1 && dbg == 0 && u == 2 && pb == 0 && tb == 5) {
     if (pf == 4) return launch_d2_u<2, LM, 0, 4, false, 5, 3, 1>(h, st, dev);
     if (pf == 3) return launch_d2_u<2, LM, 0, 3, false, 5, 3, 1>(h, st, dev);
   }
-  if (dbg == 0 && u == 2 && pb == 0 && pf == 4 && tb == 7) return launch_d2_u<2, LM, 0, 4, false, 7>(h, st, dev);
-  if (dbg == 0 && u == 2 && pb == 0 && pf == 4 && tb == 8) return launch_d2_u<2, LM, 0, 4, false, 8>(h, st, dev);
-  if (dbg == 2 && tb == 8) return launch_d2_u<2, LM, 2, 4, false, 8>(h, st, dev);
   // ENF_D2_NT: bit 0 nontemporal X loads, bit 1 nontemporal Y stores (3 default)
   static const int nt = ENF_KNOB("ENF_D2_NT", 3);
   if ((dbg == 0 || dbg == 3) && u == 2 && pb == 0 && pf == 4 && nt != 3) {

@@ -1,14 +1,10 @@
 // enf_flow_hj.hip -- the compiled (J o H)^n program (enf_hj.h: layouts, records, pair loop, the streaming
 // kernel flow_hj_kernel) launched for configs 3-5, and the compiled inverse program (J^-1, H)^n below.
-// The measured and rejected variants (the wave-specialised kernel, the asinh-form and debug-mode ladder) are
-// in enf_flow_hj_diag.hip, compiled into the diagnostics library only.
+// (The variants measured and rejected in rounds 1-5 -- the wave-specialised and mailbox kernels, the other
+// asinh forms -- are described in docs/HISTORY.md; round 6 removed their sources.)
 #include "enf_hj.h"
 
 namespace enf {
-
-#if ENF_DIAG
-hipError_t diag_dispatch_hj(const HJArgs& a, int D, int lm, int dbg, hipStream_t st, const DeviceInfo& dev);
-#endif
 
 // ---------------------------------------------------------------------------------------------------
 // The inverse program (round 4): inverse(J_n o H_n o ... o J_1 o H_1) = H_1 o J_1^-1 o ... o H_n o J_n^-1
@@ -21,7 +17,8 @@ hipError_t diag_dispatch_hj(const HJArgs& a, int D, int lm, int dbg, hipStream_t
 //   x   = lambda sh + xi                      the JohnsonTrafoInv output              (johnson_trafo.jl:36)
 //   ladj += -log|delta/lambda| + log(1 + sh^2)/2: the reference's -johnsontrafo_ladj of the output
 //         (johnson_trafo.jl:103-104), whose (x - xi)/lambda is sh up to the rounding of x; the constant part
-//         once per column (ctot), +1/2 log2 of the product of the q = 1 + sh^2 of a lane's 8 rows
+//         once per column (ctot), +1/2 log2 of the product of the q = 1 + sh^2 of a lane's 8 rows over all
+//         pairs (one log2 per lane and column per tile, round 6)
 //   dot = vh'x, x -= dot vh                   householder_trafo! (householder_trafo.jl:8-11)
 // Records per pair and row {1/delta, -gamma/delta, lambda, xi, vh} (built in double); the multipliers of tile
 // registers one slot rotated (hj_rot). A tile whose q product overflows (|sh| ~ 2^16 on every row, Inf, NaN)
@@ -102,12 +99,12 @@ __device__ __forceinline__ uint32_t sinh_small_mask(float w2) {
 }
 
 // One pair (J^-1, H) on the register tile, fast form: returns the largest q product of a lane's rows.
-template <int D, int R, int U, bool LADJ>
-__device__ __forceinline__ float hji_pair_fast(float (&x)[U][R], float (&acc)[U], const float*& r) {
+template <int D, int R, int U>
+__device__ __forceinline__ void hji_pair_fast(float (&x)[U][R], float (&prod)[U], const float*& r) {
   HJIParams<R> prm;
   prm.load(r);
   r += kHjiW * D;
-  float w[U][R], E[U][R], rE[U][R], pr[U];
+  float w[U][R], E[U][R], rE[U][R];
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -160,8 +157,7 @@ __device__ __forceinline__ float hji_pair_fast(float (&x)[U][R], float (&acc)[U]
       q[u][e] = fmaf(sh, sh, 1.0f);
       x[u][e] = fmaf(prm.m(HI_LM, e), sh, prm.m(HI_XI, e));
     }
-    pr[u] = prod_tree<R>(q[u]);
-    if (LADJ) acc[u] = fmaf(0.5f, hw_log2(pr[u]), acc[u]);
+    prod[u] *= prod_tree<R>(q[u]);
   }
   float dot[U];
   hj_dots<D, R, U, HI_VH>(x, prm, dot);
@@ -169,10 +165,6 @@ __device__ __forceinline__ float hji_pair_fast(float (&x)[U][R], float (&acc)[U]
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) x[u][e] = fmaf(-dot[u], prm.m(HI_VH, e), x[u][e]);
-  float m = pr[0];
-#pragma unroll
-  for (int u = 1; u < U; ++u) m = fmaxf(m, pr[u]);
-  return m;
 }
 
 // The same pair elementwise over the whole fp32 range: sinh finite up to |w| ~ 89.4 (E/2 formed as
@@ -213,19 +205,20 @@ struct HJIBody {
   template <bool TAIL, int DBG>
   __device__ __forceinline__ void tile(int64_t col0, float (&x)[U][R], const float (&old)[HJLay<D, R, U>::NLS]) {
     constexpr bool LADJ = LM > 0;
-    float acc[U];
+    float acc[U], prod[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc[u] = 0.f;
+    for (int u = 0; u < U; ++u) prod[u] = 1.f;
     const float* r = rec;
-    float m = 0.f;
-    for (int p = 0; p < n; ++p) m = fmaxf(m, hji_pair_fast<D, R, U, LADJ>(x, acc, r));
-    m = group_max<HJLay<D, R, U>::G>(m);
-    if (__builtin_expect(!(m <= FLT_MAX), 0)) {
+    for (int p = 0; p < n; ++p) hji_pair_fast<D, R, U>(x, prod, r);
+    if (__builtin_expect(hj_redo<HJLay<D, R, U>::G>(prod), 0)) {
       hj_load<D, R, U, TAIL, DBG, PAD>(a, col0, x);
 #pragma unroll
       for (int u = 0; u < U; ++u) acc[u] = 0.f;
       r = rec;
       for (int p = 0; p < n; ++p) hji_pair_exact<D, R, U, LADJ>(x, acc, r);
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] = 0.5f * hw_log2(prod[u]);
     }
     hj_store<D, R, U, LM, TAIL, DBG, PAD>(a, ctot, col0, x, acc, old, stage);
   }
@@ -263,18 +256,23 @@ int hj_program_pairs(const FlowArgs& a) {
 template <int LM>
 static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, const DeviceInfo& dev) {
 #if ENF_DIAG
-  {  // diagnostics build: the A/B variants of enf_flow_hj_diag.hip (ENF_DEBUG_MODE, ENF_HJ_*), else the product's
-    const hipError_t e = diag_dispatch_hj(a, D, LM, dbg, st, dev);
-    if (e != hipErrorNotSupported) return e;
+  // diagnostics build only: ENF_DEBUG_MODE 1 = synthesized tile, 2 = no stores either (compute-only timing);
+  // ENF_HJ_R16 = 16 rows per lane, one column per lane tile (two lanes per column at D = 32)
+  if (a.dreal == D && LM == 1) {
+    static const int r16 = ENF_KNOB("ENF_HJ_R16", 0);
+    if (dbg == 1) return launch_hj<32, 8, 2, 1, 4, 1>(a, st, dev);
+    if (dbg == 2) return launch_hj<32, 8, 2, 1, 4, 2>(a, st, dev);
+    if (r16 && D == 32) return launch_hj<32, 16, 1, 1, 4>(a, st, dev);
+    if (r16 && D == 64) return launch_hj<64, 16, 1, 1, 4>(a, st, dev);
   }
 #else
   (void)dbg;
 #endif
   // padded layout (round 3): D = 24 / 100 / 36 ... on the next power of two, rows past a.dreal inert
   if (a.dreal != D) {
-    if (D == 32) return launch_hj<32, 8, 2, LM, 4, 0, 1, true>(a, st, dev);
-    if (D == 64) return launch_hj<64, 8, 2, LM, 4, 0, 1, true>(a, st, dev);
-    return launch_hj<128, 8, 2, LM, 4, 0, 1, true>(a, st, dev);
+    if (D == 32) return launch_hj<32, 8, 2, LM, 4, 0, true>(a, st, dev);
+    if (D == 64) return launch_hj<64, 8, 2, LM, 4, 0, true>(a, st, dev);
+    return launch_hj<128, 8, 2, LM, 4, 0, true>(a, st, dev);
   }
   if (D == 128) return launch_hj<128, 8, 2, LM, 4>(a, st, dev);
   if (D == 32) return launch_hj<32, 8, 2, LM, 4>(a, st, dev);

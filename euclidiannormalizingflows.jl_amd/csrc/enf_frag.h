@@ -305,7 +305,7 @@ using Acc = T[U][Frag<T, D>::CPF];
 #define ENF_FRAG_CONSTS                                   \
   using F = Frag<T, D>;                                   \
   constexpr int V = F::V, G = F::G, CPF = F::CPF, SEG = F::SEG; \
-  (void)G; (void)CPF; (void)SEG;
+  (void)V; (void)G; (void)CPF; (void)SEG;
 
 // ---- step bodies: one transform applied to the wave tile x (U fragments of V values per lane).
 // r points at this lane's record group ([param][element], 16-byte vectors). acc: ladj partials.

@@ -1,36 +1,41 @@
-// enf_hj.h -- the compiled program for the flows of configs 3-5, shared by the product
-// kernels (enf_flow_hj.hip) and the diagnostics variants (enf_flow_hj_diag.hip, diagnostics build only):
+// enf_hj.h -- the compiled program for the flows of configs 3-5 (enf_flow_hj.hip):
 //   J_n o H_n o ... o J_1 o H_1   (layers H_1, J_1, H_2, J_2, ... applied in this order),
 // each H one Householder reflection (src/householder_trafo.jl:8-11), each J a JohnsonTrafo
-// (src/johnson_trafo.jl:29-32, ladj :39-42 / :76-80), fp32, D in {32, 64}, fused in one launch:
+// (src/johnson_trafo.jl:29-32, ladj :39-42 / :76-80), fp32, D in {32, 64, 128}, fused in one launch:
 // X is read once, Y and the per-sample ladj are written once.
 //
-// Per pair p (the register tile holds y, the previous Johnson output, on entry -- X itself for p = 0):
-//   dot = vh'y,  vh = v sqrt(2/v'v)                 householder_trafo! (householder_trafo.jl:8-11)
-//   z   = (y - dot vh)/lambda - xi/lambda           the reflection's output, then (x - xi)/lambda as
-//                                                    fma(x, 1/lambda, -xi/lambda) (johnson_trafo.jl:30)
-//   L_p = asinh(z)/ln2                              asinh2 (enf_frag.h): log2(|z| + sqrt(q)),
+// The register tile carries L_p = asinh(z_p)/ln2 between pairs. Every pair p is the same three full-rate
+// operations per element before its asinh (round 6: the interior hop J_{p-1} -> H_p -> J_p folded into
+// per-row constants built in double in the block prologue):
+//   dot = sum_d W_d L_d                              one FMA chain per column (W = vh_p delta'_{p-1})
+//   z_p = fma(-dot, C, fma(L, B, A))                 two FMAs
+// with vh = v sqrt(2/v'v), delta' = delta ln2 and, for p >= 1,
+//   B = delta'_{p-1}/lambda_p,  A = ((H_p gamma_{p-1}) - xi_p)/lambda_p,  C = vh_p/lambda_p
+// because z_p = (H_p(gamma_{p-1} + delta'_{p-1} L_{p-1}) - xi_p)/lambda_p and H_p y = y - vh (vh'y) is
+// linear: the constant part H_p gamma_{p-1} goes into A, the L part into W and B. Pair 0 reads X itself:
+// W = vh_0, B = 1/lambda_0, A = -xi_0/lambda_0, C = vh_0/lambda_0. The output is y_n = fma(L_n, delta'_n,
+// gamma_n) from record n. Against round 5's explicit y = gamma + delta' L before each reflection this is
+// one dependent FMA less per element and interior pair (4 -> 3). Round 1 tried a fold of gamma / delta'
+// alone and lost accuracy where y cancels; this one keeps every term the reference has: its rounding
+// errors are those of the reference's y (eps |delta' L|, which the reference incurs in delta*asinh) and of
+// the constants (rounded once, from double). Priced on the CPU before it was built (tools/hj_fold_emul.py:
+// the per-element criterion of tests/test_gpu_fp32_accuracy.py at D = 32 / 64, worst 0.59 / 0.52 of the
+// bound against 0.75 / 0.46 for the round-5 form).
+//   L_p = asinh(z_p)/ln2                             asinh2 (enf_frag.h): log2(|z| + sqrt(q)),
 //                                                    q = 1 + z^2, or the Taylor form for |z| < 1/8
-//   ladj += log|delta/lambda| - log(q)/2            johnson_trafo.jl:41; the constant part once per
-//                                                    column (ctot), -1/2 log2 of the product of the q
-//                                                    of a lane's 8 rows of one column
-//   y   = gamma_p + delta'_p L_p                    at the end of the pair, delta' = delta*ln2
-// so the last pair leaves the output in the tile. y is formed explicitly, as the reference rounds it,
-// before the next reflection: folding gamma and delta' into the next pair's constants (round 1) saves one
-// FMA per element but adds terms that the reference has already cancelled, and gave up to 16x the
-// reference's error on elements where y cancels (tests/test_gpu_fp32_accuracy.py per-element test).
-// Per element and pair: 4 FMAs (dot, 2 for z, y), q, sqrt, |z| + s, log2, the small-|z| polynomial
-// (3) and its branch-free merge (4 full-rate ops), 7/8 multiply for the ladj product.
+//   ladj = sum log|delta/lambda| - 1/2 sum log q     johnson_trafo.jl:41; the constant part once per
+//                                                    column (ctot); the q of a lane's 8 rows of one column
+//                                                    multiplied over ALL pairs (round 6: one log2 per lane
+//                                                    and column per tile instead of one per pair)
 //
-// Parameter records (LDS, built in double in each block's prologue): per pair and row
-// {delta', gamma, vh, 1/lambda, -xi/lambda, vh/lambda}; record p's {delta', gamma} slots hold pair p-1's
-// (read at the end of pair p-1, which applies them; record 0's {1, 0} is not used), record n holds
-// {delta'_n, gamma_n}.
+// Parameter records (LDS, built in double in each block's prologue): per pair and row {W, B, A, C}; record
+// n holds {0, delta'_n, gamma_n, 0} (the output: y = fma(L, B, A)).
 //
-// Fast-path guard: the product of 8 q stays finite unless |z| is large (about 2^8 on every row),
-// infinite or NaN; then the lanes of that column redo the whole program from X with the exact-range
-// elementwise form (johnson_fwd_f32_slow in enf_frag.h: asinh finite up to FLT_MAX, ladj -Inf where
-// the reference's fp32 1 + z^2 overflows).
+// Fast-path guard: the running product of q stays finite unless the column's z are large (the sum of
+// log2 q over a lane's 8 rows and n pairs above 128: about |z| > 4 on every one of them for n = 4; the
+// survey's distributions reach 62, tools/hj_fold_emul.py), infinite or NaN; then the lanes of that
+// column redo the whole program from X with the exact-range elementwise form (asinh finite up to FLT_MAX,
+// ladj -Inf where the reference's fp32 1 + z^2 overflows).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -45,7 +50,7 @@
 namespace enf {
 
 constexpr int kHjMaxPairs = 8;
-constexpr int kHjW = 6;  // record parameters per row
+constexpr int kHjW = 4;  // record parameters per row: W, B, A, C
 
 // Kernel arguments of the compiled program: the pair parameter vectors only (376 bytes; the
 // generic FlowArgs table is ~2 KB, and kernel arguments that large are staged with an extra
@@ -63,8 +68,8 @@ struct HJArgs {
   const float* xi[kHjMaxPairs];
   const float* lam[kHjMaxPairs];
 };
-// LDS: [per pair {hs, cl} + ctot: doubles][ladj staging: 4 waves x kStagePerWave floats][records]
-constexpr size_t kHjScratch = ((2 * kHjMaxPairs + 1) * sizeof(double) + 15) / 16 * 16;
+// LDS: [per pair {hs, cl, vh'gamma} + ctot: doubles][ladj staging: 4 waves x kStagePerWave floats][records]
+constexpr size_t kHjScratch = ((3 * kHjMaxPairs + 1) * sizeof(double) + 15) / 16 * 16;
 constexpr size_t kHjHeader = kHjScratch + 4 * kStagePerWave * sizeof(float);
 
 static size_t hj_lds_bytes(int D, int n) { return kHjHeader + (size_t)(n + 1) * kHjW * D * sizeof(float); }
@@ -98,11 +103,11 @@ struct HJLay {
 // half rate on gfx950 (tools/microbench5: 1.8 vs 1.0-1.2 ns per wave-instruction). The tile and the
 // records arrive by 16-byte loads into 4-register tuples whose bases the compiler aligns to even
 // registers, so x[e] and the e-th value of every record vector would share a bank. The multiplier
-// of each FMA (delta', vh, 1/lambda, vh/lambda) is therefore stored one slot rotated within its
-// 16-byte vector: row e uses slot hj_rot(e), an odd register distance from x[e]'s.
+// of each FMA (W with L in the dot, B with L, C with the previous result) is therefore stored one slot
+// rotated within its 16-byte vector: row e uses slot hj_rot(e), an odd register distance from x[e]'s.
 __host__ __device__ constexpr int hj_rot(int e) { return (e & ~3) | ((e + 1) & 3); }
-enum : int { HJ_DP = 0, HJ_GP = 1, HJ_VH = 2, HJ_IL = 3, HJ_NXI = 4, HJ_RR = 5 };
-__host__ __device__ constexpr bool hj_rotated(int q) { return q == HJ_DP || q == HJ_VH || q == HJ_IL || q == HJ_RR; }
+enum : int { HJ_W = 0, HJ_B = 1, HJ_A = 2, HJ_C = 3 };
+__host__ __device__ constexpr bool hj_rotated(int q) { return q != HJ_A; }
 
 // DBG (diagnostic builds, ENF_DEBUG_MODE): 1 = synthesize the tile instead of loading it, 2 = also
 // skip the stores (compute-only timing); cache policy A/B: 8 = nontemporal loads, 9 = plain stores.
@@ -204,33 +209,34 @@ __device__ __forceinline__ void hj_store(const HJArgs& a, float ctot, int64_t co
   }
 }
 
-// Records, pair p < n: [group g][param q][R values, value 4h+e = row h*D/NF+4g+e, rotated slot for
-// the multipliers]; record n: {delta'_{n-1}, gamma_{n-1}} (the output). A lane reads each parameter
-// of its rows with NF 16-byte LDS reads.
-template <int D, int R, int AS>
+// Records, pair p <= n: [group g][param q][R values, value 4h+e = row h*D/NF+4g+e, rotated slot for
+// the multipliers]. A lane reads each parameter of its rows with NF 16-byte LDS reads.
+template <int D, int R>
 __device__ void build_hj_program(const HJArgs& a, int n, float* __restrict__ rec, double* __restrict__ scr,
                                  float* ctot) {
-  // AS == 2 (asinh2_med3): z is carried as sqrt(K) z, so the three z records are scaled by sqrt(K)
-  const double zs = AS == 2 ? kAsinhSqrtK : 1.0;
   constexpr int NF = R / 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  // pass 1 (one wave per pair): v'v and the constant ladj part sum_d log|delta/lambda|
-  // (johnson_trafo.jl:41) in double
+  // pass 1 (one wave per pair): v'v, the constant ladj part sum_d log|delta/lambda| (johnson_trafo.jl:41)
+  // and v'gamma_{p-1} (the reflection of the previous Johnson layer's shift, folded into A) in double
   for (int p = wave; p < n; p += nw) {
     const float* v = a.v[p];
-    double vv = 0.0, cl = 0.0;
+    double vv = 0.0, cl = 0.0, vg = 0.0;
     for (int d = lane; d < a.dreal; d += 64) {  // the batch's rows (padded rows: neutral records below)
       const double vd = v[d];
       vv += vd * vd;
       cl += log(fabs((double)a.d[p][d])) - log(fabs((double)a.lam[p][d]));
+      if (p > 0) vg += vd * (double)a.g[p - 1][d];
     }
     for (int m = 32; m >= 1; m >>= 1) {
       vv += __shfl_xor(vv, m);
       cl += __shfl_xor(cl, m);
+      vg += __shfl_xor(vg, m);
     }
     if (lane == 0) {
-      scr[2 * p] = sqrt(2.0 / vv);  // householder_trafo.jl:9-10: 2 v (v'x) / (v'v)
-      scr[2 * p + 1] = cl;
+      const double hs = sqrt(2.0 / vv);  // householder_trafo.jl:9-10: 2 v (v'x) / (v'v)
+      scr[3 * p] = hs;
+      scr[3 * p + 1] = cl;
+      scr[3 * p + 2] = hs * vg;  // vh'gamma_{p-1}
     }
   }
   __syncthreads();
@@ -239,43 +245,50 @@ __device__ void build_hj_program(const HJArgs& a, int n, float* __restrict__ rec
     const int p = i / D, d = i % D;
     const int h = d / (D / NF), w = d % (D / NF), g = w / 4, e = w % 4;
     float* r = rec + (size_t)p * kHjW * D + g * kHjW * R + 4 * h;
-    double q[kHjW] = {0, 0, 0, 0, 0, 0};
-    // a padded row (d >= dreal): vh = 0, 1/lambda = 1, -xi/lambda = 0, gamma = 0 -- its zeros stay zero,
-    // with q = 1 (ladj 0); its ladj constant is not in ctot (pass 1)
+    // a padded row (d >= dreal): W = C = 0, B = 1, A = 0 -- its zeros stay zero, with q = 1 (ladj 0);
+    // its ladj constant is not in ctot (pass 1)
     const bool real = d < a.dreal;
-    q[HJ_DP] = p > 0 && real ? (double)a.d[p - 1][d] * kLn2 : 1.0;
-    q[HJ_GP] = p > 0 && real ? (double)a.g[p - 1][d] : 0.0;
-    q[HJ_IL] = 1.0;
-    if (p < n && real) {
-      const double vh = (double)a.v[p][d] * scr[2 * p];
-      const double il = zs / (double)a.lam[p][d];
-      q[HJ_VH] = vh;
-      q[HJ_IL] = il;
-      q[HJ_NXI] = -(double)a.xi[p][d] * il;
-      q[HJ_RR] = vh * il;  // sqrt(K) vh / lambda
+    double q[kHjW] = {0.0, 1.0, 0.0, 0.0};
+    if (p == n) {  // the output y_n = gamma_n + delta'_n L_n
+      if (real) {
+        q[HJ_B] = (double)a.d[p - 1][d] * kLn2;
+        q[HJ_A] = (double)a.g[p - 1][d];
+      }
+    } else if (real) {
+      const double vh = (double)a.v[p][d] * scr[3 * p];
+      const double il = 1.0 / (double)a.lam[p][d];
+      const double xi = (double)a.xi[p][d];
+      if (p == 0) {
+        q[HJ_W] = vh;
+        q[HJ_B] = il;
+        q[HJ_A] = -xi * il;
+      } else {
+        const double dp = (double)a.d[p - 1][d] * kLn2;
+        const double hg = (double)a.g[p - 1][d] - vh * scr[3 * p + 2];  // (H_p gamma_{p-1})_d
+        q[HJ_W] = vh * dp;
+        q[HJ_B] = dp * il;
+        q[HJ_A] = (hg - xi) * il;
+      }
+      q[HJ_C] = vh * il;
     }
 #pragma unroll
     for (int k = 0; k < kHjW; ++k) r[k * R + (hj_rotated(k) ? hj_rot(e) : e)] = (float)q[k];
   }
   if (threadIdx.x == 0) {
     double c = 0.0;
-    for (int p = 0; p < n; ++p) c += scr[2 * p + 1];
-    // AS == 2: the fast form sums -log2(q')/2 = -log2(q)/2 - log2(K)/2 per element (ln2 * acc)
-    if (AS == 2) c += 0.5 * D * n * log(kAsinhK);
+    for (int p = 0; p < n; ++p) c += scr[3 * p + 1];
     *ctot = (float)c;
   }
   __syncthreads();
 }
 
-// One pair's parameters of the lane's rows (6 x R values): the first three are read at the end of
-// the previous pair, the last three at the start of the pair (they are needed after the dot).
+// One record's parameters of the lane's rows (kHjW x R values).
 template <int R>
 struct HJParams {
   float v[kHjW][R];
-  template <int Q0, int Q1>
   __device__ __forceinline__ void load(const float* r) {
 #pragma unroll
-    for (int k = Q0; k < Q1; ++k)
+    for (int k = 0; k < kHjW; ++k)
 #pragma unroll
       for (int h = 0; h < R / 4; ++h) lds_vec<float, 4>(r + k * R + 4 * h, *reinterpret_cast<float(*)[4]>(&v[k][4 * h]));
   }
@@ -284,8 +297,8 @@ struct HJParams {
 
 // Householder dot of every column of the tile: two independent partial chains per column (even
 // and odd rows) over the lane's R rows, then log2(G) DPP stages across the G lanes of the column.
-// (Q: the record slot of vh in the parameter set P)
-template <int D, int R, int U, int Q = HJ_VH, typename P = HJParams<R>>
+// (Q: the record slot of the row weights in the parameter set P)
+template <int D, int R, int U, int Q = HJ_W, typename P = HJParams<R>>
 __device__ __forceinline__ void hj_dots(const float (&y)[U][R], const P& prm, float (&dot)[U]) {
   constexpr int G = HJLay<D, R, U>::G;
   float d2[U][2];
@@ -343,55 +356,49 @@ __device__ __forceinline__ float prod_tree(const float (&q)[R]) {
   }
 }
 
-// The dot and z of one pair, in place on the tile (x: the pair's input y on entry, z on exit).
-// In the reference's operation order: the reflection's output y - vh (vh'y), then (. - xi)/lambda as
-// fma(., 1/lambda, -xi/lambda) (the records' vh/lambda slot is not read).
+// The front of one pair, in place on the tile (x: L_{p-1}, or X for p = 0, on entry; z_p on exit):
+// dot = W'x over the column, z = fma(-dot, C, fma(x, B, A)).
 template <int D, int R, int U>
-__device__ __forceinline__ void hj_pair_z(float (&x)[U][R], const float* r, HJParams<R>& prm) {
-  prm.template load<HJ_IL, HJ_RR>(r);
+__device__ __forceinline__ void hj_front(float (&x)[U][R], const HJParams<R>& prm) {
   float dot[U];
   hj_dots<D, R, U>(x, prm, dot);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < R; ++e) x[u][e] = fmaf(-dot[u], prm.m(HJ_VH, e), x[u][e]);
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_B, e), prm.m(HJ_A, e));
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_IL, e), prm.m(HJ_NXI, e));
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(-dot[u], prm.m(HJ_C, e), x[u][e]);
 }
 
-// One pair (reflection + Johnson) on the register tile, fast form. x holds L (pair 0: the input x)
-// on entry and the new L on exit; r points at the lane's record group of this pair and is advanced
-// to the next record (whose first three parameters are read at the end). Returns the largest
-// product of q = 1 + z^2 over a lane's R rows of one column (+Inf / NaN: the fast form is not valid
-// for the tile). AS selects the asinh form: 1 = the mask-first merge asinh2_mask / asinh2_pick (the
-// product), and in the diagnostics build only 3 = the same merge with its mask taken from the log2
-// (asinh2_merge), 2 = asinh2_med3 (z' = sqrt(K) z, enf_frag.h) and 0 = round 1's absolute-error form.
-template <int D, int R, int U, bool LADJ, int AS = 1>
-__device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U], const float*& r, HJParams<R>& prm,
-                                              uint32_t csign) {
-  hj_pair_z<D, R, U>(x, r, prm);
+// One pair (reflection + Johnson) on the register tile, fast form. x holds L_{p-1} (pair 0: the input x)
+// on entry and L_p on exit; prm holds this pair's record on entry and the next one's on exit (r is
+// advanced to it; read after the asinh's temporaries are dead: 128 VGPRs and 65 spilled when the reads
+// were issued before the asinh). prod[u] accumulates the product of the
+// q = 1 + z^2 of the lane's R rows of column u (+Inf / NaN: the fast form is not valid for the tile).
+// asinh: the mask-first merge asinh2_mask / asinh2_pick of the Taylor form and the log form (enf_frag.h).
+template <int D, int R, int U>
+__device__ __forceinline__ void hj_pair_fast(float (&x)[U][R], float (&prod)[U], const float*& r, HJParams<R>& prm,
+                                             uint32_t csign) {
+  hj_front<D, R, U>(x, prm);
+  r += kHjW * D;
   // stage by stage over the whole tile (U*R independent chains per stage)
-  float q[U][R], t[U][R], pr[U];
-  uint32_t msel[U][R];  // AS == 1: the select mask of asinh2_pick, from q (before the transcendentals)
+  float q[U][R], t[U][R];
+  uint32_t msel[U][R];  // the select mask of asinh2_pick, from q (before the transcendentals)
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int e = 0; e < R; ++e) q[u][e] = fmaf(x[u][e], x[u][e], AS == 2 ? (float)kAsinhK : 1.0f);
-  if constexpr (AS == 1) {
+    for (int e = 0; e < R; ++e) q[u][e] = fmaf(x[u][e], x[u][e], 1.0f);
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+  for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int e = 0; e < R; ++e) msel[u][e] = asinh2_mask(q[u][e], csign);
-  }
-  // Wave priority 3 while a wave issues its sqrt / log2 group, 0 otherwise (round 3, last session): the SIMD's
-  // arbiter then issues the transcendentals of the waves in that phase first and fills the transcendental
-  // pipe's busy cycles with the other waves' FMAs, instead of picking by age. 0.682 / 0.683 / 0.686 vs
-  // 0.725 / 0.721 / 0.723 ms streaming, 0.532 / 0.548 / 0.553 vs 0.614 / 0.609 / 0.597 ms compute-only
-  // (profiles/r03_setprio_ab.jsonl); the reversed priorities, a priority around only one of the two groups,
-  // around the ladj's log2 too, or a middle priority for the reflection were slower or within noise
-  // (r03_setprio_placement_ab.jsonl, r03_setprio_placement2_ab.jsonl; those variants were removed in round 4).
+    for (int e = 0; e < R; ++e) msel[u][e] = asinh2_mask(q[u][e], csign);
+  // Wave priority 3 while a wave issues its sqrt / log2 group, 0 otherwise (round 3): the SIMD's arbiter
+  // then issues the transcendentals of the waves in that phase first and fills the transcendental pipe's
+  // busy cycles with the other waves' FMAs, instead of picking by age. 0.682 / 0.683 / 0.686 vs
+  // 0.725 / 0.721 / 0.723 ms streaming (profiles/r03_setprio_ab.jsonl; the other placements measured then
+  // were slower or within noise: r03_setprio_placement_ab.jsonl, r03_setprio_placement2_ab.jsonl).
   __builtin_amdgcn_s_setprio(3);
   if constexpr (R == 8) {
 #pragma unroll
@@ -404,14 +411,12 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
   }
   __builtin_amdgcn_s_setprio(0);
 #pragma unroll
-  for (int u = 0; u < U; ++u) pr[u] = prod_tree<R>(q[u]);
-  if constexpr (AS > 0) {  // small |z|: the Taylor form (enf_frag.h) in place of q
+  for (int u = 0; u < U; ++u) prod[u] *= prod_tree<R>(q[u]);
+  // small |z|: the Taylor form (enf_frag.h) in place of q
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+  for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int e = 0; e < R; ++e)
-        q[u][e] = AS == 2 ? asinh2_small_k(x[u][e], q[u][e]) : asinh2_small(x[u][e], q[u][e]);
-  }
+    for (int e = 0; e < R; ++e) q[u][e] = asinh2_small(x[u][e], q[u][e]);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -427,60 +432,45 @@ __device__ __forceinline__ float hj_pair_fast(float (&x)[U][R], float (&acc)[U],
       for (int e = 0; e < R; ++e) t[u][e] = hw_log2(t[u][e]);
   }
   __builtin_amdgcn_s_setprio(0);
-  if (LADJ)
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc[u] = fmaf(-0.5f, hw_log2(pr[u]), acc[u]);
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < R; ++e) x[u][e] = asinh2_pick(q[u][e], t[u][e], msel[u][e]);
+  prm.load(r);
+}
+
+// The same pair in the exact-range elementwise form: asinh finite up to FLT_MAX (log2(2|z|) above 1e18),
+// ladj -Inf where the reference's fp32 1 + z^2 overflows (johnson_trafo.jl:41).
+template <int D, int R, int U>
+__device__ __forceinline__ void hj_pair_exact(float (&x)[U][R], float (&acc)[U], const float*& r, HJParams<R>& prm,
+                                              uint32_t csign) {
+  hj_front<D, R, U>(x, prm);
+  r += kHjW * D;
+  prm.load(r);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) {
-      if constexpr (AS == 2)
-        x[u][e] = asinh2_med3(q[u][e], t[u][e]);
-      else if constexpr (AS == 1)
-        x[u][e] = asinh2_pick(q[u][e], t[u][e], msel[u][e]);
-      else if constexpr (AS == 3)
-        x[u][e] = asinh2_merge(x[u][e], q[u][e], t[u][e], csign);
-      else
-        x[u][e] = copysignf(t[u][e], x[u][e]);
+      const float z = x[u][e];
+      const float q = fmaf(z, z, 1.0f);
+      x[u][e] = fabsf(z) > 1e18f ? copysignf(hw_log2(fabsf(z)) + 1.0f, z) : asinh2_f32(z, q, hw_sqrt(q), csign);
+      acc[u] = fmaf(-0.5f, hw_log2(q), acc[u]);
     }
-  r += kHjW * D;
-  prm.template load<0, HJ_IL>(r);
-  // y_p = gamma_p + delta'_p L_p: the next record's {delta', gamma} slots (record n: the output's)
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_DP, e), prm.m(HJ_GP, e));
-  float m = pr[0];
-#pragma unroll
-  for (int u = 1; u < U; ++u) m = fmaxf(m, pr[u]);
-  return m;
 }
 
-// The same pair in the exact-range elementwise form (johnson_fwd_f32_slow): asinh finite up to
-// FLT_MAX, ladj -Inf where the reference's fp32 1 + z^2 overflows.
-// (AS == 2: the records give sqrt(K) z; z is unscaled here, and the ladj carries the fast form's
-// -log2(K)/2 per element that the column constant cancels.)
-template <int D, int R, int U, bool LADJ, int AS>
-__device__ __forceinline__ void hj_pair_exact(float (&x)[U][R], float (&acc)[U], const float*& r, HJParams<R>& prm) {
-  hj_pair_z<D, R, U>(x, r, prm);
-  constexpr float halflog2k = 3.4396521971792485e-07f;  // log2(K)/2
+// Whether the fast form is invalid for any column of the lane's tile, the same on every lane of a column:
+// a running q product that is not finite. (Tested as a flag, not as a max of the products: an overflow in
+// one pair is followed by Inf * 0 = NaN products in the next ones when the huge z turn into Inf - Inf in the
+// next front, and fmaxf drops NaN operands.)
+template <int G, int U>
+__device__ __forceinline__ bool hj_redo(const float (&prod)[U]) {
+  bool ok = true;
 #pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int e = 0; e < R; ++e) {
-      const YL yl = johnson_fwd_f32_slow(AS == 2 ? x[u][e] * (float)kAsinhRSqrtK : x[u][e], 0.f, 1.f);
-      x[u][e] = yl.y;
-      if (LADJ) acc[u] += AS == 2 ? yl.l - halflog2k : yl.l;
-    }
-  r += kHjW * D;
-  prm.template load<0, HJ_IL>(r);
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_DP, e), prm.m(HJ_GP, e));
+  for (int u = 0; u < U; ++u) ok = ok && prod[u] <= FLT_MAX;
+  return group_max<G>(ok ? 0.f : 1.f) != 0.f;
 }
 
-template <int D, int R, int U, int LM, int AS = 1, bool PAD = false>
+template <int D, int R, int U, int LM, bool PAD = false>
 struct HJBody {
   const HJArgs& a;
   const float* rec;  // this lane's record group
@@ -490,28 +480,32 @@ struct HJBody {
 
   template <bool TAIL, int DBG>
   __device__ __forceinline__ void tile(int64_t col0, float (&x)[U][R], const float (&old)[HJLay<D, R, U>::NLS]) {
-    constexpr bool LADJ = LM > 0;
-    float acc[U];
+    float acc[U], prod[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc[u] = 0.f;
+    for (int u = 0; u < U; ++u) prod[u] = 1.f;
     const float* r = rec;
     HJParams<R> prm;
-    prm.template load<0, HJ_IL>(r);
+    prm.load(r);
     const uint32_t csign = sign_mask_vgpr();
     // branch-free pair loop; a tile with a product overflow (|z| large, Inf, NaN) is redone below
-    float m = 0.f;
-    for (int p = 0; p < n; ++p) m = fmaxf(m, hj_pair_fast<D, R, U, LADJ, AS>(x, acc, r, prm, csign));
+    for (int p = 0; p < n; ++p) hj_pair_fast<D, R, U>(x, prod, r, prm, csign);
     // column-uniform: the exact form's dot products read every lane of a column (DPP)
-    m = group_max<HJLay<D, R, U>::G>(m);
-    if (__builtin_expect(!(m <= FLT_MAX), 0)) {
+    if (__builtin_expect(hj_redo<HJLay<D, R, U>::G>(prod), 0)) {
       hj_load<D, R, U, TAIL, DBG, PAD>(a, col0, x);
 #pragma unroll
       for (int u = 0; u < U; ++u) acc[u] = 0.f;
       r = rec;
-      prm.template load<0, HJ_IL>(r);
-      for (int p = 0; p < n; ++p) hj_pair_exact<D, R, U, LADJ, AS>(x, acc, r, prm);
+      prm.load(r);
+      for (int p = 0; p < n; ++p) hj_pair_exact<D, R, U>(x, acc, r, prm, csign);
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] = -0.5f * hw_log2(prod[u]);
     }
-    // (y_n = gamma_n + delta'_n L_n was formed at the end of the last pair)
+    // the output y_n = gamma_n + delta'_n L_n (record n)
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_B, e), prm.m(HJ_A, e));
     hj_store<D, R, U, LM, TAIL, DBG, PAD>(a, ctot, col0, x, acc, old, stage);
   }
 };
@@ -556,28 +550,28 @@ __device__ __forceinline__ void hj_stream(const HJArgs& a, Body& body) {
   }
 }
 
-template <int D, int R, int U, int LM, int OCC, int DBG, int AS = 1, bool PAD = false>
+template <int D, int R, int U, int LM, int OCC, int DBG, bool PAD = false>
 __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   const int n = a.n;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* scr = reinterpret_cast<double*>(smem);
-  float* ctotp = reinterpret_cast<float*>(scr + 2 * kHjMaxPairs);
+  float* ctotp = reinterpret_cast<float*>(scr + 3 * kHjMaxPairs);
   float* stage = reinterpret_cast<float*>(smem + kHjScratch) + (threadIdx.x >> 6) * kStagePerWave;
   float* rec = reinterpret_cast<float*>(smem + kHjHeader);
-  build_hj_program<D, R, AS>(a, n, rec, scr, ctotp);
+  build_hj_program<D, R>(a, n, rec, scr, ctotp);
   constexpr int G = HJLay<D, R, U>::G;
-  HJBody<D, R, U, LM, AS, PAD> body{a, rec + ((threadIdx.x & 63) % G) * kHjW * R, *ctotp, stage, n};
+  HJBody<D, R, U, LM, PAD> body{a, rec + ((threadIdx.x & 63) % G) * kHjW * R, *ctotp, stage, n};
   hj_stream<D, R, U, LM, DBG, PAD>(a, body);
 }
 
-template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, int AS = 1, bool PAD = false>
+template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, bool PAD = false>
 static hipError_t launch_hj(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
   const size_t lds = hj_lds_bytes(D, h.n);
-  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, AS, PAD>);
+  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, PAD>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)HJLay<D, R, U>::TC * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, AS, PAD>), dim3((unsigned)blocks), dim3(256), lds, st, h);
+  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, PAD>), dim3((unsigned)blocks), dim3(256), lds, st, h);
   return hipGetLastError();
 }
 
