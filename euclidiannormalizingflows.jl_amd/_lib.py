@@ -17,6 +17,7 @@ DIAG_LIB_PATH = os.path.join(_HERE, "libenf_diag.so")
 
 ENF_OK, ENF_ERR_INVALID, ENF_ERR_HIP, ENF_ERR_UNSUPPORTED, ENF_ERR_RCCL = range(5)
 ENF_F32, ENF_F64 = 0, 1
+ENF_NEGLL_ZYGOTE = 0x100  # dtype flag of the training calls: report the loss the reference records (include/enf.h)
 OP_SCALESHIFT, OP_CENTER_STRETCH, OP_CENTER_CONTRACT, OP_JOHNSON, OP_JOHNSON_INV, OP_HOUSEHOLDER = range(6)
 UNIQUE_ID_BYTES = 128
 

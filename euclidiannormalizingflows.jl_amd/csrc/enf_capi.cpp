@@ -99,8 +99,21 @@ enf_status flow_apply_cpu(bool f64, int64_t D, int64_t N, const void* X, int64_t
                           void* ladj, int32_t accumulate, const enf_layer* layers, int32_t nlayers, int32_t nthreads);
 // shared with enf_train.hip
 enf_status set_error(enf_status st, const char* msg) { return fail(st, msg); }
+thread_local int tl_negll_zygote = 0;
 enf_status current_device_info(DeviceInfo* out) { return device_info(out); }
 }  // namespace enf
+
+namespace {
+// ENF_NEGLL_ZYGOTE (include/enf.h) of a training entry point: stripped from the dtype, held for the call
+struct ZygoteScope {
+  explicit ZygoteScope(enf_dtype& dtype) {
+    enf::tl_negll_zygote = ((int)dtype & ENF_NEGLL_ZYGOTE) ? 1 : 0;
+    dtype = (enf_dtype)((int)dtype & ~ENF_NEGLL_ZYGOTE);
+  }
+  ~ZygoteScope() { enf::tl_negll_zygote = 0; }
+};
+
+}  // namespace
 
 extern "C" {
 
@@ -560,6 +573,7 @@ enf_status enf_flow_negll_grad(enf_dtype dtype, int64_t D, int64_t N, const void
                                const enf_layer* layers, int32_t nlayers, void* out, void* workspace,
                                size_t workspace_bytes, void* hip_stream) {
   ENF_TRY
+  ZygoteScope zygote(dtype);
   if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
   if (D < 0 || N < 0) return fail(ENF_ERR_INVALID, "D and N must be >= 0");
   if (ldx < (D > 0 ? D : 1)) return fail(ENF_ERR_INVALID, "ldx < D");
@@ -622,6 +636,7 @@ enf_status enf_whitening_step(enf_dtype dtype, int64_t D, int64_t N, const void*
                               int32_t nruns, const int64_t* hbatches, int32_t nhb, double eta, double epsilon,
                               double* loss_out, void* workspace, size_t workspace_bytes, void* hip_stream) {
   ENF_TRY
+  ZygoteScope zygote(dtype);
   if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
   if (D < 1 || N < 1) return fail(ENF_ERR_INVALID, "D and N must be >= 1");
   if (ldx < D) return fail(ENF_ERR_INVALID, "ldx < D");
@@ -639,6 +654,7 @@ enf_status enf_whitening_epoch(enf_dtype dtype, int64_t D, int64_t N, const void
                                int32_t nruns, const int64_t* hbatches, int32_t nhb, double eta, double epsilon,
                                double* loss_out, void* workspace, size_t workspace_bytes, void* hip_stream) {
   ENF_TRY
+  ZygoteScope zygote(dtype);
   if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
   if (D < 1 || N < 1 || batchsize < 1) return fail(ENF_ERR_INVALID, "D, N and batchsize must be >= 1");
   if (ldx < D) return fail(ENF_ERR_INVALID, "ldx < D");
@@ -817,6 +833,7 @@ enf_status enf_whitening_step_dp(enf_dtype dtype, int64_t D, int64_t N, const vo
                                  int64_t B, double* loss_out, enf_comm comm, void* workspace, size_t workspace_bytes,
                                  void* hip_stream) {
   ENF_TRY
+  ZygoteScope zygote(dtype);
   if (dtype != ENF_F32 && dtype != ENF_F64) return fail(ENF_ERR_INVALID, "bad dtype");
   if (D < 1 || N < 0 || B < 1 || N > B) return fail(ENF_ERR_INVALID, "D and B must be >= 1, 0 <= N <= B");
   if (ldx < D) return fail(ENF_ERR_INVALID, "ldx < D");

@@ -69,7 +69,22 @@ struct GradArgs {
   void* dX;
   int64_t lddx;
   int32_t diag_ts;  // diagnostics build (ENF_SMALL_TS): the one-block step's thread 0 prints its phase clocks
+  int32_t zq;       // ENF_NEGLL_ZYGOTE: block 0 adds N sum log|a| of the ScaleShiftTrafos back to the loss
 };
+
+// sum_d log|a_d| of the flow's ScaleShiftTrafos (src/scale_shift_trafo.jl:22: over a's own length -- a length-1 a
+// broadcast over the rows counts once), this lane's share (d = lane, lane + 64, ...), in double
+template <typename T>
+__device__ __forceinline__ double scaleshift_ladj_lane(const GradArgs& a, int lane) {
+  double s = 0.0;
+  for (int l = 0; l < a.nlayers; ++l) {
+    if (a.layers[l].op != OP_SCALESHIFT) continue;
+    const T* p = (const T*)a.layers[l].p[0];
+    const int n = a.layers[l].k == 1 ? 1 : a.D;
+    for (int d = lane; d < n; d += 64) s += log(fabs((double)p[d]));
+  }
+  return s;
+}
 
 // values per lane of the generic gradient kernel at kernel rows D: a 16-byte fragment, or D/64 rows
 template <typename T>
@@ -914,6 +929,9 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
 #if ENF_DIAG
   const long long ts2 = STEP && a.diag_ts ? (long long)clock64() : 0;
 #endif
+  // ENF_NEGLL_ZYGOTE: the reference's recorded loss (its ScaleShiftTrafo primal ladj is zero under Zygote,
+  // src/abstract_trafo.jl:30-33): block 0's wave 0 adds N sum log|a| back, at the parameters this step read
+  if (a.zq && blockIdx.x == 0 && wave == 0) lossp += (double)bc.N * scaleshift_ladj_lane<T>(a, lane);
   lossp = xor_tree(lossp, 64);  // (the 64-lane xor butterfly)
   if (lane == 0) lossw[wave] = lossp;
   __syncthreads();
@@ -1126,6 +1144,7 @@ enf_status make_plan(bool f64, int64_t D, int64_t N, const enf_layer* layers, in
   if (f64 && Dp == 2 && P.vl == 1 && ops_are({OP_SCALESHIFT, OP_HOUSEHOLDER, OP_CENTER_CONTRACT})) P.prog = 2;
   P.ga.nlayers = nlayers;
   P.ga.nparams = goff;
+  P.ga.zq = tl_negll_zygote;
   const size_t esz = f64 ? 8 : 4;
   const size_t gbytes = ((size_t)goff * 8 + 15) / 16 * 16;
   // records, and (fast) the log table after the waves' activations
@@ -1706,6 +1725,40 @@ enf_status chunk_backward(bool f64, int64_t D, int64_t N, const void* X, int64_t
   return ENF_OK;
 }
 
+// ENF_NEGLL_ZYGOTE on the chunked path: out[0] += N sum log|a| over the flow's ScaleShiftTrafos (one wave; the
+// one-launch path adds the same inside the gradient kernel, scaleshift_ladj_lane)
+constexpr int kZygoteMaxSS = 64;
+struct ZygoteSS {
+  const void* p[kZygoteMaxSS];
+  int32_t n[kZygoteMaxSS];
+  int32_t cnt;
+};
+template <typename T>
+__global__ __launch_bounds__(64) void zygote_loss_kernel(T* out, ZygoteSS z, int64_t N) {
+  double s = 0.0;
+  for (int i = 0; i < z.cnt; ++i)
+    for (int d = threadIdx.x; d < z.n[i]; d += 64) s += log(fabs((double)((const T*)z.p[i])[d]));
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+  if (threadIdx.x == 0) out[0] += (T)((double)N * s);
+}
+enf_status zygote_loss_chunked(bool f64, int64_t D, int64_t N, const std::vector<GradChunk>& ch, void* out,
+                               hipStream_t st) {
+  ZygoteSS z;
+  std::memset(&z, 0, sizeof z);
+  for (const GradChunk& c : ch)
+    for (const enf_layer& l : c.layers) {
+      if (l.op != OP_SCALESHIFT) continue;
+      if (z.cnt == kZygoteMaxSS) return set_error(ENF_ERR_UNSUPPORTED, "ENF_NEGLL_ZYGOTE: more than 64 ScaleShiftTrafos");
+      z.p[z.cnt] = l.p[0];
+      z.n[z.cnt++] = l.k == 1 ? 1 : (int32_t)D;
+    }
+  if (z.cnt == 0) return ENF_OK;
+  if (f64) hipLaunchKernelGGL(zygote_loss_kernel<double>, dim3(1), dim3(64), 0, st, (double*)out, z, N);
+  else hipLaunchKernelGGL(zygote_loss_kernel<float>, dim3(1), dim3(64), 0, st, (float*)out, z, N);
+  const hipError_t h = hipGetLastError();
+  return h == hipSuccess ? ENF_OK : set_error(ENF_ERR_HIP, hipGetErrorString(h));
+}
+
 // the whole negll + gradient through the chunks into out (1 + nparams of T, accumulated)
 enf_status negll_grad_chunked(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx,
                               const std::vector<GradChunk>& ch, void* out, char* ws, const ChunkWs& w, hipStream_t st) {
@@ -1715,6 +1768,7 @@ enf_status negll_grad_chunked(bool f64, int64_t D, int64_t N, const void* X, int
   double* part = (double*)(ws + w.part);
   s = negll_reduce(f64, D, N, ws + w.y, ws + w.l, part, part + 1024, true, st);
   if (s == ENF_OK) s = negll_add_total(f64, part + 1024, out, st);
+  if (s == ENF_OK && tl_negll_zygote) s = zygote_loss_chunked(f64, D, N, ch, out, st);
   if (s == ENF_OK) s = fill(f64, ws + w.m1, N, -1.0, st);  // d(loss)/d(ladj) = -1; d(loss)/dY = Y (in place)
   if (s != ENF_OK) return s;
   return chunk_backward(f64, D, N, X, ldx, ws + w.y, D, ws + w.m1, ch, ws + w.y, D, (char*)out + e, ws, w, st);

@@ -27,6 +27,7 @@
 //   reduction subtracts N times it from the loss.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
@@ -742,7 +743,15 @@ bool hj_grad_eligible(int64_t D, int64_t ldx, const void* X, const enf_layer* la
   return ldx == D && (((uintptr_t)X) & 15) == 0 && hj_grad_shape_ok(D, layers, nlayers);
 }
 
-int hj_grad_blocks(int64_t D, int64_t N, int32_t npairs) { return blocks_for(select_kernel(D, npairs, N), N); }
+// Partial rows a launch for ANY batch of at most N columns may write (the workspace reservation, make_plan): the
+// kernel's shape changes at kLargeBatch and the small-batch shape can have more blocks, so past it the reservation
+// also covers the largest batch below it -- enf_flow_negll_grad_workspace(batchsize) then suffices for a ragged
+// last minibatch.
+int hj_grad_blocks(int64_t D, int64_t N, int32_t npairs) {
+  int b = blocks_for(select_kernel(D, npairs, N), N);
+  if (N >= kLargeBatch) b = std::max(b, blocks_for(select_kernel(D, npairs, kLargeBatch - 1), kLargeBatch - 1));
+  return b;
+}
 
 hipError_t launch_hj_grad(int64_t D, int64_t N, const void* X, const enf_layer* layers, int32_t nlayers,
                           int32_t nparams, double* partial, double* ctot_out, int* nblocks, hipStream_t st) {

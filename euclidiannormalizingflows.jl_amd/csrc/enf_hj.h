@@ -286,9 +286,10 @@ __device__ void build_hj_program(const HJArgs& a, int n, float* __restrict__ rec
 template <int R>
 struct HJParams {
   float v[kHjW][R];
+  template <int Q0 = 0, int Q1 = kHjW>
   __device__ __forceinline__ void load(const float* r) {
 #pragma unroll
-    for (int k = 0; k < kHjW; ++k)
+    for (int k = Q0; k < Q1; ++k)
 #pragma unroll
       for (int h = 0; h < R / 4; ++h) lds_vec<float, 4>(r + k * R + 4 * h, *reinterpret_cast<float(*)[4]>(&v[k][4 * h]));
   }
@@ -378,11 +379,14 @@ __device__ __forceinline__ void hj_front(float (&x)[U][R], const HJParams<R>& pr
 // were issued before the asinh). prod[u] accumulates the product of the
 // q = 1 + z^2 of the lane's R rows of column u (+Inf / NaN: the fast form is not valid for the tile).
 // asinh: the mask-first merge asinh2_mask / asinh2_pick of the Taylor form and the log form (enf_frag.h).
-template <int D, int R, int U>
+// VAR (diagnostics build, ENF_HJ_VAR): where the next record's LDS reads are issued -- 0 (product) after the
+// pick, 1 = W after the front and B, A, C after the pick, 2 = all after the sqrt group.
+template <int D, int R, int U, int VAR = 0>
 __device__ __forceinline__ void hj_pair_fast(float (&x)[U][R], float (&prod)[U], const float*& r, HJParams<R>& prm,
                                              uint32_t csign) {
   hj_front<D, R, U>(x, prm);
   r += kHjW * D;
+  if constexpr (VAR == 1) prm.template load<HJ_W, HJ_W + 1>(r);
   // stage by stage over the whole tile (U*R independent chains per stage)
   float q[U][R], t[U][R];
   uint32_t msel[U][R];  // the select mask of asinh2_pick, from q (before the transcendentals)
@@ -410,6 +414,7 @@ __device__ __forceinline__ void hj_pair_fast(float (&x)[U][R], float (&prod)[U],
       for (int e = 0; e < R; ++e) t[u][e] = hw_sqrt(q[u][e]);
   }
   __builtin_amdgcn_s_setprio(0);
+  if constexpr (VAR == 2) prm.load(r);
 #pragma unroll
   for (int u = 0; u < U; ++u) prod[u] *= prod_tree<R>(q[u]);
   // small |z|: the Taylor form (enf_frag.h) in place of q
@@ -436,7 +441,8 @@ __device__ __forceinline__ void hj_pair_fast(float (&x)[U][R], float (&prod)[U],
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) x[u][e] = asinh2_pick(q[u][e], t[u][e], msel[u][e]);
-  prm.load(r);
+  if constexpr (VAR == 0) prm.load(r);
+  if constexpr (VAR == 1) prm.template load<HJ_B, kHjW>(r);
 }
 
 // The same pair in the exact-range elementwise form: asinh finite up to FLT_MAX (log2(2|z|) above 1e18),
@@ -470,7 +476,7 @@ __device__ __forceinline__ bool hj_redo(const float (&prod)[U]) {
   return group_max<G>(ok ? 0.f : 1.f) != 0.f;
 }
 
-template <int D, int R, int U, int LM, bool PAD = false>
+template <int D, int R, int U, int LM, bool PAD = false, int VAR = 0>
 struct HJBody {
   const HJArgs& a;
   const float* rec;  // this lane's record group
@@ -488,7 +494,7 @@ struct HJBody {
     prm.load(r);
     const uint32_t csign = sign_mask_vgpr();
     // branch-free pair loop; a tile with a product overflow (|z| large, Inf, NaN) is redone below
-    for (int p = 0; p < n; ++p) hj_pair_fast<D, R, U>(x, prod, r, prm, csign);
+    for (int p = 0; p < n; ++p) hj_pair_fast<D, R, U, VAR>(x, prod, r, prm, csign);
     // column-uniform: the exact form's dot products read every lane of a column (DPP)
     if (__builtin_expect(hj_redo<HJLay<D, R, U>::G>(prod), 0)) {
       hj_load<D, R, U, TAIL, DBG, PAD>(a, col0, x);
@@ -501,7 +507,9 @@ struct HJBody {
 #pragma unroll
       for (int u = 0; u < U; ++u) acc[u] = -0.5f * hw_log2(prod[u]);
     }
-    // the output y_n = gamma_n + delta'_n L_n (record n)
+    // the output y_n = gamma_n + delta'_n L_n (record n). (Writing this epilogue out in both branches, so that the
+    // wait-count pass does not see the redo branch's reload of X outstanding at the join, measured the same:
+    // 0.597 vs 0.594 ms, interleaved, profiles/r06_epi_ab_v1.jsonl.)
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -550,7 +558,7 @@ __device__ __forceinline__ void hj_stream(const HJArgs& a, Body& body) {
   }
 }
 
-template <int D, int R, int U, int LM, int OCC, int DBG, bool PAD = false>
+template <int D, int R, int U, int LM, int OCC, int DBG, bool PAD = false, int VAR = 0>
 __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   const int n = a.n;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -560,18 +568,18 @@ __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   float* rec = reinterpret_cast<float*>(smem + kHjHeader);
   build_hj_program<D, R>(a, n, rec, scr, ctotp);
   constexpr int G = HJLay<D, R, U>::G;
-  HJBody<D, R, U, LM, PAD> body{a, rec + ((threadIdx.x & 63) % G) * kHjW * R, *ctotp, stage, n};
+  HJBody<D, R, U, LM, PAD, VAR> body{a, rec + ((threadIdx.x & 63) % G) * kHjW * R, *ctotp, stage, n};
   hj_stream<D, R, U, LM, DBG, PAD>(a, body);
 }
 
-template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, bool PAD = false>
+template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, bool PAD = false, int VAR = 0>
 static hipError_t launch_hj(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
   const size_t lds = hj_lds_bytes(D, h.n);
-  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, PAD>);
+  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, PAD, VAR>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)HJLay<D, R, U>::TC * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, PAD>), dim3((unsigned)blocks), dim3(256), lds, st, h);
+  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, PAD, VAR>), dim3((unsigned)blocks), dim3(256), lds, st, h);
   return hipGetLastError();
 }
 

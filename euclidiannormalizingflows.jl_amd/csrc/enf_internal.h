@@ -26,6 +26,10 @@ constexpr int kStagePerWave = 256;
 constexpr size_t kLdsHeader = kLdsScalars + 4 * kStagePerWave * sizeof(double);
 constexpr size_t kLdsParamBudget = 32 * 1024;  // parameter records per launch
 
+// ENF_NEGLL_ZYGOTE of the running training call (include/enf.h): set by the C API entry for the duration of the
+// call, read when the gradient launch is planned (GradArgs::zq) -- 1: the reported loss omits ScaleShiftTrafo's ladj
+extern thread_local int tl_negll_zygote;
+
 struct LayerDesc {
   int32_t op;
   int32_t k;

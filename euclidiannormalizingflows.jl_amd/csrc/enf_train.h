@@ -94,9 +94,13 @@ __device__ __forceinline__ T dpp_mov(T x) {
 template <int M, typename T>
 __device__ __forceinline__ T add_xor_swap(T x) {
   static_assert(M == 16 || M == 32, "the permlane swaps pair lanes 16 or 32 apart");
+#if defined(__gfx950__)
   // The instruction itself, not the builtin: hipcc 7.2 reads the builtin's second result from the first result's
-  // register for a 32-bit value (the swapped half added to itself; tools/r5/xt/xt.hip checks these against the
-  // shuffles on the GPU). Two wait states between the VALU writes of the operands and the swap.
+  // register for a 32-bit value in this use (the swapped half added to itself: the round-5 run-27 failure, DESIGN
+  // §4). Hazard (gfx950): a v_permlane16/32_swap that reads a VGPR written by a VALU instruction needs two wait
+  // states after that write -- the compiler's own hazard recognizer pads its builtin with the same `s_nop 1`, but
+  // it cannot see into this asm, so the pad is written here. tests/test_gpu_round6.py::test_cross_lane_primitives
+  // checks every group size against the __shfl_xor butterfly bit for bit on the GPU (tests/xlane/).
   struct Pair {
     uint32_t a, b;
   };
@@ -114,6 +118,10 @@ __device__ __forceinline__ T add_xor_swap(T x) {
     const Pair lo = sw((uint32_t)u), hi = sw((uint32_t)(u >> 32));
     return __builtin_bit_cast(T, ((uint64_t)hi.a << 32) | lo.a) + __builtin_bit_cast(T, ((uint64_t)hi.b << 32) | lo.b);
   }
+#else
+  // (other targets -- and the host pass -- have no permlane swaps: the shuffle, bit-identical)
+  return x + __shfl_xor(x, M);
+#endif
 }
 // The xor butterfly over the lanes of a group of P (power of two, <= 64) consecutive lanes, strides P/2 .. 1 in that
 // order: exactly `for (m = P / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m)`. Strides 32 and 16 are permlane swaps,

@@ -31,6 +31,9 @@ const libenf = get(ENV, "ENF_LIBRARY", "libenf.so")
 
 # enums of include/enf.h (checked against the header by tests/test_julia_binding.py)
 const ENF_F32, ENF_F64 = Cint(0), Cint(1)
+# dtype flag of the training calls (include/enf.h): the loss reported is the one the reference records under
+# Zygote -- rrule(similar_fill) makes every ScaleShiftTrafo's primal ladj zero (src/abstract_trafo.jl:30-33)
+const ENF_NEGLL_ZYGOTE = Cint(0x100)
 const OP_SCALESHIFT, OP_CENTER_STRETCH, OP_CENTER_CONTRACT = Int32(0), Int32(1), Int32(2)
 const OP_JOHNSON, OP_JOHNSON_INV, OP_HOUSEHOLDER = Int32(3), Int32(4), Int32(5)
 const ENF_JSU_PDF, ENF_JSU_LOGPDF, ENF_JSU_CDF, ENF_JSU_LOGCDF = Int32(0), Int32(1), Int32(2), Int32(3)
@@ -281,12 +284,12 @@ end
 
 # unnormalised sums: out[1] += N * negll, out[2:end] += its gradient (enf_flow_negll_grad)
 function _negll_grad_sums!(out::HipMatrix{R}, X::HipMatrix{R}, col0::Integer, ncols::Integer, layers,
-                           ws::HipBuffer) where {R}
+                           ws::HipBuffer; zygote::Bool = false) where {R}
     GC.@preserve out X layers ws begin
         check(ccall((:enf_flow_negll_grad, libenf), Cint,
                     (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Ptr{EnfLayer}, Int32, Ptr{Cvoid}, Ptr{Cvoid},
                      Csize_t, Ptr{Cvoid}),
-                    _dt(R), X.D, ncols, X.buf.ptr + col0 * X.D * sizeof(R), X.D, layers, length(layers),
+                    _dt(R) | (zygote ? ENF_NEGLL_ZYGOTE : Cint(0)), X.D, ncols, X.buf.ptr + col0 * X.D * sizeof(R), X.D, layers, length(layers),
                     out.buf.ptr, ws.ptr, ws.bytes, C_NULL))
     end
     out
@@ -312,7 +315,9 @@ function _tangent(f, g, pos, D)
     NamedTuple{names}(Tuple(vals)), pos
 end
 
-function mvnormal_negll_trafograd(trafo::_Supported, X::HipMatrix{T}) where {T}
+# negll as the reference returns it (under Zygote, ScaleShiftTrafo's primal ladj zero: + sum log|a|);
+# similar_fill_quirk = false returns the true negll. The gradient is the same either way.
+function mvnormal_negll_trafograd(trafo::_Supported, X::HipMatrix{T}; similar_fill_quirk::Bool = true) where {T}
     fs = _leaves(trafo)
     R = _flow_eltype(fs, T)
     Xr = _convert(X, R)
@@ -320,7 +325,7 @@ function mvnormal_negll_trafograd(trafo::_Supported, X::HipMatrix{T}) where {T}
     np = _param_count(layers, Xr.D)
     ws = _grad_workspace(R, Xr.D, Xr.N, layers)
     out = HipMatrix(zeros(R, 1 + np, 1))
-    GC.@preserve keep _negll_grad_sums!(out, Xr, 0, Xr.N, layers, ws)
+    GC.@preserve keep _negll_grad_sums!(out, Xr, 0, Xr.N, layers, ws; zygote = similar_fill_quirk)
     g = Array(out)[:, 1] ./ Xr.N
     d_trafo, _ = _tangent(trafo, g, 1, Xr.D)
     g[1], d_trafo
@@ -428,7 +433,8 @@ end
 
 function optimize_whitening(smpls::HipMatrix{T}, initial_trafo::Function, optimizer::Optimisers.ADAGrad;
                             nbatches::Integer = 100, nepochs::Integer = 100, optstate = nothing,
-                            negll_history = Vector{Float64}(), comm::Union{Nothing,EnfComm} = nothing) where {T}
+                            negll_history = Vector{Float64}(), comm::Union{Nothing,EnfComm} = nothing,
+                            similar_fill_quirk::Bool = true) where {T}
     fs = _leaves(initial_trafo)
     R = _flow_eltype(fs, T)
     X = _convert(smpls, R)
@@ -458,6 +464,9 @@ function optimize_whitening(smpls::HipMatrix{T}, initial_trafo::Function, optimi
         push!(layers, EnfLayer(op, k, Tuple(ptrs)))
     end
     world, rank = comm === nothing ? (1, 0) : (comm.nranks, comm.rank)
+    # the training calls' dtype: negll_history as the reference records it (ENF_NEGLL_ZYGOTE) unless
+    # similar_fill_quirk = false
+    dtq = _dt(R) | (similar_fill_quirk ? ENF_NEGLL_ZYGOTE : Cint(0))
     batchsize = max(round(Int, N / nbatches), 1)
     starts = 0:batchsize:N-1
     ws = _grad_workspace(R, D, batchsize, layers)
@@ -478,7 +487,7 @@ function optimize_whitening(smpls::HipMatrix{T}, initial_trafo::Function, optimi
                             (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Int64, Ptr{EnfLayer}, Int32, Ptr{Cvoid}, Ptr{Cvoid},
                              Ptr{Int64}, Int32, Ptr{Int64}, Int32, Cdouble, Cdouble, Ptr{Cdouble}, Ptr{Cvoid},
                              Csize_t, Ptr{Cvoid}),
-                            _dt(R), D, N, X.buf.ptr, D, batchsize, layers, length(layers), theta.buf.ptr,
+                            dtq, D, N, X.buf.ptr, D, batchsize, layers, length(layers), theta.buf.ptr,
                             acc.buf.ptr, runs, length(runs) ÷ 2, hb, length(hb) ÷ 3, rule.eta, rule.epsilon,
                             loss_ptr, ws.ptr, ws.bytes, C_NULL))
                 s += length(starts)
@@ -493,7 +502,7 @@ function optimize_whitening(smpls::HipMatrix{T}, initial_trafo::Function, optimi
                             (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Ptr{EnfLayer}, Int32, Ptr{Cvoid}, Ptr{Cvoid},
                              Ptr{Int64}, Int32, Ptr{Int64}, Int32, Cdouble, Cdouble, Ptr{Cdouble}, Ptr{Cvoid},
                              Csize_t, Ptr{Cvoid}),
-                            _dt(R), D, B, X.buf.ptr + b0 * D * sizeof(R), D, layers, length(layers), theta.buf.ptr,
+                            dtq, D, B, X.buf.ptr + b0 * D * sizeof(R), D, layers, length(layers), theta.buf.ptr,
                             acc.buf.ptr, runs, length(runs) ÷ 2, hb, length(hb) ÷ 3, rule.eta, rule.epsilon,
                             loss_ptr, ws.ptr, ws.bytes, C_NULL))
             elseif isempty(tied) && limits_ok  # data-parallel: gradient, RCCL sum of the rank's totals, update (enf_whitening_step_dp)
@@ -501,12 +510,12 @@ function optimize_whitening(smpls::HipMatrix{T}, initial_trafo::Function, optimi
                             (Cint, Int64, Int64, Ptr{Cvoid}, Int64, Ptr{EnfLayer}, Int32, Ptr{Cvoid}, Ptr{Cvoid},
                              Ptr{Int64}, Int32, Ptr{Int64}, Int32, Cdouble, Cdouble, Int64, Ptr{Cdouble}, Ptr{Cvoid},
                              Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
-                            _dt(R), D, hi - lo, X.buf.ptr + lo * D * sizeof(R), D, layers, length(layers), theta.buf.ptr,
+                            dtq, D, hi - lo, X.buf.ptr + lo * D * sizeof(R), D, layers, length(layers), theta.buf.ptr,
                             acc.buf.ptr, runs, length(runs) ÷ 2, hb, length(hb) ÷ 3, rule.eta, rule.epsilon, B,
                             loss_ptr, comm === nothing ? C_NULL : comm.h, ws.ptr, ws.bytes, C_NULL))
             else      # local sums, cross-rank sum, tied-field sums, then the update on every rank
                 _memcpy(out.buf.ptr, Ptr{Cvoid}(pointer(zero_out)), sizeof(zero_out), MEMCPY_H2D)
-                hi > lo && _negll_grad_sums!(out, X, lo, hi - lo, layers, ws)
+                hi > lo && _negll_grad_sums!(out, X, lo, hi - lo, layers, ws; zygote = similar_fill_quirk)
                 comm === nothing || allreduce_sum!(comm, out)
                 if !isempty(tied)  # the (1 + P) sums are small: fix them up on the host
                     g = Array(out)

@@ -27,11 +27,13 @@ normalised by the GLOBAL minibatch size, so every rank applies the identical upd
 Trainable parameters are the array-valued fields (Optimisers/Functors treat scalar fields as
 constants; Zygote still returns their gradient, summed to a number). A length-1 vector field
 broadcast over the D rows is ONE trainable (its gradient is the sum over the rows; on the device
-its D copies receive that same summed gradient, so they stay equal). Known reference quirk: under Zygote the primal ladj of a
-ScaleShiftTrafo is 0 (rrule(similar_fill), src/abstract_trafo.jl:30-33), so the reference's
-recorded negll misses +sum(log|a|); ``mvnormal_negll_trafograd(..., similar_fill_quirk=True)``
-reproduces that value (the gradient is unaffected either way); optimize_whitening records the
-true negll.
+its D copies receive that same summed gradient, so they stay equal).
+
+Reference quirk, reproduced by default: under Zygote the primal ladj of a ScaleShiftTrafo
+is 0 (rrule(similar_fill), src/abstract_trafo.jl:30-33), so the negll that mvnormal_negll_trafograd returns and
+optimize_whitening records in negll_history is the true negll + sum(log|a|) at the step's parameters (the
+gradient is unaffected). ``similar_fill_quirk=False`` reports the true negll instead. The library computes the
+offset on the device inside the step's own launches (the ENF_NEGLL_ZYGOTE dtype flag, include/enf.h).
 """
 from __future__ import annotations
 
@@ -160,10 +162,10 @@ def _dtype_of(trafo, X):
     return _promote(_kind(X), *[_kind(p) for t in leaves(trafo) for p in t.params()])
 
 
-def _grad_call(state: FlowState, X: torch.Tensor, out: torch.Tensor, ws: torch.Tensor):
+def _grad_call(state: FlowState, X: torch.Tensor, out: torch.Tensor, ws: torch.Tensor, zygote: bool = False):
     D, N = X.shape
     L = _lib.lib()
-    dt = _lib.ENF_F64 if state.dtype == torch.float64 else _lib.ENF_F32
+    dt = (_lib.ENF_F64 if state.dtype == torch.float64 else _lib.ENF_F32) | (_lib.ENF_NEGLL_ZYGOTE if zygote else 0)
     with torch.cuda.device(X.device):
         stream = torch.cuda.current_stream(X.device).cuda_stream
         _lib.check(L.enf_flow_negll_grad(dt, D, N, X.data_ptr(), _ld(X), state.layers(), len(state.trafos),
@@ -178,47 +180,21 @@ def _workspace(state: FlowState, N: int):
     return torch.empty(max(1, nb.value // 8), dtype=torch.float64, device=state.device)
 
 
-def _scaleshift_a_segments(state: FlowState):
-    """(segment index, trafo) of every ScaleShiftTrafo's `a` vector in theta."""
-    out, seg = [], 0
-    for t in state.trafos:
-        for name in t.FIELDS:
-            if isinstance(t, ScaleShiftTrafo) and name == "a":
-                out.append((seg, t))
-            seg += 1
-    return out
-
-
-def _scaleshift_a_range(state: FlowState, seg: int, t) -> tuple:
-    """[start, end) of the entries of a ScaleShiftTrafo's `a` that its ladj sums: all D rows of a
-    length-D vector, the single entry of a length-1 vector (expanded to D copies in theta;
-    src/scale_shift_trafo.jl:22 sums over a's own length)."""
-    s0, s1 = int(state.offsets[seg]), int(state.offsets[seg + 1])
-    return (s0, s0 + 1) if t._k() == 1 else (s0, s1)
-
-
-def _scaleshift_ladj_const(state: FlowState) -> float:
-    c = 0.0
-    th = state.theta.detach().cpu().numpy()
-    for seg, t in _scaleshift_a_segments(state):
-        s0, s1 = _scaleshift_a_range(state, seg, t)
-        c += float(np.sum(np.log(np.abs(th[s0:s1]))))
-    return c
-
-
-def mvnormal_negll_trafograd(trafo, X, similar_fill_quirk: bool = False):
+def mvnormal_negll_trafograd(trafo, X, similar_fill_quirk: bool = True):
     """(negll, gradient) of mvnormal_negll_trafo (src/optimize_whitening.jl:18-22).
 
-    The gradient is returned as a list per transform (application order) of per-field arrays."""
+    negll is the value the reference returns, i.e. under Zygote with the ScaleShiftTrafo ladj's primal taken as 0
+    (+ sum log|a|, module docstring); similar_fill_quirk=False returns the true negll. The gradient is returned as a
+    list per transform (application order) of per-field arrays."""
     M, _, _ = _to_device_matrix(X)
     dtype = _dtype_of(trafo, M)
     M = _colmajor(M, dtype)
     state = FlowState(trafo, M.shape[0], dtype, M.device)
     out = torch.zeros(1 + state.nparams, dtype=dtype, device=M.device)
-    _grad_call(state, M, out, _workspace(state, M.shape[1]))
+    _grad_call(state, M, out, _workspace(state, M.shape[1]), zygote=similar_fill_quirk)
     N = M.shape[1]
     res = (out / N).cpu().numpy()
-    negll = float(res[0]) + (_scaleshift_ladj_const(state) if similar_fill_quirk else 0.0)
+    negll = float(res[0])
     return negll, _tangent(state, res[1:])
 
 
@@ -361,13 +337,13 @@ def allreduce_sum_(buf: torch.Tensor, world: int, group=None) -> torch.Tensor:
 def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None, nbatches: int = 100,
                        nepochs: int = 100, optstate: Optional[FlowState] = None,
                        negll_history: Optional[List[float]] = None, process_group=None,
-                       similar_fill_quirk: bool = False, graph: bool = False, comm=None,
+                       similar_fill_quirk: bool = True, graph: bool = False, comm=None,
                        data_parallel: bool = False,
                        _dp_step: bool = False, _separate_update: bool = False,
                        _per_step: bool = False) -> WhiteningResult:
-    """src/optimize_whitening.jl:25-45 on the device (see module docstring). similar_fill_quirk=True
-    records the negll the reference records under Zygote (ScaleShiftTrafo's primal ladj taken as 0,
-    src/abstract_trafo.jl:30-33: + sum log|a| per sample); the updates are the same either way.
+    """src/optimize_whitening.jl:25-45 on the device (see module docstring). negll_history holds what the reference
+    records under Zygote (ScaleShiftTrafo's primal ladj taken as 0, src/abstract_trafo.jl:30-33: + sum log|a| at
+    each step's parameters); similar_fill_quirk=False records the true negll. The updates are the same either way.
 
     optstate continues a previous run as the reference does (state = deepcopy(optstate), trafo =
     deepcopy(initial_trafo)): the parameters come from initial_trafo, the ADAGrad accumulator and rule
@@ -410,12 +386,12 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
     batchsize = max(B for B, _, _ in plan)
     L = _lib.lib()
     dt = _lib.ENF_F64 if dtype == torch.float64 else _lib.ENF_F32
+    dtq = dt | (_lib.ENF_NEGLL_ZYGOTE if similar_fill_quirk else 0)  # the training calls' dtype (loss reporting)
     out = torch.zeros(1 + state.nparams, dtype=dtype, device=M.device)
     ws = _workspace(state, batchsize)
     hist = torch.zeros(nepochs * len(plan), dtype=torch.float64, device=M.device)
     hbatches = householder_batches(state)
     segs = trainable_runs(state)
-    ss_a = [_scaleshift_a_range(state, i, t) for i, t in _scaleshift_a_segments(state)]
     tied = state.tied_segments()
     # one rank: the fused step (gradient, loss, ADAGrad and re-normalisation in three launches)
     fused = world == 1 and not tied and comm is None
@@ -429,44 +405,36 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
         fused = False
     def one_epoch(hbuf: torch.Tensor, stream: int) -> None:
         """Enqueue the steps of one epoch on `stream`; the loss of step j goes to hbuf[j]."""
-        if fused and not similar_fill_quirk and not _per_step:
+        if fused and not _per_step:
             # the whole epoch in one call (enf_whitening_epoch: one launch when the minibatches fit the one-launch
             # step, else enf_whitening_step per batch; the same result bit for bit)
             _lib.check(L.enf_whitening_epoch(
-                dt, D, N, M.data_ptr(), _ld(M), batchsize, state.layers(), len(state.trafos), state.theta.data_ptr(),
+                dtq, D, N, M.data_ptr(), _ld(M), batchsize, state.layers(), len(state.trafos), state.theta.data_ptr(),
                 state.acc.data_ptr(), runs.ctypes.data, len(segs), hbs.ctypes.data, len(hbatches), optimizer.eta,
                 optimizer.epsilon, hbuf.data_ptr(), ws.data_ptr(), ws.numel() * 8, stream))
             return
         for j, (B, lo, hi) in enumerate(plan):
             if fused and hi > lo:
-                q = []
-                if similar_fill_quirk:  # with the parameters of this step's forward
-                    q = [torch.log(state.theta[s0:s1].abs()).sum() for s0, s1 in ss_a]
                 _lib.check(L.enf_whitening_step(
-                    dt, D, hi - lo, M[:, lo:hi].data_ptr(), _ld(M), state.layers(), len(state.trafos),
+                    dtq, D, hi - lo, M[:, lo:hi].data_ptr(), _ld(M), state.layers(), len(state.trafos),
                     state.theta.data_ptr(), state.acc.data_ptr(), runs.ctypes.data, len(segs), hbs.ctypes.data,
                     len(hbatches), optimizer.eta, optimizer.epsilon, hbuf[j:].data_ptr(), ws.data_ptr(),
                     ws.numel() * 8, stream))
-                for t in q:
-                    hbuf[j:j + 1] += t
                 continue
-            if comm is not None and not tied and apply_fused and not similar_fill_quirk:
+            if comm is not None and not tied and apply_fused:
                 # data-parallel in one call: gradient of the share, RCCL sum of the kernels' double slice totals,
                 # one tail launch (enf_whitening_step_dp; round 4)
                 _lib.check(L.enf_whitening_step_dp(
-                    dt, D, hi - lo, M[:, lo:hi].data_ptr() if hi > lo else None, _ld(M), state.layers(),
+                    dtq, D, hi - lo, M[:, lo:hi].data_ptr() if hi > lo else None, _ld(M), state.layers(),
                     len(state.trafos), state.theta.data_ptr(), state.acc.data_ptr(), runs.ctypes.data, len(segs),
                     hbs.ctypes.data, len(hbatches), optimizer.eta, optimizer.epsilon, B, hbuf[j:].data_ptr(),
                     comm.handle, ws.data_ptr(), ws.numel() * 8, stream))
                 continue
             # data-parallel: local sums, cross-rank sum, then the update on every rank
-            q = []
-            if similar_fill_quirk:  # with the parameters of this step's forward
-                q = [torch.log(state.theta[s0:s1].abs()).sum() for s0, s1 in ss_a]
             out.zero_()
             if hi > lo:
                 Xb = M[:, lo:hi]
-                _lib.check(L.enf_flow_negll_grad(dt, D, hi - lo, Xb.data_ptr(), _ld(M), state.layers(),
+                _lib.check(L.enf_flow_negll_grad(dtq, D, hi - lo, Xb.data_ptr(), _ld(M), state.layers(),
                                                  len(state.trafos), out.data_ptr(), ws.data_ptr(),
                                                  ws.numel() * 8, stream))
             if comm is not None:
@@ -490,8 +458,6 @@ def optimize_whitening(smpls, initial_trafo, optimizer: Optional[ADAGrad] = None
                 for off, k, ldv in hbatches:
                     _lib.check(L.enf_householder_normalize_strided(dt, D, k, state.theta[off:].data_ptr(), ldv,
                                                                    stream))
-            for t in q:
-                hbuf[j:j + 1] += t
 
     P = len(plan)
     with torch.cuda.device(M.device):

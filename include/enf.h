@@ -53,6 +53,15 @@ typedef enum {
 } enf_status;
 
 typedef enum { ENF_F32 = 0, ENF_F64 = 1 } enf_dtype;
+/* Flag OR'd into the dtype of the training entry points (enf_flow_negll_grad, enf_whitening_step,
+ * enf_whitening_epoch, enf_whitening_step_dp): the loss they report is the one the reference RECORDS,
+ * mvnormal_negll_trafo under Zygote.pullback (src/optimize_whitening.jl:18-22, 36-41), where
+ * rrule(similar_fill) returns zeros as the primal (src/abstract_trafo.jl:30-33), so every ScaleShiftTrafo's
+ * ladj sum(log|a|) (src/scale_shift_trafo.jl:22-23) is missing from it: the reported loss is the true negll +
+ * sum log|a| at the step's parameters (the unnormalised out[0] of enf_flow_negll_grad: + N sum log|a|). The
+ * gradient is unchanged (the rrule's pullback passes sum(dOmega) to the ladj value). Without the flag the
+ * true negll is reported. */
+#define ENF_NEGLL_ZYGOTE 0x100
 
 /* Transform kinds; params p[0..3] are DEVICE pointers to length-D vectors of the flow's dtype
  * (a Julia scalar parameter is broadcast to length D by the host). */

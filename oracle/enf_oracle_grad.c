@@ -194,17 +194,20 @@
     return rc;                                                                                         \
   }                                                                                                    \
   /* optimize_whitening (optimize_whitening.jl:25-45) over Ntot columns X in nbatches minibatches of        */ \
-  /* round(Ntot / nbatches) (Iterators.partition: the last one shorter), nepochs epochs: per minibatch   */ \
+  /* round(Ntot / nbatches), ties to even (Julia round(Int, x), optimize_whitening.jl:31; Iterators.partition: the last one shorter), nepochs epochs: per minibatch   */ \
   /* the gradient above, Optimisers.update with ADAGrad(eta, epsilon) (acc += g^2; theta -= eta g /      */ \
   /* (sqrt(acc) + epsilon), acc starting at epsilon) on every parameter, then the HouseholderTrafo        */ \
   /* functor's normalize! of each V column (householder_trafo.jl:134-146). The layers' parameter         */ \
   /* pointers must point into theta (enf layout, nparams = or_param_count); acc has nparams entries.     */ \
-  /* hist receives nepochs * nbatches_actual losses. Returns the number of steps, or -1.                 */ \
+  /* hist receives nepochs * nbatches_actual losses: with zygote != 0 the loss the reference RECORDS,     */ \
+  /* i.e. under Zygote.pullback, where rrule(similar_fill) makes every ScaleShiftTrafo's primal ladj zero */ \
+  /* (abstract_trafo.jl:30-33): + sum_d log|a_d| at the step's parameters. Returns the number of steps,  */ \
+  /* or -1.                                                                                              */ \
   int64_t or_optimize_whitening_##S(int64_t D, int64_t Ntot, const T* X, const oracle_layer* layers,     \
                                     int32_t nlayers, T* theta, T* acc, int64_t nbatches, int64_t nepochs, \
-                                    T eta, T eps, T* hist) {                                           \
+                                    T eta, T eps, T* hist, int32_t zygote) {                           \
     const int64_t np = or_param_count_##S(D, layers, nlayers);                                          \
-    int64_t bs = (int64_t)llround((double)Ntot / (double)nbatches);                                   \
+    int64_t bs = (int64_t)nearbyint((double)Ntot / (double)nbatches); /* ties to even, as round(Int, .) */ \
     if (bs < 1) bs = 1;                                                                                \
     T* out = (T*)malloc((size_t)(1 + np) * sizeof(T));                                                 \
     int64_t step = 0;                                                                                  \
@@ -215,7 +218,11 @@
           free(out);                                                                                   \
           return -1;                                                                                   \
         }                                                                                              \
-        hist[step++] = out[0];                                                                         \
+        T rec = out[0];                                                                                \
+        for (int32_t l = 0; zygote && l < nlayers; ++l)                                                \
+          if (layers[l].op == OR_SCALESHIFT)                                                           \
+            for (int64_t d = 0; d < D; ++d) rec += LOG(FABS(((const T*)layers[l].p[0])[d]));             \
+        hist[step++] = rec;                                                                            \
         for (int64_t i = 0; i < np; ++i) {                                                             \
           const T g = out[1 + i];                                                                      \
           acc[i] = acc[i] + g * g;                                                                     \

@@ -75,7 +75,8 @@ def lib() -> ctypes.CDLL:
             f = getattr(_lib, f"or_optimize_whitening_{S}")
             f.restype = ctypes.c_int64
             f.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.POINTER(_Layer), ctypes.c_int32,
-                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, T, T, ctypes.c_void_p]
+                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, T, T, ctypes.c_void_p,
+                          ctypes.c_int32]
         f = _lib.or_norminvcdf_f64
         f.restype, f.argtypes = ctypes.c_double, [ctypes.c_double]
         f = _lib.or_jsu_eval_vec_f64
@@ -240,9 +241,19 @@ def negll_grad(layers, X: np.ndarray):
     return float(out[0]), out[1:]
 
 
-def optimize_whitening(layers, X: np.ndarray, nbatches: int, nepochs: int, eta: float = 0.1, epsilon: float = 1e-8):
+def scaleshift_ladj(layers) -> float:
+    """sum log|a| over the flow's ScaleShiftTrafos (src/scale_shift_trafo.jl:22, over a's own length): what the
+    reference's recorded negll carries extra under Zygote, where rrule(similar_fill) makes that ladj's primal zero
+    (src/abstract_trafo.jl:30-33)."""
+    return float(sum(np.sum(np.log(np.abs(np.asarray(ps[0], np.float64)))) for op, ps in layers if op == OP_SCALESHIFT))
+
+
+def optimize_whitening(layers, X: np.ndarray, nbatches: int, nepochs: int, eta: float = 0.1, epsilon: float = 1e-8,
+                       zygote: bool = False):
     """optimize_whitening (src/optimize_whitening.jl:25-45) with ADAGrad(eta, epsilon) on the CPU: returns
-    (theta, acc, negll_history), theta in the theta_of layout."""
+    (theta, acc, negll_history), theta in the theta_of layout. zygote=True records the loss as the reference does
+    under Zygote (scaleshift_ladj of the step's parameters added to every entry); False the true negll. The
+    minibatch size is round(N / nbatches) with ties to even, as Julia's round(Int, x) (optimize_whitening.jl:31)."""
     X = np.asfortranarray(X)
     D, N = X.shape
     S = _grad_dtype(X.dtype)
@@ -252,7 +263,8 @@ def optimize_whitening(layers, X: np.ndarray, nbatches: int, nepochs: int, eta: 
     bs = max(int(round(N / nbatches)), 1)
     hist = np.zeros(nepochs * (-(-N // bs)), dtype=X.dtype)
     n = getattr(lib(), f"or_optimize_whitening_{S}")(D, N, X.ctypes.data, arr, len(layers), theta.ctypes.data,
-                                                     acc.ctypes.data, nbatches, nepochs, eta, epsilon, hist.ctypes.data)
+                                                     acc.ctypes.data, nbatches, nepochs, eta, epsilon, hist.ctypes.data,
+                                                     1 if zygote else 0)
     if n < 0:
         raise ValueError("oracle: unknown op in flow")
     return theta, acc, hist[:n]

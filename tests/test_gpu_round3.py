@@ -44,7 +44,7 @@ def test_negll_grad_large_D_finite_differences(enf, gpu, oracle, D):
     rng = np.random.default_rng(1000 + D)
     layers = mixed_layers(rng, D, np.float64)
     X = np.asfortranarray(0.8 * rng.standard_normal((D, 301)))
-    negll, grads = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X))
+    negll, grads = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X), similar_fill_quirk=False)
     ref = oracle_negll(oracle, layers, X)
     assert loss_close(negll, ref, 1e-12), (negll, ref)
     g = np.concatenate([np.asarray(a).reshape(-1, order="F") for per in grads for a in per])
@@ -64,7 +64,7 @@ def test_negll_grad_D256_fp32(enf, gpu, oracle):
     layers = [(5, rand_params(rng, 5, D, np.float32)), (3, rand_params(rng, 3, D, np.float32)),
               (0, rand_params(rng, 0, D, np.float32)), (4, rand_params(rng, 4, D, np.float32))]
     X = np.asfortranarray((0.8 * rng.standard_normal((D, 2049))).astype(np.float32))
-    n32, g32 = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X))
+    n32, g32 = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X), similar_fill_quirk=False)
     l64 = [(op, [np.asarray(p, np.float64) for p in ps]) for op, ps in layers]
     X64 = np.asfortranarray(X.astype(np.float64))
     ref = oracle_negll(oracle, l64, X64)
@@ -156,7 +156,7 @@ def test_scaleshift_length1_a_ladj_and_gradient(enf, gpu, dtype):
     # host path (enf_flow_apply_cpu) agrees
     Yh, Lh = enf.with_logabsdet_jacobian(f, X)
     assert np.allclose(np.asarray(Lh).reshape(-1), np.log(abs(a)), rtol=tol, atol=tol)
-    negll, grads = enf.mvnormal_negll_trafograd(f, colmajor_cuda(X))
+    negll, grads = enf.mvnormal_negll_trafograd(f, colmajor_cuda(X), similar_fill_quirk=False)
     X64 = X.astype(np.float64)
     Y64 = a * X64 + b
     want_negll = ((Y64 ** 2 + np.log(2 * np.pi)) / 2).sum() / N - np.log(abs(a))
@@ -193,7 +193,7 @@ def test_mvnormal_negll_trafo_device_reduction(enf, gpu, oracle, dtype, D):
     tol = 2e-5 if dtype == np.float32 else 1e-11
     assert abs(got - ref) <= tol * (abs(ref) + 1), (got, ref)
     if D <= 256:
-        ng, _ = enf.mvnormal_negll_trafograd(f, colmajor_cuda(X))
+        ng, _ = enf.mvnormal_negll_trafograd(f, colmajor_cuda(X), similar_fill_quirk=False)
         assert abs(got - ng) <= tol * (abs(ref) + 1)
 
 

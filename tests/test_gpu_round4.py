@@ -189,7 +189,7 @@ def test_negll_grad_20_layers_finite_differences(enf, gpu, oracle):
     D = 5
     layers = _long_flow(rng, D, np.float64)
     X = np.asfortranarray(0.8 * rng.standard_normal((D, 257)))
-    negll, grads = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X))
+    negll, grads = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X), similar_fill_quirk=False)
     ref = oracle_negll(oracle, layers, X)
     assert loss_close(negll, ref, 1e-12), (negll, ref)
     g = np.concatenate([np.asarray(a).reshape(-1, order="F") for per in grads for a in per])
@@ -217,7 +217,7 @@ def test_negll_grad_chained_householder_40_columns(enf, gpu, oracle):
     layers = [(3, rand_params(rng, 3, D, np.float64)), (5, rand_params(rng, 5, D, np.float64, K=40)),
               (3, rand_params(rng, 3, D, np.float64))]
     X = np.asfortranarray(0.8 * rng.standard_normal((D, 301)))
-    negll, grads = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X))
+    negll, grads = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X), similar_fill_quirk=False)
     ref = oracle_negll(oracle, layers, X)
     assert loss_close(negll, ref, 1e-12), (negll, ref)
     g = np.concatenate([np.asarray(a).reshape(-1, order="F") for per in grads for a in per])
@@ -261,7 +261,7 @@ def test_negll_grad_large_D_fp32(enf, gpu, oracle, D):
               (3, rand_params(rng, 3, D, np.float32)), (0, rand_params(rng, 0, D, np.float32)),
               (2, rand_params(rng, 2, D, np.float32)), (1, rand_params(rng, 1, D, np.float32))]
     X = np.asfortranarray((0.8 * rng.standard_normal((D, 1025))).astype(np.float32))
-    n32, g32 = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X))
+    n32, g32 = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X), similar_fill_quirk=False)
     l64 = [(op, [np.asarray(p, np.float64) for p in ps]) for op, ps in layers]
     X64 = np.asfortranarray(X.astype(np.float64))
     ref = oracle_negll(oracle, l64, X64)
@@ -282,7 +282,7 @@ def test_negll_grad_large_D_fp64_chunked(enf, gpu, oracle):
     D = 300
     layers = mixed_layers(rng, D, np.float64)
     X = np.asfortranarray(0.8 * rng.standard_normal((D, 129)))
-    negll, grads = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X))
+    negll, grads = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X), similar_fill_quirk=False)
     ref = oracle_negll(oracle, layers, X)
     assert loss_close(negll, ref, 1e-12), (negll, ref)
     g = np.concatenate([np.asarray(a).reshape(-1, order="F") for per in grads for a in per])

@@ -165,7 +165,7 @@ def test_negll_grad_vs_oracle_reverse_pass(enf, gpu, oracle, D):
     rng = np.random.default_rng(5400 + D)
     layers = [(op, rand_params(rng, op, D, np.float64, K=2 if op == 5 else 1)) for op in [0, 5, 2, 3, 1, 4, 5, 3]]
     X = np.asfortranarray(0.8 * rng.standard_normal((D, 4001)))
-    negll, grads = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X))
+    negll, grads = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X), similar_fill_quirk=False)
     g = np.concatenate([np.asarray(a).reshape(-1, order="F") for per in grads for a in per])
     n_ref, g_ref = oracle.negll_grad(layers, X)
     assert loss_close(negll, n_ref, 1e-12), (negll, n_ref)
@@ -201,7 +201,9 @@ def test_examples_training_vs_oracle(enf, gpu, oracle, example):
     X, _ = oracle.flow_apply(true, XW)
     X = np.asfortranarray(X)
     opt = enf.ADAGrad()  # Optimisers 0.2 defaults: eta = 0.1f0, epsilon = eps(Float32)
-    th_ref, _, hist_ref = oracle.optimize_whitening(init, X, nbatches=50, nepochs=1, eta=opt.eta, epsilon=opt.epsilon)
+    # (the reference's recorded history, round 6: under Zygote the 2d flow's ScaleShift ladj is missing from it)
+    th_ref, _, hist_ref = oracle.optimize_whitening(init, X, nbatches=50, nepochs=1, eta=opt.eta, epsilon=opt.epsilon,
+                                                    zygote=True)
     r = enf.optimize_whitening(colmajor_cuda(X), make_flow(enf, init), opt, nbatches=50, nepochs=1)
     hist = np.asarray(r.negll_history)
     assert hist.shape == hist_ref.shape
