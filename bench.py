@@ -361,7 +361,13 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--D", type=int, default=32)
-    ap.add_argument("--N", type=int, default=10_000_000, help="samples per GPU")
+    ap.add_argument("--N", type=int, default=10_000_000,
+                    help="samples per GPU (--scaling weak, the default) or in all (--scaling strong)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: every rank streams its own N columns (the default line); strong: the N columns are "
+                         "split over the ranks in contiguous shards (rank r: [N r/world, N (r+1)/world)), value = N x "
+                         "steps / the max-over-ranks time -- the fixed-size reading of the metric's 'N=1e7 at 1/2/4/8 "
+                         "GPUs' (VERDICT r05 item 6)")
     ap.add_argument("--pairs", type=int, default=4, help="number of (Householder, Johnson) pairs")
     ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
     ap.add_argument("--settle-ms", type=float, default=200.0,
@@ -421,7 +427,11 @@ def main():
     np_dtype = np.float32 if args.dtype == "f32" else np.float64
     t_dtype = torch.float32 if args.dtype == "f32" else torch.float64
     esz = 4 if args.dtype == "f32" else 8
-    D, N = args.D, args.N
+    D = args.D
+    strong = args.scaling == "strong"
+    # this rank's columns: all N per rank (weak), or its contiguous shard of the N columns (strong)
+    N = (args.N * (rank + 1)) // world - (args.N * rank) // world if strong else args.N
+    N_total = args.N if strong else args.N * world
     set_bytes = N * (2 * D + 1) * esz  # one launch's X, Y and ladj
     fwd_layers = build_flow(D, args.pairs, np_dtype, pattern=args.pattern)
     layers = invert_layers(fwd_layers) if args.inverse else fwd_layers
@@ -598,7 +608,7 @@ def main():
     t_local, kern_ms_max = max_over_ranks([wall, kern_ms], dev, world)
     per_rank_kernel_ms = gather_ranks(kern_ms, dev, world, rank)
     ms_per_step = t_local / args.steps * 1e3
-    total_samples = N * world * args.steps
+    total_samples = N_total * args.steps
     value = total_samples / t_local
 
     bytes_per_launch = bytes_per_launch_of(N, D, esz)
@@ -621,7 +631,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu and not args.selftest_cpu and not args.inverse:
         cpu = cpu_baseline(layers, D, np_dtype, args.cpu_seconds)
     train = None
-    headline = (D, N, args.pairs, args.dtype, args.pattern, args.inverse) == (32, 10_000_000, 4, "f32", None, False)
+    headline = (D, N, args.pairs, args.dtype, args.pattern, args.inverse, strong) == (32, 10_000_000, 4, "f32", None,
+                                                                                     False, False)
     if args.selftest_cpu and not args.no_train:  # the config-5 leg's rank plumbing on gloo
         import bench_train
 
@@ -646,7 +657,7 @@ def main():
             "timing": ("one HIP graph replay of the K launches (events around it; no host launch cost)" if use_graph
                        else "eager launches, HIP events between consecutive launches"),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": ("selftest (CPU stand-in step, measures nothing)" if args.selftest_cpu else
@@ -655,8 +666,10 @@ def main():
             "config": {"workload": (f"inverse of {'∘'.join(reversed(layer_letters(fwd_layers)))} = "
                                     if args.inverse else "")
                                    + f"{'∘'.join(reversed(layer_letters(layers)))} composed flow "
-                                   f"fwd+ladj, D={D}, N={N} per GPU",
-                       "D": D, "N_per_gpu": N, "layers": len(layers), "parallelism": f"sample-shard x{world}"},
+                                   + (f"fwd+ladj, D={D}, N={args.N} in all, split over {world} GPU(s)" if strong
+                                      else f"fwd+ladj, D={D}, N={N} per GPU"),
+                       "D": D, "N_per_gpu": N, "N_total": N_total, "layers": len(layers),
+                       "parallelism": f"sample-shard x{world}"},
             "distributed": {"world_size": world, "backend": backend if world > 1 else None,
                             "data_path_collective": None, "per_rank_kernel_ms": per_rank_kernel_ms},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -43,12 +43,24 @@ def test_bench_launches_two_ranks():
     assert len(d["per_rank_kernel_ms"]) == 2 and all(v > 0 for v in d["per_rank_kernel_ms"])
     # whole-job aggregate: both ranks' samples over the max-over-ranks wall time
     assert out["value"] == pytest.approx(2 * 1000 * 3 / (out["ms_per_step"] * 3 / 1e3), rel=1e-6)
-    assert out["scaling"] == "weak"
+    assert out["scaling"] == "weak" and out["config"]["N_total"] == 2000
     # the config-5 leg at N = 2: minibatch shares tile every batch, the ranks agree, and the step the GPU
     # run times is the graph-captured libenf RCCL (EnfComm) data-parallel step
     t = out["train"]
     assert t["n_gpus"] == 2 and t["ranks_agree"] and len(t["per_rank_s"]) == 2
     assert "EnfComm" in t["step"] and "captured in the HIP graph" in t["step"]
+
+
+@pytest.mark.parametrize("gpus", [1, 2, 3])
+def test_bench_strong_scaling_line(gpus):
+    """--scaling strong: the N = 1000 columns are split over the ranks in contiguous shards
+    (1000 = 333 + 333 + 334 at three ranks), value = N x steps / the max-over-ranks time, "scaling": "strong"."""
+    out = run_bench("--gpus", str(gpus), "--scaling", "strong", "--no-train")
+    assert out["n_gpus"] == gpus and out["scaling"] == "strong"
+    c = out["config"]
+    assert c["N_total"] == 1000 and c["N_per_gpu"] == 1000 // gpus  # (rank 0: [0, 1000 // gpus))
+    assert "in all, split over" in c["workload"]
+    assert out["value"] == pytest.approx(1000 * 3 / (out["ms_per_step"] * 3 / 1e3), rel=1e-6)
 
 
 def test_bench_world_mismatch_is_an_error():
