@@ -257,13 +257,10 @@ template <int LM>
 static hipError_t dispatch_hj(const HJArgs& a, int D, int dbg, hipStream_t st, const DeviceInfo& dev) {
 #if ENF_DIAG
   // diagnostics build only: ENF_DEBUG_MODE 1 = synthesized tile, 2 = no stores either (compute-only timing);
-  // ENF_HJ_R16 = 16 rows per lane, one column per lane tile (two lanes per column at D = 32); ENF_HJ_VAR: the
-  // placement of the next record's LDS reads (hj_pair_fast)
+  // ENF_HJ_R16 = 16 rows per lane, one column per lane tile (two lanes per column at D = 32; spills at this record
+  // count)
   if (a.dreal == D && LM == 1) {
     static const int r16 = ENF_KNOB("ENF_HJ_R16", 0);
-    static const int var = ENF_KNOB("ENF_HJ_VAR", 0);
-    if (dbg == 0 && D == 32 && var == 1) return launch_hj<32, 8, 2, 1, 4, 0, false, 1>(a, st, dev);
-    if (dbg == 0 && D == 32 && var == 2) return launch_hj<32, 8, 2, 1, 4, 0, false, 2>(a, st, dev);
     if (dbg == 1) return launch_hj<32, 8, 2, 1, 4, 1>(a, st, dev);
     if (dbg == 2) return launch_hj<32, 8, 2, 1, 4, 2>(a, st, dev);
     if (r16 && D == 32) return launch_hj<32, 16, 1, 1, 4>(a, st, dev);

@@ -202,7 +202,8 @@ __device__ __forceinline__ void hj_store(const HJArgs& a, float ctot, int64_t co
 #pragma unroll
     for (int k = 0; k < L::NLS; ++k) {
       const int c = k * 64 + (L::TC >= 64 ? lane : lane % L::TC);
-      const float v = fmaf((float)kLn2, stage[c], ctot) + old[k];
+      const float w = fmaf((float)kLn2, stage[c], ctot);
+      const float v = LM == 2 ? w + old[k] : w;  // (LM 1: no add of the zero `old`)
       const int64_t col = col0 + c;
       if ((!TAIL && ENF_INB(col < a.N, "hj ladj", col, a.N)) || (TAIL && col < a.N)) ladj[col] = v;
     }
@@ -286,10 +287,9 @@ __device__ void build_hj_program(const HJArgs& a, int n, float* __restrict__ rec
 template <int R>
 struct HJParams {
   float v[kHjW][R];
-  template <int Q0 = 0, int Q1 = kHjW>
   __device__ __forceinline__ void load(const float* r) {
 #pragma unroll
-    for (int k = Q0; k < Q1; ++k)
+    for (int k = 0; k < kHjW; ++k)
 #pragma unroll
       for (int h = 0; h < R / 4; ++h) lds_vec<float, 4>(r + k * R + 4 * h, *reinterpret_cast<float(*)[4]>(&v[k][4 * h]));
   }
@@ -299,20 +299,32 @@ struct HJParams {
 // Householder dot of every column of the tile: two independent partial chains per column (even
 // and odd rows) over the lane's R rows, then log2(G) DPP stages across the G lanes of the column.
 // (Q: the record slot of the row weights in the parameter set P)
-template <int D, int R, int U, int Q = HJ_W, typename P = HJParams<R>>
+// CH: partial chains per column -- 1 (product, round 6): one chain of R, no add; 2 (rounds 1-5): even / odd rows,
+// one add to combine. One chain: 0.595 vs 0.603 ms on config 3 (9.08M vs 9.35M cycles, interleaved A/B,
+// profiles/r06_ballot_ab_v1.jsonl): the dependent FMAs hide behind the other column and the other waves.
+template <int D, int R, int U, int Q = HJ_W, typename P = HJParams<R>, int CH = 1>
 __device__ __forceinline__ void hj_dots(const float (&y)[U][R], const P& prm, float (&dot)[U]) {
   constexpr int G = HJLay<D, R, U>::G;
-  float d2[U][2];
+  if constexpr (CH == 1) {
 #pragma unroll
-  for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) dot[u] = prm.m(Q, 0) * y[u][0];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) d2[u][c] = prm.m(Q, c) * y[u][c];
+    for (int e = 1; e < R; ++e)
 #pragma unroll
-  for (int e = 2; e < R; ++e)
+      for (int u = 0; u < U; ++u) dot[u] = fmaf(prm.m(Q, e), y[u][e], dot[u]);
+  } else {
+    float d2[U][2];
 #pragma unroll
-    for (int u = 0; u < U; ++u) d2[u][e & 1] = fmaf(prm.m(Q, e), y[u][e], d2[u][e & 1]);
+    for (int u = 0; u < U; ++u)
 #pragma unroll
-  for (int u = 0; u < U; ++u) dot[u] = d2[u][0] + d2[u][1];
+      for (int c = 0; c < 2; ++c) d2[u][c] = prm.m(Q, c) * y[u][c];
+#pragma unroll
+    for (int e = 2; e < R; ++e)
+#pragma unroll
+      for (int u = 0; u < U; ++u) d2[u][e & 1] = fmaf(prm.m(Q, e), y[u][e], d2[u][e & 1]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) dot[u] = d2[u][0] + d2[u][1];
+  }
   if constexpr (G >= 2) {
 #pragma unroll
     for (int u = 0; u < U; ++u) dot[u] += dpp<0xB1>(dot[u]);
@@ -375,18 +387,16 @@ __device__ __forceinline__ void hj_front(float (&x)[U][R], const HJParams<R>& pr
 
 // One pair (reflection + Johnson) on the register tile, fast form. x holds L_{p-1} (pair 0: the input x)
 // on entry and L_p on exit; prm holds this pair's record on entry and the next one's on exit (r is
-// advanced to it; read after the asinh's temporaries are dead: 128 VGPRs and 65 spilled when the reads
-// were issued before the asinh). prod[u] accumulates the product of the
+// advanced to it; read after the asinh's temporaries are dead: 128 VGPRs and 65 spilled when the reads were
+// issued before the asinh, and reading W early and the rest late measured no better, profiles/r06_var_ab_v1.jsonl).
+// prod[u] accumulates the product of the
 // q = 1 + z^2 of the lane's R rows of column u (+Inf / NaN: the fast form is not valid for the tile).
 // asinh: the mask-first merge asinh2_mask / asinh2_pick of the Taylor form and the log form (enf_frag.h).
-// VAR (diagnostics build, ENF_HJ_VAR): where the next record's LDS reads are issued -- 0 (product) after the
-// pick, 1 = W after the front and B, A, C after the pick, 2 = all after the sqrt group.
-template <int D, int R, int U, int VAR = 0>
+template <int D, int R, int U>
 __device__ __forceinline__ void hj_pair_fast(float (&x)[U][R], float (&prod)[U], const float*& r, HJParams<R>& prm,
                                              uint32_t csign) {
   hj_front<D, R, U>(x, prm);
   r += kHjW * D;
-  if constexpr (VAR == 1) prm.template load<HJ_W, HJ_W + 1>(r);
   // stage by stage over the whole tile (U*R independent chains per stage)
   float q[U][R], t[U][R];
   uint32_t msel[U][R];  // the select mask of asinh2_pick, from q (before the transcendentals)
@@ -414,7 +424,6 @@ __device__ __forceinline__ void hj_pair_fast(float (&x)[U][R], float (&prod)[U],
       for (int e = 0; e < R; ++e) t[u][e] = hw_sqrt(q[u][e]);
   }
   __builtin_amdgcn_s_setprio(0);
-  if constexpr (VAR == 2) prm.load(r);
 #pragma unroll
   for (int u = 0; u < U; ++u) prod[u] *= prod_tree<R>(q[u]);
   // small |z|: the Taylor form (enf_frag.h) in place of q
@@ -441,8 +450,7 @@ __device__ __forceinline__ void hj_pair_fast(float (&x)[U][R], float (&prod)[U],
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) x[u][e] = asinh2_pick(q[u][e], t[u][e], msel[u][e]);
-  if constexpr (VAR == 0) prm.load(r);
-  if constexpr (VAR == 1) prm.template load<HJ_B, kHjW>(r);
+  prm.load(r);
 }
 
 // The same pair in the exact-range elementwise form: asinh finite up to FLT_MAX (log2(2|z|) above 1e18),
@@ -464,19 +472,24 @@ __device__ __forceinline__ void hj_pair_exact(float (&x)[U][R], float (&acc)[U],
     }
 }
 
-// Whether the fast form is invalid for any column of the lane's tile, the same on every lane of a column:
-// a running q product that is not finite. (Tested as a flag, not as a max of the products: an overflow in
-// one pair is followed by Inf * 0 = NaN products in the next ones when the huge z turn into Inf - Inf in the
-// next front, and fmaxf drops NaN operands.)
+// Whether the fast form is invalid for a column of the lane's tile, the same on the G lanes of a column: a running
+// q product that is not finite. (Tested per lane as a flag, not as a max of the products: an overflow in one pair
+// is followed by Inf * 0 = NaN products in the next ones when the huge z turn into Inf - Inf in the next front,
+// and fmaxf drops NaN operands. The flags of the wave by one ballot, then the lane's G-bit group of it: fewer
+// VALU operations than a DPP max over the group. A wave-uniform test, redoing the whole wave tile, made the
+// compiler spill 97 VGPRs.)
 template <int G, int U>
 __device__ __forceinline__ bool hj_redo(const float (&prod)[U]) {
   bool ok = true;
 #pragma unroll
   for (int u = 0; u < U; ++u) ok = ok && prod[u] <= FLT_MAX;
-  return group_max<G>(ok ? 0.f : 1.f) != 0.f;
+  const uint64_t bad = __builtin_amdgcn_ballot_w64(!ok);
+  if (bad == 0) return false;  // (uniform: the common case takes no per-lane work)
+  const int lane = threadIdx.x & 63;
+  return ((bad >> (lane & ~(G - 1))) & ((G >= 64 ? ~0ull : (1ull << G) - 1))) != 0;
 }
 
-template <int D, int R, int U, int LM, bool PAD = false, int VAR = 0>
+template <int D, int R, int U, int LM, bool PAD = false>
 struct HJBody {
   const HJArgs& a;
   const float* rec;  // this lane's record group
@@ -494,8 +507,8 @@ struct HJBody {
     prm.load(r);
     const uint32_t csign = sign_mask_vgpr();
     // branch-free pair loop; a tile with a product overflow (|z| large, Inf, NaN) is redone below
-    for (int p = 0; p < n; ++p) hj_pair_fast<D, R, U, VAR>(x, prod, r, prm, csign);
-    // column-uniform: the exact form's dot products read every lane of a column (DPP)
+    for (int p = 0; p < n; ++p) hj_pair_fast<D, R, U>(x, prod, r, prm, csign);
+    // wave-uniform: the exact form's dot products read every lane of a column (DPP)
     if (__builtin_expect(hj_redo<HJLay<D, R, U>::G>(prod), 0)) {
       hj_load<D, R, U, TAIL, DBG, PAD>(a, col0, x);
 #pragma unroll
@@ -558,7 +571,7 @@ __device__ __forceinline__ void hj_stream(const HJArgs& a, Body& body) {
   }
 }
 
-template <int D, int R, int U, int LM, int OCC, int DBG, bool PAD = false, int VAR = 0>
+template <int D, int R, int U, int LM, int OCC, int DBG, bool PAD = false>
 __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   const int n = a.n;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -568,18 +581,18 @@ __global__ __launch_bounds__(256, OCC) void flow_hj_kernel(HJArgs a) {
   float* rec = reinterpret_cast<float*>(smem + kHjHeader);
   build_hj_program<D, R>(a, n, rec, scr, ctotp);
   constexpr int G = HJLay<D, R, U>::G;
-  HJBody<D, R, U, LM, PAD, VAR> body{a, rec + ((threadIdx.x & 63) % G) * kHjW * R, *ctotp, stage, n};
+  HJBody<D, R, U, LM, PAD> body{a, rec + ((threadIdx.x & 63) % G) * kHjW * R, *ctotp, stage, n};
   hj_stream<D, R, U, LM, DBG, PAD>(a, body);
 }
 
-template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, bool PAD = false, int VAR = 0>
+template <int D, int R, int U, int LM, int OCC = 1, int DBG = 0, bool PAD = false>
 static hipError_t launch_hj(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
   const size_t lds = hj_lds_bytes(D, h.n);
-  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, PAD, VAR>);
+  const void* k = reinterpret_cast<const void*>(&flow_hj_kernel<D, R, U, LM, OCC, DBG, PAD>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)HJLay<D, R, U>::TC * 4, lds, dev, &blocks);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, PAD, VAR>), dim3((unsigned)blocks), dim3(256), lds, st, h);
+  hipLaunchKernelGGL((flow_hj_kernel<D, R, U, LM, OCC, DBG, PAD>), dim3((unsigned)blocks), dim3(256), lds, st, h);
   return hipGetLastError();
 }
 
