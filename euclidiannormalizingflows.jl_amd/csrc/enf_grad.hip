@@ -741,6 +741,11 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
   const int r0 = D >= V ? V * (lane % G) : 0;
   const int grp = D >= V ? lane % G : 0;
   const int64_t ntiles = (bc.N + COLS - 1) / COLS;
+  // ENF_NEGLL_ZYGOTE: the reference's recorded loss (its ScaleShiftTrafo primal ladj is zero under Zygote,
+  // src/abstract_trafo.jl:30-33): block 0's wave 0 adds N sum log|a| back, at the parameters this step read --
+  // started here, so its loads and logs overlap the tiles instead of lengthening the step's tail
+  const double zq_lane =
+      (a.zq && blockIdx.x == 0 && wave == 0) ? (double)bc.N * scaleshift_ladj_lane<T>(a, lane) : 0.0;
   double lossp = 0.0;
   for (int64_t t = (int64_t)blockIdx.x * nw + wave; t < ntiles; t += (int64_t)gridDim.x * nw) {
     const int64_t c0 = t * COLS + (lane / G) * CPF;
@@ -929,9 +934,7 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
 #if ENF_DIAG
   const long long ts2 = STEP && a.diag_ts ? (long long)clock64() : 0;
 #endif
-  // ENF_NEGLL_ZYGOTE: the reference's recorded loss (its ScaleShiftTrafo primal ladj is zero under Zygote,
-  // src/abstract_trafo.jl:30-33): block 0's wave 0 adds N sum log|a| back, at the parameters this step read
-  if (a.zq && blockIdx.x == 0 && wave == 0) lossp += (double)bc.N * scaleshift_ladj_lane<T>(a, lane);
+  lossp += zq_lane;
   lossp = xor_tree(lossp, 64);  // (the 64-lane xor butterfly)
   if (lane == 0) lossw[wave] = lossp;
   __syncthreads();
