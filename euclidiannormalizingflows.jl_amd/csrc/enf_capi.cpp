@@ -841,9 +841,11 @@ enf_status enf_whitening_step_dp(enf_dtype dtype, int64_t D, int64_t N, const vo
   if (vs != ENF_OK) return vs;
   if ((N > 0 && !X) || !theta || !acc || !loss_out) return fail(ENF_ERR_INVALID, "X, theta, acc or loss_out is NULL");
   if ((nruns > 0 && !runs) || (nhb > 0 && !hbatches)) return fail(ENF_ERR_INVALID, "runs or hbatches is NULL");
+  int nranks = 1;
+  if (comm && ncclCommCount(comm->comm, &nranks) != ncclSuccess) return fail(ENF_ERR_RCCL, "ncclCommCount failed");
   return enf::whitening_step_dp(dtype == ENF_F64, D, N, X, ldx, layers, nlayers, theta, acc, runs, nruns, hbatches, nhb,
                                 eta, epsilon, B, loss_out, comm ? rccl_allreduce : nullptr, comm, workspace,
-                                workspace_bytes, (hipStream_t)hip_stream);
+                                workspace_bytes, (hipStream_t)hip_stream, nranks);
   ENF_CATCH
 }
 

@@ -1505,13 +1505,13 @@ enf_status step_args(int64_t D, void* theta, void* acc, const int64_t* runs, int
   return ENF_OK;
 }
 
-// B: the global batch size the update normalises by (N on one rank); ar: the cross-rank sum of this rank's
-// totals (1 + nparams doubles, MODE_SUM) between the gradient and the update (enf_whitening_step_dp), or none
+// B: the global batch size the update normalises by (N on one rank); ar: the cross-rank sum between the gradient
+// and the update (enf_whitening_step_dp), or none; nranks: the ranks of that sum.
 enf_status whitening_step_single(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
                                  int32_t nlayers, void* theta, void* acc, const int64_t* runs, int32_t nruns,
                                  const int64_t* hb, int32_t nhb, double eta, double epsilon, double* loss_out,
                                  void* workspace, size_t workspace_bytes, hipStream_t st, int64_t B, AllreduceFn ar,
-                                 void* ar_ctx) {
+                                 void* ar_ctx, int nranks) {
   Plan P;
   enf_status s = make_plan(f64, D, N > 0 ? N : 1, layers, nlayers, P);
   if (s != ENF_OK) return s;
@@ -1519,6 +1519,39 @@ enf_status whitening_step_single(bool f64, int64_t D, int64_t N, const void* X, 
   s = step_args(D, theta, acc, runs, nruns, hb, nhb, eta, epsilon, loss_out, B, P.ga.nparams, a);
   if (s != ENF_OK) return s;
   const size_t n1 = 1 + (size_t)P.ga.nparams;
+  // Data-parallel step of the fused (J o H)^n fp32 kernel over a share of the minibatch (round 6, VERDICT r05 item
+  // 5): the cross-rank sum carries the gradient kernel's partial rows themselves -- every rank launches the grid of
+  // ceil(B / nranks) columns, and block 0 adds the row {-N ctot, 0...} -- and the update launch sums the summed rows
+  // in its fixed order: no reduction launch between the gradient and the sum. The choice depends on the flow, B and
+  // nranks only, so every rank takes it (the rows of all ranks must line up); one rank with its whole batch
+  // (N == B) keeps the path below, bit-identical to enf_whitening_step.
+  if (ar && !f64 && (nranks > 1 || N < B) && ldx == D && hj_grad_shape_ok(D, layers, nlayers)) {
+    if (N > 0 && (((uintptr_t)X) & 15) != 0)
+      return set_error(ENF_ERR_UNSUPPORTED, "enf_whitening_step_dp: X must be 16-byte aligned on this flow");
+    const int64_t Nplan = nranks > 1 ? (B + nranks - 1) / nranks : (N > 0 ? N : 1);
+    const int R = hj_grad_launch_rows(D, Nplan, nlayers / 2) + 1;  // (+ the ctot row)
+    if (!workspace || workspace_bytes < ((size_t)R + 2) * n1 * sizeof(double))
+      return set_error(ENF_ERR_INVALID, "enf_whitening_step_dp: workspace too small (enf_flow_negll_grad_workspace "
+                                        "of ceil(B / ranks) columns)");
+    double* rows = (double*)workspace;
+    hipError_t e = hipSuccess;
+    if (N > 0) {
+      int nb = 0;
+      e = launch_hj_grad(D, N, X, layers, nlayers, P.ga.nparams, rows, rows + (size_t)R * n1, &nb, st, Nplan, true);
+      if (e != hipSuccess) return set_error(ENF_ERR_HIP, hipGetErrorString(e));
+      if (nb != R) return set_error(ENF_ERR_HIP, "enf_whitening_step_dp: unexpected gradient grid");
+    } else if (hipMemsetAsync(rows, 0, (size_t)R * n1 * sizeof(double), st) != hipSuccess) {
+      return set_error(ENF_ERR_HIP, "hipMemsetAsync");
+    }
+    s = ar(ar_ctx, rows, (int64_t)R * (int64_t)n1, true, st);
+    if (s != ENF_OK) return s;
+    P.ra.partial = rows;
+    P.ra.nblocks = R;
+    P.ra.ctot = nullptr;
+    P.ra.tot = rows + (size_t)R * n1;
+    e = launch_reduce<MODE_STEP>(f64, P.ra, a, st);
+    return e == hipSuccess ? ENF_OK : set_error(ENF_ERR_HIP, hipGetErrorString(e));
+  }
   // one rank, a batch of one block, not the fused (J o H)^n kernel: gradient and update in ONE launch (round 5)
   static const int small_ok = ENF_KNOB("ENF_STEP_SMALL", 1);
   if (small_ok && !ar && N > 0 && P.blocks == 1 && P.small_lds <= kGradLdsMax &&
@@ -1838,16 +1871,17 @@ enf_status whitening_step(bool f64, int64_t D, int64_t N, const void* X, int64_t
                           const int64_t* hb, int32_t nhb, double eta, double epsilon, double* loss_out,
                           void* workspace, size_t workspace_bytes, hipStream_t st) {
   return whitening_step_dp(f64, D, N, X, ldx, layers, nlayers, theta, acc, runs, nruns, hb, nhb, eta, epsilon, N,
-                           loss_out, nullptr, nullptr, workspace, workspace_bytes, st);
+                           loss_out, nullptr, nullptr, workspace, workspace_bytes, st, 1);
 }
 
 enf_status whitening_step_dp(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
                              int32_t nlayers, void* theta, void* acc, const int64_t* runs, int32_t nruns,
                              const int64_t* hb, int32_t nhb, double eta, double epsilon, int64_t B, double* loss_out,
-                             AllreduceFn ar, void* ar_ctx, void* workspace, size_t workspace_bytes, hipStream_t st) {
+                             AllreduceFn ar, void* ar_ctx, void* workspace, size_t workspace_bytes, hipStream_t st,
+                             int nranks) {
   if (fits_one_launch(f64, D, N, layers, nlayers))
     return whitening_step_single(f64, D, N, X, ldx, layers, nlayers, theta, acc, runs, nruns, hb, nhb, eta, epsilon,
-                                 loss_out, workspace, workspace_bytes, st, B, ar, ar_ctx);
+                                 loss_out, workspace, workspace_bytes, st, B, ar, ar_ctx, nranks);
   std::vector<GradChunk> ch;
   ChunkWs w;
   enf_status s = chunked_setup(f64, D, N, layers, nlayers, workspace, workspace_bytes, ch, w, "enf_whitening_step");
@@ -1912,7 +1946,7 @@ enf_status whitening_epoch(bool f64, int64_t D, int64_t N, const void* X, int64_
     const int64_t b0 = j * bs, B = N - b0 < bs ? N - b0 : bs;
     enf_status s = whitening_step_dp(f64, D, B, (const char*)X + (size_t)b0 * (size_t)ldx * esz, ldx, layers, nlayers,
                                      theta, acc, runs, nruns, hb, nhb, eta, epsilon, B, loss_out + j, nullptr, nullptr,
-                                     workspace, workspace_bytes, st);
+                                     workspace, workspace_bytes, st, 1);
     if (s != ENF_OK) return s;
   }
   return ENF_OK;

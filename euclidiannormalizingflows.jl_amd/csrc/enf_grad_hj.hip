@@ -321,7 +321,10 @@ __device__ __forceinline__ void ctot_block(const HJGradArgs& a, double* __restri
     double c = 0.0;
     for (int p = 0; p < n; ++p) c += scr[p];
     *a.ctot_out = c;
+    if (a.ctot_row) a.ctot_row[0] = -(double)a.N * c;
   }
+  if (a.ctot_row)
+    for (int i = 1 + tid; i <= a.nparams; i += NT) a.ctot_row[i] = 0.0;
 }
 
 // Block epilogue: loss (without the constant ladj) and the flow gradient (layer order, the enf_flow_param_count
@@ -753,8 +756,13 @@ int hj_grad_blocks(int64_t D, int64_t N, int32_t npairs) {
   return b;
 }
 
+int hj_grad_launch_rows(int64_t D, int64_t Nplan, int32_t npairs) {
+  return blocks_for(select_kernel(D, npairs, Nplan), Nplan);
+}
+
 hipError_t launch_hj_grad(int64_t D, int64_t N, const void* X, const enf_layer* layers, int32_t nlayers,
-                          int32_t nparams, double* partial, double* ctot_out, int* nblocks, hipStream_t st) {
+                          int32_t nparams, double* partial, double* ctot_out, int* nblocks, hipStream_t st,
+                          int64_t Nplan, bool ctot_row) {
   HJGradArgs a;
   std::memset(&a, 0, sizeof a);
   a.X = (const float*)X;
@@ -779,9 +787,11 @@ hipError_t launch_hj_grad(int64_t D, int64_t N, const void* X, const enf_layer* 
     off += 4 * (int32_t)D;
   }
   if (off != nparams) return hipErrorInvalidValue;
-  const KSel s = select_kernel(D, a.n, N);
-  const int blocks = blocks_for(s, N);
-  *nblocks = blocks;
+  const int64_t Np = Nplan > 0 ? Nplan : N;
+  const KSel s = select_kernel(D, a.n, Np);
+  const int blocks = blocks_for(s, Np);
+  a.ctot_row = ctot_row ? partial + (int64_t)blocks * (1 + nparams) : nullptr;
+  *nblocks = blocks + (ctot_row ? 1 : 0);
   if (s.lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(s.k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds);
     if (e != hipSuccess) return e;

@@ -45,12 +45,14 @@ enf_status whitening_step(bool f64, int64_t D, int64_t N, const void* X, int64_t
 // through the caller's communicator)
 typedef enf_status (*AllreduceFn)(void* ctx, void* buf, int64_t count, bool f64, hipStream_t st);
 // One rank's data-parallel optimize_whitening step (enf_whitening_step_dp): the gradient of its N columns, the
-// cross-rank sum ar of the slice totals (double; none on one rank), then the tail normalised by the global batch
-// B (loss, ADAGrad, re-normalisation) -- whitening_step is the case B = N, ar = none
+// cross-rank sum ar over nranks ranks of the slice totals -- or, on the fused (J o H)^n path, of the partial rows
+// (double; none on one rank), then the tail normalised by the global batch B (loss, ADAGrad, re-normalisation) --
+// whitening_step is the case B = N, ar = none, nranks = 1
 enf_status whitening_step_dp(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
                              int32_t nlayers, void* theta, void* acc, const int64_t* runs, int32_t nruns,
                              const int64_t* hb, int32_t nhb, double eta, double epsilon, int64_t B, double* loss_out,
-                             AllreduceFn ar, void* ar_ctx, void* workspace, size_t workspace_bytes, hipStream_t st);
+                             AllreduceFn ar, void* ar_ctx, void* workspace, size_t workspace_bytes, hipStream_t st,
+                             int nranks);
 // The single-rank steps of one epoch over the minibatches [b0, b0 + bs) of N columns (enf_whitening_epoch)
 enf_status whitening_epoch(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, int64_t bs,
                            const enf_layer* layers, int32_t nlayers, void* theta, void* acc, const int64_t* runs,

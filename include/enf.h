@@ -293,8 +293,12 @@ enf_status enf_allreduce_sum(enf_comm comm, void* buf, int64_t count, enf_dtype 
  * enf_flow_negll_grad + enf_allreduce_sum + enf_whitening_apply (and the zeroing of their buffer) with gradient +
  * totals + all-reduce + one update launch; on one rank (comm NULL or a 1-rank communicator, B = N) identical to
  * enf_whitening_step. A flow beyond one gradient launch's bounds (the chunked path of enf_flow_negll_grad) sums
- * each rank's gradient in the dtype before the all-reduce (its chunks accumulate into a buffer of T). workspace:
- * enf_flow_negll_grad_workspace(N) bytes. Every rank must call it with the same B, runs and batches. */
+ * each rank's gradient in the dtype before the all-reduce (its chunks accumulate into a buffer of T). Round 6: on the
+ * fused fp32 (J o H)^n path with more than one rank (or N < B) the all-reduce carries the gradient kernel's partial
+ * rows (every rank launches the grid of ceil(B / ranks) columns; about 5 KB per row at D = 32, 4 pairs) and the
+ * update launch sums them -- no reduction launch in between. workspace: enf_flow_negll_grad_workspace of
+ * max(N, ceil(B / ranks)) columns (the global batch B always suffices). Every rank must call it with the same B,
+ * runs and batches. */
 enf_status enf_whitening_step_dp(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,
                                  const enf_layer* layers, int32_t nlayers, void* theta, void* acc, const int64_t* runs,
                                  int32_t nruns, const int64_t* hbatches, int32_t nhb, double eta, double epsilon,
