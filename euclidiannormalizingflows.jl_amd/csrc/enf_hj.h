@@ -301,7 +301,7 @@ struct HJParams {
 // (Q: the record slot of the row weights in the parameter set P)
 // CH: partial chains per column -- 1 (product, round 6): one chain of R, no add; 2 (rounds 1-5): even / odd rows,
 // one add to combine. One chain: 0.595 vs 0.603 ms on config 3 (9.08M vs 9.35M cycles, interleaved A/B,
-// profiles/r06_ballot_ab_v1.jsonl): the dependent FMAs hide behind the other column and the other waves.
+// profiles/r06/ballot_ab_v1.jsonl): the dependent FMAs hide behind the other column and the other waves.
 template <int D, int R, int U, int Q = HJ_W, typename P = HJParams<R>, int CH = 1>
 __device__ __forceinline__ void hj_dots(const float (&y)[U][R], const P& prm, float (&dot)[U]) {
   constexpr int G = HJLay<D, R, U>::G;
@@ -388,7 +388,7 @@ __device__ __forceinline__ void hj_front(float (&x)[U][R], const HJParams<R>& pr
 // One pair (reflection + Johnson) on the register tile, fast form. x holds L_{p-1} (pair 0: the input x)
 // on entry and L_p on exit; prm holds this pair's record on entry and the next one's on exit (r is
 // advanced to it; read after the asinh's temporaries are dead: 128 VGPRs and 65 spilled when the reads were
-// issued before the asinh, and reading W early and the rest late measured no better, profiles/r06_var_ab_v1.jsonl).
+// issued before the asinh, and reading W early and the rest late measured no better, profiles/r06/var_ab_v1.jsonl).
 // prod[u] accumulates the product of the
 // q = 1 + z^2 of the lane's R rows of column u (+Inf / NaN: the fast form is not valid for the tile).
 // asinh: the mask-first merge asinh2_mask / asinh2_pick of the Taylor form and the log form (enf_frag.h).
@@ -522,7 +522,7 @@ struct HJBody {
     }
     // the output y_n = gamma_n + delta'_n L_n (record n). (Writing this epilogue out in both branches, so that the
     // wait-count pass does not see the redo branch's reload of X outstanding at the join, measured the same:
-    // 0.597 vs 0.594 ms, interleaved, profiles/r06_epi_ab_v1.jsonl.)
+    // 0.597 vs 0.594 ms, interleaved, profiles/r06/epi_ab_v1.jsonl.)
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
