@@ -11,7 +11,7 @@ namespace enf {
 // (src/johnson_trafo.jl:82 inverse(JohnsonTrafo) = JohnsonTrafoInv, src/householder_trafo.jl:153-154 a single
 // reflection is its own inverse), i.e. the layers J^-1, H, J^-1, H, ... applied in this order, fp32, the
 // layouts of the forward program (D = 32 / 64 / 128, padded or not), fused in one launch. Per pair p:
-//   w   = (y - gamma)/delta                  as fma(y, 1/delta, -gamma/delta)       (johnson_trafo.jl:36)
+//   w   = (y - gamma)/delta                                                            (johnson_trafo.jl:36)
 //   sh  = sinh(w): |w| < 1/2: w (1 + w^2/6 + w^4/120 + w^6/5040) (truncation < 1e-8 relative),
 //         else H - 1/(4H), H = E/2 = exp2(w log2 e - 1) -- both odd in w, merged branch-free by a mask from w^2
 //   x   = lambda sh + xi                      the JohnsonTrafoInv output              (johnson_trafo.jl:36)
@@ -20,70 +20,74 @@ namespace enf {
 //         once per column (ctot), +1/2 log2 of the product of the q = 1 + sh^2 of a lane's 8 rows over all
 //         pairs (one log2 per lane and column per tile, round 6)
 //   dot = vh'x, x -= dot vh                   householder_trafo! (householder_trafo.jl:8-11)
-// Records per pair and row {1/delta, -gamma/delta, lambda, xi, vh} (built in double); the multipliers of tile
-// registers one slot rotated (hj_rot). A tile whose q product overflows (|sh| ~ 2^16 on every row, Inf, NaN)
-// is redone from X elementwise (exact-range sinh, log2 per element: ladj +Inf where the reference's fp32
-// 1 + z^2 overflows).
-constexpr int kHjiW = 5;
-enum : int { HI_ID = 0, HI_NG = 1, HI_LM = 2, HI_XI = 3, HI_VH = 4 };
-__host__ __device__ constexpr bool hi_rotated(int q) { return q == HI_ID || q == HI_LM || q == HI_VH; }
-static size_t hji_lds_bytes(int D, int n) { return kHjHeader + (size_t)n * kHjiW * D * sizeof(float); }
-
-template <int R>
-struct HJIParams {
-  float v[kHjiW][R];
-  __device__ __forceinline__ void load(const float* r) {
-#pragma unroll
-    for (int k = 0; k < kHjiW; ++k)
-#pragma unroll
-      for (int h = 0; h < R / 4; ++h) lds_vec<float, 4>(r + k * R + 4 * h, *reinterpret_cast<float(*)[4]>(&v[k][4 * h]));
-  }
-  __device__ __forceinline__ float m(int k, int e) const { return v[k][hi_rotated(k) ? hj_rot(e) : e]; }
-};
+// Round 6: the hop x -> H -> the next pair's w is folded into per-row constants as in the forward program
+// (enf_hj.h): the tile carries sh between pairs, and every hop is dot = W'sh, v = fma(-dot, C, fma(sh, B, A)),
+// the same three operations as the forward's front (hj_front), with (entry records E_p, p = 1 .. n)
+//   p < n: W = vh_{p-1} lambda_{p-1}, B = lambda_{p-1}/delta_p, A = ((H_{p-1} xi_{p-1}) - gamma_p)/delta_p,
+//          C = vh_{p-1}/delta_p                                    (v = w_p, the next pair's argument)
+//   p = n: W = vh_{n-1} lambda_{n-1}, B = lambda_{n-1}, A = H_{n-1} xi_{n-1}, C = vh_{n-1}   (v = the output)
+// and E_0 = {0, 1/delta_0, -gamma_0/delta_0, 0} applied to the input without a dot: 3 instead of 4 dependent
+// operations per element and hop. Records built in double; the multipliers of tile registers one slot rotated
+// (hj_rot). A tile whose q product overflows (|sh| ~ 2^16 on every row, Inf, NaN) is redone from X elementwise
+// (exact-range sinh, log2 per element: ladj +Inf where the reference's fp32 1 + z^2 overflows).
 
 template <int D, int R>
 __device__ void build_hji_program(const HJArgs& a, int n, float* __restrict__ rec, double* __restrict__ scr,
                                   float* ctot) {
   constexpr int NF = R / 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int p = wave; p < n; p += nw) {  // v'v and sum_d log|delta/lambda| (johnson_trafo.jl:41) in double
+  // v'v, sum_d log|delta/lambda| (johnson_trafo.jl:41) and v'xi (the reflection of the shift xi, folded into A)
+  for (int p = wave; p < n; p += nw) {
     const float* v = a.v[p];
-    double vv = 0.0, cl = 0.0;
+    double vv = 0.0, cl = 0.0, vx = 0.0;
     for (int d = lane; d < a.dreal; d += 64) {
       const double vd = v[d];
       vv += vd * vd;
       cl += log(fabs((double)a.d[p][d])) - log(fabs((double)a.lam[p][d]));
+      vx += vd * (double)a.xi[p][d];
     }
     for (int m = 32; m >= 1; m >>= 1) {
       vv += __shfl_xor(vv, m);
       cl += __shfl_xor(cl, m);
+      vx += __shfl_xor(vx, m);
     }
     if (lane == 0) {
-      scr[2 * p] = sqrt(2.0 / vv);
-      scr[2 * p + 1] = cl;
+      const double hs = sqrt(2.0 / vv);
+      scr[3 * p] = hs;
+      scr[3 * p + 1] = cl;
+      scr[3 * p + 2] = hs * vx;  // vh'xi
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < n * D; i += blockDim.x) {
+  for (int i = threadIdx.x; i < (n + 1) * D; i += blockDim.x) {
     const int p = i / D, d = i % D;
     const int h = d / (D / NF), w = d % (D / NF), g = w / 4, e = w % 4;
-    float* r = rec + (size_t)p * kHjiW * D + g * kHjiW * R + 4 * h;
-    // a padded row (d >= dreal): w = 0, sh = 0, x = 0, vh = 0 -- its zeros stay zero with q = 1 (ladj 0)
-    double q[kHjiW] = {1.0, 0.0, 1.0, 0.0, 0.0};
+    float* r = rec + (size_t)p * kHjW * D + g * kHjW * R + 4 * h;
+    // a padded row (d >= dreal): W = C = 0, B = 1, A = 0 -- its zeros stay zero with q = 1 (ladj 0)
+    double q[kHjW] = {0.0, 1.0, 0.0, 0.0};
     if (d < a.dreal) {
-      const double id = 1.0 / (double)a.d[p][d];
-      q[HI_ID] = id;
-      q[HI_NG] = -(double)a.g[p][d] * id;
-      q[HI_LM] = (double)a.lam[p][d];
-      q[HI_XI] = (double)a.xi[p][d];
-      q[HI_VH] = (double)a.v[p][d] * scr[2 * p];
+      if (p == 0) {
+        const double id = 1.0 / (double)a.d[0][d];
+        q[HJ_B] = id;
+        q[HJ_A] = -(double)a.g[0][d] * id;
+      } else {
+        const double vh = (double)a.v[p - 1][d] * scr[3 * (p - 1)];
+        const double lm = (double)a.lam[p - 1][d];
+        const double hx = (double)a.xi[p - 1][d] - vh * scr[3 * (p - 1) + 2];  // (H_{p-1} xi_{p-1})_d
+        const double id = p < n ? 1.0 / (double)a.d[p][d] : 1.0;
+        const double gm = p < n ? (double)a.g[p][d] : 0.0;
+        q[HJ_W] = vh * lm;
+        q[HJ_B] = lm * id;
+        q[HJ_A] = (hx - gm) * id;
+        q[HJ_C] = vh * id;
+      }
     }
 #pragma unroll
-    for (int k = 0; k < kHjiW; ++k) r[k * R + (hi_rotated(k) ? hj_rot(e) : e)] = (float)q[k];
+    for (int k = 0; k < kHjW; ++k) r[k * R + (hj_rotated(k) ? hj_rot(e) : e)] = (float)q[k];
   }
   if (threadIdx.x == 0) {
     double c = 0.0;
-    for (int p = 0; p < n; ++p) c -= scr[2 * p + 1];  // -johnsontrafo_ladj: -log|delta/lambda|
+    for (int p = 0; p < n; ++p) c -= scr[3 * p + 1];  // -johnsontrafo_ladj: -log|delta/lambda|
     *ctot = (float)c;
   }
   __syncthreads();
@@ -98,18 +102,27 @@ __device__ __forceinline__ uint32_t sinh_small_mask(float w2) {
   return (uint32_t)((int32_t)(__builtin_bit_cast(uint32_t, w2) - 0x3E800000u) >> 31);
 }
 
-// One pair (J^-1, H) on the register tile, fast form: returns the largest q product of a lane's rows.
+// The input's entry E_0: w_0 = fma(y, 1/delta_0, -gamma_0/delta_0) (no reflection before the first J^-1)
+template <int R, int U>
+__device__ __forceinline__ void hji_entry0(float (&x)[U][R], const HJParams<R>& prm) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int e = 0; e < R; ++e) x[u][e] = fmaf(x[u][e], prm.m(HJ_B, e), prm.m(HJ_A, e));
+}
+
+// One pair (J^-1, then the folded hop H -> next) on the register tile, fast form: x holds w_p on entry and w_{p+1}
+// (after the last pair: the output) on exit; prm holds entry record E_p's successor on exit (r advanced). prod[u]
+// accumulates the product of the q of the lane's rows of column u.
 template <int D, int R, int U>
-__device__ __forceinline__ void hji_pair_fast(float (&x)[U][R], float (&prod)[U], const float*& r) {
-  HJIParams<R> prm;
-  prm.load(r);
-  r += kHjiW * D;
+__device__ __forceinline__ void hji_pair_fast(float (&x)[U][R], float (&prod)[U], const float*& r, HJParams<R>& prm) {
+  r += kHjW * D;
   float w[U][R], E[U][R], rE[U][R];
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) {
-      w[u][e] = fmaf(x[u][e], prm.m(HI_ID, e), prm.m(HI_NG, e));
+      w[u][e] = x[u][e];
       E[u][e] = fmaf(w[u][e], (float)kLog2e, -1.0f);  // exp2 of this is E/2
     }
   // wave priority 3 around the transcendental groups, as in hj_pair_fast
@@ -153,45 +166,34 @@ __device__ __forceinline__ void hji_pair_fast(float (&x)[U][R], float (&prod)[U]
 #pragma unroll
     for (int e = 0; e < R; ++e) {
       // (E - 1/E)/2 = E/2 - 1/(4 E/2): one fma on the halved exponential and its reciprocal
-      const float sh = asinh2_pick(w[u][e], fmaf(-0.25f, rE[u][e], E[u][e]), msk[u][e]);
-      q[u][e] = fmaf(sh, sh, 1.0f);
-      x[u][e] = fmaf(prm.m(HI_LM, e), sh, prm.m(HI_XI, e));
+      x[u][e] = asinh2_pick(w[u][e], fmaf(-0.25f, rE[u][e], E[u][e]), msk[u][e]);
+      q[u][e] = fmaf(x[u][e], x[u][e], 1.0f);
     }
     prod[u] *= prod_tree<R>(q[u]);
   }
-  float dot[U];
-  hj_dots<D, R, U, HI_VH>(x, prm, dot);
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int e = 0; e < R; ++e) x[u][e] = fmaf(-dot[u], prm.m(HI_VH, e), x[u][e]);
+  prm.load(r);  // E_{p+1} (read once the sinh's temporaries are dead: 10 VGPRs spilled when read before it)
+  hj_front<D, R, U>(x, prm);
 }
 
 // The same pair elementwise over the whole fp32 range: sinh finite up to |w| ~ 89.4 (E/2 formed as
 // exp2(|w| log2 e - 1)), the ladj's log2 per element (+Inf where 1 + sh^2 overflows, as the reference's).
-template <int D, int R, int U, bool LADJ>
-__device__ __forceinline__ void hji_pair_exact(float (&x)[U][R], float (&acc)[U], const float*& r) {
-  HJIParams<R> prm;
+template <int D, int R, int U>
+__device__ __forceinline__ void hji_pair_exact(float (&x)[U][R], float (&acc)[U], const float*& r, HJParams<R>& prm) {
+  r += kHjW * D;
   prm.load(r);
-  r += kHjiW * D;
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int e = 0; e < R; ++e) {
-      const float w = fmaf(x[u][e], prm.m(HI_ID, e), prm.m(HI_NG, e));
+      const float w = x[u][e];
       const float aw = fabsf(w);
       const float h = hw_exp2(fmaf(aw, (float)kLog2e, -1.0f));
       const float big = copysignf(fmaf(-0.25f, hw_rcp(h), h), w);
       const float sh = aw < 0.5f ? sinh_small(w, w * w) : big;
-      x[u][e] = fmaf(prm.m(HI_LM, e), sh, prm.m(HI_XI, e));
-      if (LADJ) acc[u] += 0.5f * hw_log2(fmaf(sh, sh, 1.0f));
+      x[u][e] = sh;
+      acc[u] = fmaf(0.5f, hw_log2(fmaf(sh, sh, 1.0f)), acc[u]);
     }
-  float dot[U];
-  hj_dots<D, R, U, HI_VH>(x, prm, dot);
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int e = 0; e < R; ++e) x[u][e] = fmaf(-dot[u], prm.m(HI_VH, e), x[u][e]);
+  hj_front<D, R, U>(x, prm);
 }
 
 template <int D, int R, int U, int LM, bool PAD>
@@ -204,18 +206,22 @@ struct HJIBody {
 
   template <bool TAIL, int DBG>
   __device__ __forceinline__ void tile(int64_t col0, float (&x)[U][R], const float (&old)[HJLay<D, R, U>::NLS]) {
-    constexpr bool LADJ = LM > 0;
     float acc[U], prod[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) prod[u] = 1.f;
     const float* r = rec;
-    for (int p = 0; p < n; ++p) hji_pair_fast<D, R, U>(x, prod, r);
+    HJParams<R> prm;
+    prm.load(r);
+    hji_entry0<R, U>(x, prm);
+    for (int p = 0; p < n; ++p) hji_pair_fast<D, R, U>(x, prod, r, prm);
     if (__builtin_expect(hj_redo<HJLay<D, R, U>::G>(prod), 0)) {
       hj_load<D, R, U, TAIL, DBG, PAD>(a, col0, x);
 #pragma unroll
       for (int u = 0; u < U; ++u) acc[u] = 0.f;
       r = rec;
-      for (int p = 0; p < n; ++p) hji_pair_exact<D, R, U, LADJ>(x, acc, r);
+      prm.load(r);
+      hji_entry0<R, U>(x, prm);
+      for (int p = 0; p < n; ++p) hji_pair_exact<D, R, U>(x, acc, r, prm);
     } else {
 #pragma unroll
       for (int u = 0; u < U; ++u) acc[u] = 0.5f * hw_log2(prod[u]);
@@ -229,12 +235,12 @@ __global__ __launch_bounds__(256, 4) void flow_hji_kernel(HJArgs a) {
   const int n = a.n;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* scr = reinterpret_cast<double*>(smem);
-  float* ctotp = reinterpret_cast<float*>(scr + 2 * kHjMaxPairs);
+  float* ctotp = reinterpret_cast<float*>(scr + 3 * kHjMaxPairs);
   float* stage = reinterpret_cast<float*>(smem + kHjScratch) + (threadIdx.x >> 6) * kStagePerWave;
   float* rec = reinterpret_cast<float*>(smem + kHjHeader);
   build_hji_program<D, R>(a, n, rec, scr, ctotp);
   constexpr int G = HJLay<D, R, U>::G;
-  HJIBody<D, R, U, LM, PAD> body{a, rec + ((threadIdx.x & 63) % G) * kHjiW * R, *ctotp, stage, n};
+  HJIBody<D, R, U, LM, PAD> body{a, rec + ((threadIdx.x & 63) % G) * kHjW * R, *ctotp, stage, n};
   hj_stream<D, R, U, LM, 0, PAD>(a, body);
 }
 
@@ -294,7 +300,7 @@ int hji_program_pairs(const FlowArgs& a) {
 template <int D, int LM, bool PAD>
 static hipError_t launch_hji(const HJArgs& h, hipStream_t st, const DeviceInfo& dev) {
   constexpr int R = 8, U = 2;
-  const size_t lds = hji_lds_bytes(D, h.n);
+  const size_t lds = hj_lds_bytes(D, h.n);
   const void* k = reinterpret_cast<const void*>(&flow_hji_kernel<D, R, U, LM, PAD>);
   int64_t blocks = 0;
   hipError_t e = frag_grid(k, h.N, (int64_t)HJLay<D, R, U>::TC * 4, lds, dev, &blocks);

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--settle-ms", type=float, default=300.0,
                     help="run the flow untimed for this long first (the clock ramps over the first ~25 launches)")
     ap.add_argument("--product", action="store_true", help="time the shipping libenf.so instead")
+    ap.add_argument("--inverse", action="store_true",
+                    help="time inverse(flow) on the forward flow's outputs (bench.py --inverse's workload)")
     ap.add_argument("--lib", default=None, help="time this build of the ABI instead (e.g. tools/ab/libenf_r5.so)")
     ap.add_argument("--flush-mb", type=int, default=0,
                     help="write a buffer of this many MB before every call (evicts the L2s and the MALL: cold-cache "
@@ -48,18 +50,30 @@ def main():
     npd = np.float32 if args.dtype == "f32" else np.float64
     td = torch.float32 if args.dtype == "f32" else torch.float64
     D, N = args.D, args.N
-    layers = bench.build_flow(D, args.pairs, npd, pattern=args.pattern)
+    fwd = bench.build_flow(D, args.pairs, npd, pattern=args.pattern)
+    layers = bench.invert_layers(fwd) if args.inverse else fwd
     g = torch.Generator(device=dev).manual_seed(0x5EED)
     X = torch.randn((N, D), generator=g, device=dev, dtype=td)
     Y = torch.empty_like(X)
     ladj = torch.empty(N, device=dev, dtype=td)
-    dparams = [[torch.from_numpy(np.ascontiguousarray(np.asarray(p).T)).to(dev) for p in ps] for _, ps in layers]
-    arr = (lib.Layer * len(layers))()
-    for i, ((op, ps), dp) in enumerate(zip(layers, dparams)):
-        arr[i].op = op
-        arr[i].k = (np.asarray(ps[0]).shape[1] if np.asarray(ps[0]).ndim == 2 else 1) if op == 5 else 0
-        for q, t in enumerate(dp):
-            arr[i].p[q] = t.data_ptr()
+
+    def layer_array(lays):
+        dps = [[torch.from_numpy(np.ascontiguousarray(np.asarray(p).T)).to(dev) for p in ps] for _, ps in lays]
+        a = (lib.Layer * len(lays))()
+        for i, ((op, ps), dp) in enumerate(zip(lays, dps)):
+            a[i].op = op
+            a[i].k = (np.asarray(ps[0]).shape[1] if np.asarray(ps[0]).ndim == 2 else 1) if op == 5 else 0
+            for q, t in enumerate(dp):
+                a[i].p[q] = t.data_ptr()
+        return a, dps
+
+    arr, dparams = layer_array(layers)
+    dt0 = lib.ENF_F32 if args.dtype == "f32" else lib.ENF_F64
+    if args.inverse:  # the inverse reads the forward's outputs (as bench.py --inverse)
+        farr, fdp = layer_array(fwd)
+        lib.check(L.enf_flow_apply(dt0, D, N, X.data_ptr(), D, Y.data_ptr(), D, ladj.data_ptr(), 0, farr, len(fwd), None))
+        torch.cuda.synchronize()
+        X, Y = Y, X
     st = torch.cuda.current_stream(dev)
     dt = lib.ENF_F32 if args.dtype == "f32" else lib.ENF_F64
 
