@@ -53,6 +53,7 @@ def test_negll_grad_finite_differences(enf, gpu, oracle, D):
     X = np.asfortranarray(0.8 * rng.standard_normal((D, 257)))
     negll, grads = enf.mvnormal_negll_trafograd(make_flow(enf, layers), colmajor_cuda(X), similar_fill_quirk=False)
     ref = oracle_negll(oracle, layers, X)
+    assert np.isfinite(ref), ref  # (a finite-difference test: the loss must be finite)
     assert loss_close(negll, ref, 1e-12), (negll, ref)
     g = np.concatenate([np.asarray(a).reshape(-1, order="F") for per in grads for a in per])
     th0 = flat(layers, D)
