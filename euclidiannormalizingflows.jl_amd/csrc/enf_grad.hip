@@ -687,6 +687,11 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
   // over its lanes, then vh = v sqrt(2/v'v) (householder_trafo.jl:9-10) written by the same wave; FAST, the other
   // steps' row constants (rec_extra) -- the reflections' chains and the exp / log chains run side by side, one
   // barrier for both
+  // ENF_NEGLL_ZYGOTE: the reference's recorded loss (its ScaleShiftTrafo primal ladj is zero under Zygote,
+  // src/abstract_trafo.jl:30-33): block 0 adds N sum log|a| back, at the parameters this step read. FAST, the wave
+  // that writes a ScaleShift step's row constants sums the log|a| it just stored (the value the forward adds) and
+  // adds it to its own loss partial; otherwise wave 0 sums them from the parameters in global memory
+  double zq_lane = 0.0;
   auto step_consts = [&](const int s, const int op) {
     const int rn = rec_nparams(op, FAST);
     if (op == OP_HOUSEHOLDER) {
@@ -710,6 +715,11 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
       if (rec_extra(op) > 0)
         for (int i = lane; i < nent; i += 64)
           rec_extra_store<V>(op, (double*)(rec + a.roff[s] + (D >= V ? i / V : 0) * rn * V + i % V), ltab);
+      if (op == OP_SCALESHIFT && a.zq && blockIdx.x == 0) {
+        const int n = a.layers[a.layer[s]].k == 1 ? 1 : a.D;  // (a length-1 a counts once)
+        for (int d = lane; d < n; d += 64)  // (the entries this lane just stored)
+          zq_lane += (double)rec[a.roff[s] + (D >= V ? d / V : 0) * rn * V + d % V + 2 * V];
+      }
     }
   };
   {
@@ -741,11 +751,9 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
   const int r0 = D >= V ? V * (lane % G) : 0;
   const int grp = D >= V ? lane % G : 0;
   const int64_t ntiles = (bc.N + COLS - 1) / COLS;
-  // ENF_NEGLL_ZYGOTE: the reference's recorded loss (its ScaleShiftTrafo primal ladj is zero under Zygote,
-  // src/abstract_trafo.jl:30-33): block 0's wave 0 adds N sum log|a| back, at the parameters this step read --
-  // started here, so its loads and logs overlap the tiles instead of lengthening the step's tail
-  const double zq_lane =
-      (a.zq && blockIdx.x == 0 && wave == 0) ? (double)bc.N * scaleshift_ladj_lane<T>(a, lane) : 0.0;
+  // (the ENF_NEGLL_ZYGOTE sum without the FAST records: started here, so its loads and logs overlap the tiles)
+  if constexpr (!FAST)
+    if (a.zq && blockIdx.x == 0 && wave == 0) zq_lane = scaleshift_ladj_lane<T>(a, lane);
   double lossp = 0.0;
   for (int64_t t = (int64_t)blockIdx.x * nw + wave; t < ntiles; t += (int64_t)gridDim.x * nw) {
     const int64_t c0 = t * COLS + (lane / G) * CPF;
@@ -934,7 +942,7 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
 #if ENF_DIAG
   const long long ts2 = STEP && a.diag_ts ? (long long)clock64() : 0;
 #endif
-  lossp += zq_lane;
+  lossp = fma(zq_lane, (double)bc.N, lossp);
   lossp = xor_tree(lossp, 64);  // (the 64-lane xor butterfly)
   if (lane == 0) lossw[wave] = lossp;
   __syncthreads();
@@ -1505,6 +1513,9 @@ enf_status step_args(int64_t D, void* theta, void* acc, const int64_t* runs, int
   return ENF_OK;
 }
 
+// the largest gradient-row payload the data-parallel step hands to the collective instead of reducing it first
+constexpr size_t kRowsCollectiveMax = 64 << 10;
+
 // B: the global batch size the update normalises by (N on one rank); ar: the cross-rank sum between the gradient
 // and the update (enf_whitening_step_dp), or none; nranks: the ranks of that sum.
 enf_status whitening_step_single(bool f64, int64_t D, int64_t N, const void* X, int64_t ldx, const enf_layer* layers,
@@ -1522,14 +1533,18 @@ enf_status whitening_step_single(bool f64, int64_t D, int64_t N, const void* X, 
   // Data-parallel step of the fused (J o H)^n fp32 kernel over a share of the minibatch (round 6, VERDICT r05 item
   // 5): the cross-rank sum carries the gradient kernel's partial rows themselves -- every rank launches the grid of
   // ceil(B / nranks) columns, and block 0 adds the row {-N ctot, 0...} -- and the update launch sums the summed rows
-  // in its fixed order: no reduction launch between the gradient and the sum. The choice depends on the flow, B and
-  // nranks only, so every rank takes it (the rows of all ranks must line up); one rank with its whole batch
-  // (N == B) keeps the path below, bit-identical to enf_whitening_step.
-  if (ar && !f64 && (nranks > 1 || N < B) && ldx == D && hj_grad_shape_ok(D, layers, nlayers)) {
+  // in its fixed order: no reduction launch between the gradient and the sum. The rows trade that launch (~4.4 us)
+  // for R times the collective's bytes, so they are taken only while they stay small (kRowsCollectiveMax): config
+  // 5's share has R = 197 rows of 641 doubles (1 MB), which an 8-rank ring all-reduce over xGMI moves far slower than
+  // one row (the one-rank emulation's 18.2 us does not see that cost; no 8-GPU box to measure it). The choice
+  // depends on the flow, B and nranks only, so every rank takes it (the rows of all ranks must line up); one rank
+  // with its whole batch (N == B) keeps the path below, bit-identical to enf_whitening_step.
+  const bool rows_ok = ar && !f64 && (nranks > 1 || N < B) && ldx == D && hj_grad_shape_ok(D, layers, nlayers);
+  const int64_t Nplan = nranks > 1 ? (B + nranks - 1) / nranks : (N > 0 ? N : 1);
+  const int R = rows_ok ? hj_grad_launch_rows(D, Nplan, nlayers / 2) + 1 : 0;  // (+ the ctot row)
+  if (rows_ok && (size_t)R * n1 * sizeof(double) <= kRowsCollectiveMax) {
     if (N > 0 && (((uintptr_t)X) & 15) != 0)
       return set_error(ENF_ERR_UNSUPPORTED, "enf_whitening_step_dp: X must be 16-byte aligned on this flow");
-    const int64_t Nplan = nranks > 1 ? (B + nranks - 1) / nranks : (N > 0 ? N : 1);
-    const int R = hj_grad_launch_rows(D, Nplan, nlayers / 2) + 1;  // (+ the ctot row)
     if (!workspace || workspace_bytes < ((size_t)R + 2) * n1 * sizeof(double))
       return set_error(ENF_ERR_INVALID, "enf_whitening_step_dp: workspace too small (enf_flow_negll_grad_workspace "
                                         "of ceil(B / ranks) columns)");

@@ -479,7 +479,7 @@ __device__ __forceinline__ void step_center_stretch(Tile<T, D, U>& x, Acc<T, D, 
         for (int u = 0; u < U; ++u) {
           if constexpr (std::is_same_v<T, float>) {
             // center_stretch.jl:4-8 with e = exp(|b x|); ladj = -contract_ladj(y) (:41-42)
-            const float bl = rr[0][e], c = rr[1][e], lnb = rr[2][e], E1 = rr[3][e], E2 = rr[4][e], bal = rr[5][e];
+            const float bl = rr[0][e], c = rr[1][e], lnb = rr[2][e], E1 = rr[3][e], E2 = rr[4][e];
             const float xv = x[u][e];
             const float ex = hw_exp2(fabsf(xv * bl));
             const float ome = 1.0f - ex;

@@ -296,7 +296,9 @@ enf_status enf_allreduce_sum(enf_comm comm, void* buf, int64_t count, enf_dtype 
  * each rank's gradient in the dtype before the all-reduce (its chunks accumulate into a buffer of T). Round 6: on the
  * fused fp32 (J o H)^n path with more than one rank (or N < B) the all-reduce carries the gradient kernel's partial
  * rows (every rank launches the grid of ceil(B / ranks) columns; about 5 KB per row at D = 32, 4 pairs) and the
- * update launch sums them -- no reduction launch in between. workspace: enf_flow_negll_grad_workspace of
+ * update launch sums them -- no reduction launch in between -- while those rows total at most 64 KiB (larger
+ * payloads are reduced to one row first: a ring all-reduce of R rows costs more than the launch it saves).
+ * Results are the same bit for bit either way. workspace: enf_flow_negll_grad_workspace of
  * max(N, ceil(B / ranks)) columns (the global batch B always suffices). Every rank must call it with the same B,
  * runs and batches. */
 enf_status enf_whitening_step_dp(enf_dtype dtype, int64_t D, int64_t N, const void* X, int64_t ldx,

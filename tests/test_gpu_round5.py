@@ -58,12 +58,13 @@ def _hj_layers(rng, D, n, dtype=np.float32):
     return layers
 
 
-@pytest.mark.parametrize("case", ["hj", "hj_d64", "chunked"])
+@pytest.mark.parametrize("case", ["hj", "hj_d64", "chunked", "hj1_rows"])
 def test_whitening_step_dp_share_equals_grad_plus_apply(enf, gpu, case):
     """enf_whitening_step_dp on a one-rank communicator with N = a share of the minibatch and B = the whole
     minibatch (B > N > 0) == enf_flow_negll_grad over the share + enf_whitening_apply(B): parameters, ADAGrad
     state and loss bit for bit, over 4 consecutive steps with different shares (the fused (J o H)^4 kernel at
-    D = 32 and 64, and a chunked 20-layer flow)."""
+    D = 32 and 64 -- rows over 64 KiB, reduced before the sum --, a chunked 20-layer flow, and J o H at D = 32 on
+    2000 columns, whose gradient rows (at most 33 of 161 doubles) the sum carries themselves)."""
     import torch
 
     from euclidiannormalizingflows_jl_amd import _lib
@@ -73,11 +74,11 @@ def test_whitening_step_dp_share_equals_grad_plus_apply(enf, gpu, case):
     rng = np.random.default_rng(5200)
     if case.startswith("hj"):
         D = 64 if case == "hj_d64" else 32
-        layers = _hj_layers(rng, D, 4)
+        layers = _hj_layers(rng, D, 1 if case == "hj1_rows" else 4)
     else:
         D = 8
         layers = [(op, ps) for op, ps in _long_flow(rng, D, np.float32) if op != 0]
-    B = 20_000
+    B = 2_000 if case == "hj1_rows" else 20_000
     X = colmajor_cuda((rng.standard_normal((D, B)) * 0.7).astype(np.float32))
     f = make_flow(enf, layers)
     opt = enf.ADAGrad()
@@ -93,7 +94,9 @@ def test_whitening_step_dp_share_equals_grad_plus_apply(enf, gpu, case):
     st = torch.cuda.current_stream().cuda_stream
     comm = enf.EnfComm.single()
     try:
-        for it, (lo, hi) in enumerate([(0, 7_001), (7_001, 20_000), (5_000, 5_003), (123, 19_999)]):
+        shares = ([(0, 7_001), (7_001, 20_000), (5_000, 5_003), (123, 19_999)] if B == 20_000 else
+                  [(0, 701), (701, 2_000), (500, 503), (12, 1_999)])
+        for it, (lo, hi) in enumerate(shares):
             N = hi - lo
             Xs = X[:, lo:hi]
             _lib.check(L.enf_whitening_step_dp(_lib.ENF_F32, D, N, Xs.data_ptr(), D, sa.layers(), len(sa.trafos),
