@@ -727,6 +727,8 @@ int blocks_for(const KSel& s, int64_t N) {
   int64_t blocks = (tiles + s.w - 1) / s.w;
   const int64_t cap = (int64_t)cached_cu * per_cu;
   if (blocks > cap) blocks = cap;
+  static const int max_knob = ENF_KNOB("ENF_HJG_MAXBLOCKS", 0);  // diagnostics: a grid cap (0: none)
+  if (max_knob > 0 && blocks > max_knob) blocks = max_knob;
   return (int)(blocks < 1 ? 1 : blocks);
 }
 
