@@ -377,6 +377,9 @@ def main():
                          "for nodes whose power management settles more slowly; 0 disables")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-train", action="store_true", help="skip the config-5 training leg (`train` object)")
+    ap.add_argument("--train-timeout", type=float, default=240.0,
+                    help="several ranks: seconds the training leg may take before the headline line is printed "
+                         "without it and the ranks exit")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of each CPU baseline leg")
     ap.add_argument("--pattern", default=None,
                     help="layer letters in application order (S C K J I H, H<k> = k chained reflections), e.g. "
@@ -638,16 +641,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not args.selftest_cpu and not args.inverse:
         cpu = cpu_baseline(layers, D, np_dtype, args.cpu_seconds)
-    train = None
     headline = (D, N, args.pairs, args.dtype, args.pattern, args.inverse, strong) == (32, 10_000_000, 4, "f32", None,
                                                                                      False, False)
-    if args.selftest_cpu and not args.no_train:  # the config-5 leg's rank plumbing on gloo
-        import bench_train
-
-        train = bench_train.train_leg_selftest(world, rank, steps=min(args.steps, 20))
-    elif headline and not args.no_train:
-        train = train_leg(dev, world, rank)
-
+    out = None
     if rank == 0:
         out = {
             "metric": "samples/sec fwd+logdetjac through composed flow, D=32 N=1e7, at 1/2/4/8 GPUs",
@@ -693,8 +689,35 @@ def main():
                          "rocprof_kernel_stats": rocprof},
             "valu": valu,
             "cpu_baseline": cpu,
-            "train": train,
+            "train": None,
         }
+    # the config-5 leg after the headline is measured; on several ranks under a watchdog, so that a collective that
+    # never completes (libenf's own RCCL communicator) still leaves the headline line, with the train object's error
+    if args.selftest_cpu and not args.no_train:  # the config-5 leg's rank plumbing on gloo
+        import bench_train
+
+        train = bench_train.train_leg_selftest(world, rank, steps=min(args.steps, 20))
+    elif headline and not args.no_train:
+        watchdog = None
+        if world > 1:
+            import threading
+
+            def expire():
+                if rank == 0:
+                    out["train"] = {"error": f"watchdog: the training leg did not finish in {args.train_timeout:g} s"}
+                    print(json.dumps(out), file=json_out, flush=True)
+                os._exit(0)  # (no exec: the process ends; the GPU work it left is torn down with it)
+
+            watchdog = threading.Timer(args.train_timeout, expire)
+            watchdog.daemon = True
+            watchdog.start()
+        train = train_leg(dev, world, rank)
+        if watchdog is not None:
+            watchdog.cancel()
+    else:
+        train = None
+    if rank == 0:
+        out["train"] = train
         print(json.dumps(out), file=json_out, flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
