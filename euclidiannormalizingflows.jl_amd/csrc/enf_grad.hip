@@ -755,6 +755,9 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
   if constexpr (!FAST)
     if (a.zq && blockIdx.x == 0 && wave == 0) zq_lane = scaleshift_ladj_lane<T>(a, lane);
   double lossp = 0.0;
+#if ENF_DIAG
+  long long tsF = 0, tsL = 0;  // the first tile's forward end and loss end (diagnostics)
+#endif
   for (int64_t t = (int64_t)blockIdx.x * nw + wave; t < ntiles; t += (int64_t)gridDim.x * nw) {
     const int64_t c0 = t * COLS + (lane / G) * CPF;
     T x[V];
@@ -817,6 +820,9 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
     } else {
       for (int s = 0; s < a.nsteps; ++s) fwd_step(s, a.op[s]);
     }
+#if ENF_DIAG
+    if (STEP && a.diag_ts && !tsF) tsF = (long long)clock64();
+#endif
     T yfin[V];  // the flow's output (the last step's output for the backward's in-range forms)
 #pragma unroll
     for (int e = 0; e < V; ++e) yfin[e] = x[e];
@@ -833,6 +839,9 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
       }
       lossp += (double)part;
     }
+#if ENF_DIAG
+    if (STEP && a.diag_ts && !tsL) tsL = (long long)clock64();
+#endif
     // ---- backward: g = dS/dy = y (invalid columns carry g = 0 and contribute nothing); VJP: g = dY,
     // the ladj cotangent of each column dladj (0 when absent)
     T g[V], cl[CPF];
@@ -975,8 +984,9 @@ __device__ __forceinline__ void negll_grad_impl(const GradArgs& a, const ReduceA
         __syncthreads();
         const long long ts4 = (long long)clock64();
         if (tid == 0)
-          printf("ENF_SMALL_TS prologue %lld (loads %lld, v'v %lld, records %lld) tiles %lld partials %lld update %lld "
-                 "(shader clocks)\n", ts1 - ts0, tsA - ts0, tsB - tsA, ts1 - tsB, ts2 - ts1, ts3 - ts2, ts4 - ts3);
+          printf("ENF_SMALL_TS prologue %lld (loads %lld, v'v %lld, records %lld) tiles %lld (to fwd end %lld, loss %lld) "
+                 "partials %lld update %lld (shader clocks)\n", ts1 - ts0, tsA - ts0, tsB - tsA, ts1 - tsB, ts2 - ts1,
+                 tsF ? tsF - ts1 : 0, tsL ? tsL - tsF : 0, ts3 - ts2, ts4 - ts3);
       }
 #endif
       return;
